@@ -1,0 +1,168 @@
+"""ORACLE -- test infrastructure only.
+
+CPU (NumPy) restatement of the reference EKF localisation step
+(extended_kalman_filter.py) and of the EKF-SLAM extension named by
+BASELINE.json config 4.  Only tests/, __graft_entry__.smoke() and bench.py's
+cpu_baseline leg may use it.
+
+Pinned: ``EKFOracle`` reproduces tests/golden/ekf.npz (360 steps of the
+reference main_ekf, seed 3) bit-exactly on the fixture machine.
+``ekfslam_*`` has NO reference counterpart (the reference has no EKF-SLAM):
+parity for it is against this restatement only -- "parity unpinned" by the
+reference.  Its measurement model is the ScanSensor range/bearing/orientation
+model of graph_based_slam.py:150-153 with the covariance of :187-194.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from pf_oracle import HALF_PI, to_world_frame, wrap_angle
+
+
+class EKFParams:
+    """extended_kalman_filter.py:29-84."""
+
+    def __init__(self, period_ms=100):
+        self.dt = period_ms / 1000
+        self.omega = np.deg2rad(10.0)
+        self.vel = 10.0 * self.omega
+        self.c = np.array([[1.0, 0.0, 0.0], [0.0, 1.0, 0.0]])
+        self.q = np.diag([0.1, 0.1, np.deg2rad(0.1)]) ** 2
+        self.r = np.diag([1.0, 1.0]) ** 2
+        self.x0 = np.array([10.0, 0.0, np.deg2rad(90.0)])
+        self.p0 = np.diag([0.01, 0.01, np.deg2rad(30.0)]) ** 2
+
+
+def ekf_motion(x, dt, vel, omega):
+    """extended_kalman_filter.py:160-178 for one (3,) state."""
+    a = dt * np.cos(x[2])
+    b = dt * np.sin(x[2])
+    return np.array([x[0] + vel * a, x[1] + vel * b, wrap_angle(x[2] + omega * dt)])
+
+
+def ekf_jacobian(x, dt, vel):
+    """extended_kalman_filter.py:180-194."""
+    return np.array([[1.0, 0.0, -dt * vel * np.sin(x[2])],
+                     [0.0, 1.0, dt * vel * np.cos(x[2])],
+                     [0.0, 0.0, 1.0]])
+
+
+def ekf_update(x_hat, P, z, p: EKFParams, control=None):
+    """extended_kalman_filter.py:108-128.  Returns (x_hat_m, x_hat, P)."""
+    v, om = (p.vel, p.omega) if control is None else control
+    xm = ekf_motion(x_hat, p.dt, v, om).reshape(3, 1)
+    F = ekf_jacobian(x_hat, p.dt, v)
+    Pm = (F @ P @ F.T) + p.q
+    e = z.reshape(2, 1) - (p.c @ xm)
+    S = (p.c @ Pm @ p.c.T) + p.r
+    G = (Pm @ p.c.T) @ np.linalg.inv(S)
+    xh = xm + (G @ e)
+    xh[2, 0] = wrap_angle(xh[2, 0])
+    Pn = (np.identity(3) - G @ p.c) @ Pm
+    return xm[:, 0], xh[:, 0], Pn
+
+
+class EKFWorld:
+    """Truth / observation / dead reckoning of main_ekf (:97-106)."""
+
+    def __init__(self, p: EKFParams):
+        self.p = p
+        self.x_true = p.x0.copy()
+        self.x_dr = p.x0.copy()
+
+    def advance(self):
+        p = self.p
+        self.x_true = ekf_motion(self.x_true, p.dt, p.vel, p.omega)
+        w = np.random.multivariate_normal([0.0, 0.0], p.r, 1).T          # :100
+        y_l = (p.c @ np.array([[0.0], [0.0], [np.deg2rad(90.0)]])) + w     # :141-144
+        z = to_world_frame(self.x_true, y_l.T).T[:, 0]                     # :145-146
+        v = np.random.multivariate_normal([0.0, 0.0, 0.0], p.q, 1).T       # :105
+        self.x_dr = ekf_motion(self.x_dr, p.dt, p.vel, p.omega) + v[:, 0]
+        return z
+
+
+def run_reference_order(seed: int, steps: int, period_ms=100):
+    np.random.seed(seed)
+    p = EKFParams(period_ms)
+    world = EKFWorld(p)
+    x_hat, P = p.x0.copy(), p.p0.copy()
+    rows = []
+    for _ in range(steps):
+        z = world.advance()
+        xm, x_hat, P = ekf_update(x_hat, P, z, p)
+        rows.append(dict(x_true=world.x_true.copy(), x_dr=world.x_dr.copy(), z=z,
+                         x_hat_m=xm, P=P.copy(), x_hat=x_hat.copy()))
+    return rows
+
+
+# ------------------------------------------------------------- EKF-SLAM
+def scan_cov(dist, r_dist, r_dir, r_orient):
+    """graph_based_slam.py:187-194 measurement covariance (range, bearing, orientation)."""
+    d = dist * r_dist
+    return np.diag([d ** 2, (dist * np.sin(r_dir)) ** 2, r_dir ** 2 + r_orient ** 2])
+
+
+def scan_predict(xr, lm):
+    """graph_based_slam.py:150-153: landmark (x, y, phi) seen from pose xr ->
+    (range, bearing, orientation).  Orientation follows the sensor's
+    convention ``BASE_ANG - yaw`` plus the landmark's own heading phi."""
+    c, s = np.cos(HALF_PI - xr[2]), np.sin(HALF_PI - xr[2])
+    dx, dy = lm[0] - xr[0], lm[1] - xr[1]
+    rx = c * dx - s * dy
+    ry = s * dx + c * dy
+    return np.array([np.hypot(rx, ry), np.arctan2(ry, rx), wrap_angle(HALF_PI - xr[2] + lm[2])])
+
+
+def scan_jacobian(xr, lm):
+    """d(range, bearing, orientation) / d(robot x,y,yaw ; landmark x,y,phi)."""
+    dx, dy = lm[0] - xr[0], lm[1] - xr[1]
+    q = dx * dx + dy * dy
+    r = np.sqrt(q)
+    Hr = np.array([[-dx / r, -dy / r, 0.0],
+                   [dy / q, -dx / q, -1.0],
+                   [0.0, 0.0, -1.0]])
+    Hl = np.array([[dx / r, dy / r, 0.0],
+                   [-dy / q, dx / q, 0.0],
+                   [0.0, 0.0, 1.0]])
+    return Hr, Hl
+
+
+def ekfslam_step(mu, P, control, obs_ids, obs, dt, q_robot, noise):
+    """One EKF-SLAM predict + batched update.
+
+    mu (n,), P (n,n) with n = 3 + 3*NLM; robot motion = the reference EKF's
+    linear model (:160-194); ``obs`` (k,3) range/bearing/orientation of the
+    landmarks ``obs_ids``; ``noise`` = (r_dist, r_dir, r_orient).  The
+    update is P <- P - K S K^T with K = P H^T S^-1 (rank-3k)."""
+    v, om = control
+    n = mu.size
+    mu = mu.copy()
+    xr = mu[:3].copy()
+    F = ekf_jacobian(xr, dt, v)
+    mu[:3] = ekf_motion(xr, dt, v, om)
+    P = P.copy()
+    P[:3, :] = F @ P[:3, :]
+    P[:, :3] = P[:, :3] @ F.T
+    P[:3, :3] += q_robot
+    k = len(obs_ids)
+    H = np.zeros((3 * k, n))
+    innov = np.zeros(3 * k)
+    Rb = np.zeros((3 * k, 3 * k))
+    for t, (j, o) in enumerate(zip(obs_ids, obs)):
+        sl = slice(3 + 3 * j, 6 + 3 * j)
+        zhat = scan_predict(mu[:3], mu[sl])
+        Hr, Hl = scan_jacobian(mu[:3], mu[sl])
+        H[3 * t:3 * t + 3, :3] = Hr
+        H[3 * t:3 * t + 3, sl] = Hl
+        e = o - zhat
+        e[1] = wrap_angle(e[1])
+        e[2] = wrap_angle(e[2])
+        innov[3 * t:3 * t + 3] = e
+        Rb[3 * t:3 * t + 3, 3 * t:3 * t + 3] = scan_cov(o[0], *noise)
+    PHt = P @ H.T
+    S = H @ PHt + Rb
+    K = PHt @ np.linalg.inv(S)
+    mu = mu + K @ innov
+    mu[2] = wrap_angle(mu[2])
+    P = P - K @ S @ K.T
+    return mu, P

@@ -1,0 +1,286 @@
+"""Generate the golden fixtures under tests/golden/ from the REFERENCE itself.
+
+Runs only in the build container, where takuyani/SLAM-Robot_Simu is mounted
+read-only at /root/reference.  The reference is imported (never copied); its
+private methods are called through their name-mangled attributes and a few
+global functions are wrapped to observe values the reference keeps internal.
+Only data (inputs and outputs) is written.
+
+    PYTHONDONTWRITEBYTECODE=1 MPLBACKEND=Agg python tests/golden/make_golden.py
+
+One harness addition is unavoidable: particle_filter.py:191 calls
+``matplotlib.mlab.bivariate_normal``, removed in matplotlib 3.1.  The published
+formula is injected into ``matplotlib.mlab`` before the first step (nothing
+under /root/reference is modified).
+"""
+import os
+import sys
+import contextlib
+import io
+
+import numpy as np
+
+REF = os.environ.get("SLAM_REFERENCE", "/root/reference")
+OUT = os.path.dirname(os.path.abspath(__file__))
+sys.dont_write_bytecode = True
+os.environ.setdefault("MPLBACKEND", "Agg")
+sys.path.insert(0, REF)
+
+import matplotlib  # noqa: E402
+from matplotlib import mlab  # noqa: E402
+
+
+def _bivariate_normal(X, Y, sigmax=1.0, sigmay=1.0, mux=0.0, muy=0.0, sigmaxy=0.0):
+    xm, ym = X - mux, Y - muy
+    rho = sigmaxy / (sigmax * sigmay)
+    q = xm ** 2 / sigmax ** 2 + ym ** 2 / sigmay ** 2 - 2 * rho * xm * ym / (sigmax * sigmay)
+    den = 2 * np.pi * sigmax * sigmay * np.sqrt(1 - rho ** 2)
+    return np.exp(-q / (2 * (1 - rho ** 2))) / den
+
+
+mlab.bivariate_normal = _bivariate_normal
+
+
+def _quiet():
+    return contextlib.redirect_stdout(io.StringIO())
+
+
+# --------------------------------------------------------------- primitives
+def heavy_weights(rs, n, zero_frac=0.0):
+    """Deterministic heavy-tailed positive weights built with multiplications
+    only (bit-identical on every IEEE machine, so large inputs are stored as a
+    seed instead of as data)."""
+    u = rs.random_sample(n)
+    v = rs.random_sample(n)
+    w = u * u
+    w = w * w
+    w = w * w
+    w = w * w * v            # ~u**16 * v : spans many decades
+    if zero_frac > 0:
+        w[rs.random_sample(n) < zero_frac] = 0.0
+    return w
+
+
+def gen_units():
+    from mylib import limit, transform
+    rs = np.random.RandomState(1234)
+    ang = np.concatenate([
+        np.array([0.0, -0.0, np.pi, -np.pi, 3 * np.pi, -3 * np.pi, np.pi + 1e-12,
+                  -np.pi - 1e-12, 2 * np.pi, -2 * np.pi, 7.5, -7.5, 100.0, -100.0,
+                  1e-300, -1e-300, np.nextafter(np.pi, 10), np.nextafter(-np.pi, -10)]),
+        rs.uniform(-20, 20, 500)])
+    wrapped = np.array([limit.limit_angle(a) for a in ang])
+
+    poses = np.stack([rs.uniform(-20, 20, 64), rs.uniform(-20, 20, 64),
+                      rs.uniform(-4, 4, 64)], axis=1)
+    pts = rs.uniform(-15, 15, (64, 7, 2))
+    w2r = np.stack([transform.world2robot(p.reshape(3, 1), q) for p, q in zip(poses, pts)])
+    r2w = np.stack([transform.robot2world(p.reshape(3, 1), q) for p, q in zip(poses, pts)])
+
+    dx = np.concatenate([rs.normal(size=300) * 0.5, rs.normal(size=100) * 30, [0.0, 40.0, 1e3]])
+    dy = np.concatenate([rs.normal(size=300) * 0.5, rs.normal(size=100) * 30, [0.0, -40.0, 1e3]])
+    gauss = _bivariate_normal(dx, dy, 0.3, 0.3, 0.0, 0.0, 0.0)
+
+    sums = {}
+    for n in [1, 7, 8, 100, 128, 129, 500, 1000, 8192, 8193, 20000, 100003, 1 << 20]:
+        a = heavy_weights(np.random.RandomState(n), n)
+        sums[n] = float(np.sum(a.reshape(1, n)))
+    np.savez_compressed(
+        os.path.join(OUT, "units.npz"),
+        ang_in=ang, ang_out=wrapped, poses=poses, pts=pts, w2r=w2r, r2w=r2w,
+        gdx=dx, gdy=dy, gauss=gauss,
+        sum_sizes=np.array(list(sums)), sum_out=np.array([sums[n] for n in sums]))
+
+
+# ------------------------------------------------------- particle filter
+def _make_pf(pfm, n, lm):
+    with _quiet():
+        pf = pfm.ParticleFilter(100)
+    pf._ParticleFilter__NP = n
+    pf._ParticleFilter__NP_RECIP = 1 / n
+    pf._ParticleFilter__ESS_TH = n / 100.0
+    pf._ParticleFilter__LM = lm
+    x0 = pf._ParticleFilter__x_true
+    pf._ParticleFilter__px = np.tile(x0, (1, n))
+    pf._ParticleFilter__pw_ini = np.full((1, n), 1 / n)
+    pf._ParticleFilter__pw = np.full((1, n), 1 / n)
+    return pf
+
+
+class _RandRecorder:
+    def __init__(self):
+        self.real = np.random.rand
+        self.last = None
+
+    def __call__(self, *a):
+        v = self.real(*a)
+        self.last = v
+        return v
+
+
+def resample_tags(pfm, pf, pw, u, fn=None):
+    """Indices chosen by the reference __resampling for weights pw and rand()=u.
+    ``fn``: the unwrapped bound method when the instance attribute is wrapped."""
+    fn = fn or pf._ParticleFilter__resampling
+    n = pw.size
+    tags = np.tile(np.arange(n, dtype=np.float64), (3, 1))
+    saved, th = np.random.rand, pf._ParticleFilter__ESS_TH
+    np.random.rand = lambda *a: u
+    pf._ParticleFilter__ESS_TH = np.inf          # force the resampling branch
+    try:
+        px, _ = fn(tags, pw.reshape(1, n).copy())
+    finally:
+        np.random.rand = saved
+        pf._ParticleFilter__ESS_TH = th
+    return px[0].astype(np.int64)
+
+
+def gen_pf_c1(seed=0, n=500, nl=20, steps=1000):
+    """BASELINE config 1: 500 particles x 20 landmarks x 1000 steps, seed 0."""
+    import particle_filter as pfm
+    lm = np.random.RandomState(seed + 1).uniform(-10.0, 10.0, (nl, 2))
+    np.random.seed(seed)
+    pf = _make_pf(pfm, n, lm)
+    rec = _RandRecorder()
+    obs_log, res_log = [], []
+    orig_obs = pf._ParticleFilter__observation
+    orig_res = pf._ParticleFilter__resampling
+
+    def obs_wrap(x):
+        z = orig_obs(x)
+        obs_log.append(z.copy())
+        return z
+
+    def res_wrap(px, pw):
+        ess = float(np.reciprocal(pw @ pw.T)[0, 0])
+        rec.last = None
+        np.random.rand = rec
+        try:
+            px2, pw2 = orig_res(px, pw)
+        finally:
+            np.random.rand = rec.real
+        res_log.append((ess, rec.last, pw.copy()))
+        return px2, pw2
+
+    pf._ParticleFilter__observation = obs_wrap
+    pf._ParticleFilter__resampling = res_wrap
+    keep = set(range(20)) | set(range(49, steps, 50))
+    cols = {k: [] for k in ["x_true", "x_est", "max_idx", "max_val", "ess", "resampled", "u"]}
+    px_keep, pw_keep, keep_steps = [], [], []
+    idx_keep, idx_steps = [], []
+    for k in range(steps):
+        with _quiet():
+            _, xt, xe, px, _, mi, mv = pf.main_pf()
+        ess, u, pw_prev = res_log[-1]
+        cols["x_true"].append(xt[:, 0].copy())
+        cols["x_est"].append(xe[:, 0].copy())
+        cols["max_idx"].append(int(mi))
+        cols["max_val"].append(float(mv))
+        cols["ess"].append(ess)
+        cols["resampled"].append(u is not None)
+        cols["u"].append(np.nan if u is None else float(u))
+        if u is not None and len(idx_keep) < 12:
+            idx_keep.append(resample_tags(pfm, pf, pw_prev[0], u, fn=orig_res))
+            idx_steps.append(k)
+        if k in keep:
+            px_keep.append(px.copy())
+            pw_keep.append(pf._ParticleFilter__pw[0].copy())
+            keep_steps.append(k)
+    np.savez_compressed(
+        os.path.join(OUT, "pf_c1.npz"), seed=seed, n=n, lm=lm,
+        z=np.array(obs_log), **{k: np.array(v) for k, v in cols.items()},
+        px_keep=np.array(px_keep), pw_keep=np.array(pw_keep), keep_steps=np.array(keep_steps),
+        idx_keep=np.array(idx_keep), idx_steps=np.array(idx_steps))
+
+
+def gen_pf_stages(seed=7):
+    """Kernel-level vectors: __likelihood / __resampling / __predict of the
+    reference on synthetic particle sets (including underflowing weights)."""
+    import particle_filter as pfm
+    rs = np.random.RandomState(seed)
+    out = {}
+    for tag, n, nl, spread in [("a", 2000, 100, 0.6), ("b", 777, 20, 2.0), ("c", 4096, 5, 0.3)]:
+        lm = rs.uniform(-10.0, 10.0, (nl, 2))
+        pf = _make_pf(pfm, n, lm)
+        px = np.vstack([10 + rs.normal(size=n) * spread, rs.normal(size=n) * spread,
+                        np.pi / 2 + rs.normal(size=n) * spread * 0.3])
+        pw = rs.random_sample(n)
+        pw /= np.sum(pw)
+        if tag == "b":       # inconsistent observations: every product underflows
+            z = rs.uniform(-12, 12, (nl, 2))
+        else:                # observations of a pose inside the cloud
+            from mylib import transform
+            z = transform.world2robot(np.array([[10.1], [-0.1], [np.pi / 2 + 0.05]]), lm)
+            z = z + rs.normal(size=z.shape) * 0.3
+        lik = pf._ParticleFilter__likelihood(px.copy(), pw.reshape(1, n).copy(), z)
+        out.update({f"lik_{tag}_lm": lm, f"lik_{tag}_px": px, f"lik_{tag}_pw": pw,
+                    f"lik_{tag}_z": z, f"lik_{tag}_out": lik[0]})
+        # predict: reseed so the noise can be regenerated by the checker
+        np.random.seed(seed + 100)
+        pred = pf._ParticleFilter__predict(px.copy())
+        out.update({f"pred_{tag}_in": px, f"pred_{tag}_out": pred,
+                    f"pred_{tag}_seed": np.array(seed + 100)})
+    # resampling index sets on concentrated / flat / zero-heavy weights
+    for tag, n in [("r500", 500), ("r1000", 1000), ("r8193", 8193), ("r65536", 65536),
+                   ("r1m", 1 << 20)]:
+        pf = _make_pf(pfm, n, np.zeros((1, 2)))
+        wseed = 1000 + n
+        w = heavy_weights(np.random.RandomState(wseed), n,
+                          zero_frac=0.5 if tag in ("r8193", "r1m") else 0.0)
+        if tag in ("r8193", "r1m"):
+            w[:64] = 0.0
+        w = w / np.sum(w.reshape(1, n))
+        u = float(rs.random_sample())
+        idx = resample_tags(pfm, pf, w, u)
+        # indices are monotone: store them run-length encoded (exact)
+        vals, counts = np.unique(idx, return_counts=True)
+        out.update({f"{tag}_wseed": np.array(wseed), f"{tag}_u": np.array(u),
+                    f"{tag}_idx_vals": vals.astype(np.int32),
+                    f"{tag}_idx_counts": counts.astype(np.int32)})
+    np.savez_compressed(os.path.join(OUT, "pf_stages.npz"), **out)
+
+
+# ------------------------------------------------------------ motion model
+def gen_motion(seed=11):
+    import motion_model as mm
+    rs = np.random.RandomState(seed)
+    poses = np.stack([rs.uniform(-10, 10, 300), rs.uniform(-10, 10, 300),
+                      rs.uniform(-3, 3, 300)], axis=1)
+    cases = [(1.0, 0.05, 0.05, 0.01, 0.01, 0.01, 0.01, np.pi / 2, np.deg2rad(90.0)),
+             (0.1, 0.1, 0.1, 0.1, 0.1, 0.1, 0.1, 10 * np.deg2rad(10.0), np.deg2rad(10.0)),
+             (2.0, 0.1, 0.1, 0.1, 0.1, 0.1, 0.1, 10 * np.deg2rad(10.0), np.deg2rad(10.0))]
+    out = {"poses": poses}
+    for c, (dt, a1, a2, a3, a4, a5, a6, v, w) in enumerate(cases):
+        m = mm.MotionModel(dt, a1, a2, a3, a4, a5, a6)
+        np.random.seed(seed + c)
+        noisy = np.stack([m.moveWithNoise(p.reshape(3, 1), v, w)[:, 0] for p in poses])
+        clean = np.stack([m.moveWithoutNoise(p.reshape(3, 1), v, w)[:, 0] for p in poses])
+        out.update({f"case{c}": np.array([dt, a1, a2, a3, a4, a5, a6, v, w]),
+                    f"noisy{c}": noisy, f"clean{c}": clean, f"seed{c}": np.array(seed + c)})
+    np.savez_compressed(os.path.join(OUT, "motion.npz"), **out)
+
+
+# -------------------------------------------------------------------- EKF
+def gen_ekf(seed=3, steps=360):
+    import extended_kalman_filter as ekfm
+    np.random.seed(seed)
+    with _quiet():
+        ekf = ekfm.ExtendedKalmanFilter(100)
+    rows = {k: [] for k in ["x_true", "x_dr", "z", "x_hat_m", "P", "x_hat"]}
+    for _ in range(steps):
+        xt, xdr, z, xm, P = ekf.main_ekf()
+        rows["x_true"].append(xt[:, 0].copy())
+        rows["x_dr"].append(xdr[:, 0].copy())
+        rows["z"].append(z[:, 0].copy())
+        rows["x_hat_m"].append(xm[:, 0].copy())
+        rows["P"].append(P.copy())
+        rows["x_hat"].append(ekf._ExtendedKalmanFilter__x_hat[:, 0].copy())
+    np.savez_compressed(os.path.join(OUT, "ekf.npz"), seed=seed,
+                        **{k: np.array(v) for k, v in rows.items()})
+
+
+if __name__ == "__main__":
+    which = sys.argv[1:] or ["units", "pf_c1", "pf_stages", "motion", "ekf"]
+    for w in which:
+        print("generating", w, flush=True)
+        globals()["gen_" + w]()
