@@ -1,0 +1,122 @@
+/*
+ * slam_hip.h -- C-ABI of libslam_hip.so, the MI355X (gfx950) implementation of
+ * the per-step SLAM state-estimation hot path of takuyani/SLAM-Robot_Simu.
+ *
+ * The reference is pure Python/NumPy with no FFI of its own; these entry points
+ * are what a ctypes binding of its estimator classes binds.
+ * Every function below names the reference interface it replaces.
+ *
+ * Conventions
+ *   - Plain pointers and sizes only.  Host buffers are caller-owned and are only
+ *     read/written during the call; device memory is owned by the handle.
+ *   - Return 0 on success, a negative SLAM_ERR_* code on failure;
+ *     slam_last_error() (thread-local) describes the last failure.
+ *   - A handle is not thread-safe (the reference is single-threaded).
+ *   - All arithmetic is IEEE fp64, as in the reference.
+ */
+#ifndef SLAM_HIP_H
+#define SLAM_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SLAM_OK 0
+#define SLAM_ERR_ARG (-1)
+#define SLAM_ERR_HIP (-2)
+/* particle_filter.py:219: a resample position beyond the last cumulative
+ * weight raises IndexError in the reference; the device clamps to NP-1 and
+ * reports this code from the call that hit it. */
+#define SLAM_ERR_INDEX (-3)
+#define SLAM_ERR_STATE (-4)
+#define SLAM_ERR_COMM (-6)
+
+int slam_version(void);
+const char* slam_last_error(void);
+int slam_device_count(int* n);
+
+/* ====================================================================
+ * Particle filter -- replaces ParticleFilter (particle_filter.py:18-237)
+ * ==================================================================== */
+typedef struct slam_pf slam_pf;
+
+enum { SLAM_MOTION_LINEAR = 0,     /* particle_filter.py:121-142 (x' = A x + B u) + N(0,Q) */
+       SLAM_MOTION_VELOCITY = 1 }; /* motion_model.py:31-62 (sample_motion_model_velocity) */
+enum { SLAM_LIK_PRODUCT = 0,       /* particle_filter.py:185-192: sequential product of NL densities */
+       SLAM_LIK_LOGSUM = 1 };      /* same density as exp(-sum(q)/2) * den^-NL (one exp per particle) */
+
+typedef struct {
+    double dt;            /* particle_filter.py:30  DT_s = period_ms / 1000 */
+    double ess_threshold; /* particle_filter.py:33  ESS_TH = NP / 100 */
+    double r_cov[4];      /* particle_filter.py:68-70 R (2x2, row-major) */
+    double q_factor[9];   /* device-RNG noise map: noise_j = sum_k g_k q_factor[3k+j]
+                             (numpy: sqrt(s)[:,None]*v of svd(Q), particle_filter.py:165) */
+    double alphas[6];     /* motion_model.py:20-29 a1..a6 (velocity motion model) */
+    double x0[3];         /* particle_filter.py:74-81 initial pose of every particle */
+    uint64_t seed;        /* device RNG (Philox-4x32-10) key */
+    int32_t motion;       /* SLAM_MOTION_* */
+    int32_t likelihood;   /* SLAM_LIK_* */
+} slam_pf_config;
+
+typedef struct {
+    double x_est[3];      /* particle_filter.py:117  px[:, argmax] */
+    double cov[9];        /* weighted particle covariance (np.cov(px, aweights=pw, bias=True)) */
+    double max_val;       /* particle_filter.py:115 */
+    double ess;           /* 1 / sum(w^2) of the normalised weights after this step */
+    double weight_sum;    /* particle_filter.py:234 np.sum before normalisation */
+    int64_t max_idx;      /* particle_filter.py:116 (first index on ties) */
+    int32_t resampled;    /* this step ran the resampling branch (particle_filter.py:211) */
+    int32_t resample_next;/* ess < ESS_TH: the next step will resample */
+    int32_t status;       /* bit0: resample clamp (reference IndexError); bit1: exact-scan fallback */
+    int32_t n_special;    /* exact-cumsum diagnostics: sequentially folded elements */
+} slam_pf_result;
+
+/* ParticleFilter.__init__ (particle_filter.py:21-84).  landmarks: n_landmarks x 2 row-major. */
+int slam_pf_create(const slam_pf_config* cfg, int64_t n_particles, int32_t n_landmarks,
+                   const double* landmarks, int device, slam_pf** out);
+int slam_pf_destroy(slam_pf* h);
+int slam_pf_set_landmarks(slam_pf* h, const double* landmarks);
+/* Any pointer may be NULL (left unchanged).  Arrays of NP doubles. */
+int slam_pf_set_state(slam_pf* h, const double* x, const double* y, const double* th,
+                      const double* w);
+int slam_pf_get_state(slam_pf* h, double* x, double* y, double* th, double* w);
+
+/* One estimator step of main_pf (particle_filter.py:102-117):
+ * resampling (if the previous step's ESS < ESS_TH) -> predict -> likelihood ->
+ * normalise -> estimate.
+ *   control:  (v, omega)                         (particle_filter.py:46-58)
+ *   z:        NL x 2 robot-frame observations    (particle_filter.py:151-153)
+ *   noise:    NP x 3 host array or NULL.  LINEAR: additive (x, y, yaw) noise =
+ *             np.random.multivariate_normal(0, Q, NP) (particle_filter.py:165);
+ *             VELOCITY: standard normals in draw order (v, w, gamma) per particle
+ *             (motion_model.py:46-48).  NULL: on-device Philox stream.
+ *   u_resample: rand() of particle_filter.py:214 (ofs = u / NP); NaN: device RNG. */
+int slam_pf_step(slam_pf* h, const double* control, const double* z, const double* noise,
+                 double u_resample, slam_pf_result* res);
+
+/* Stage entry points (the reference's private methods). */
+int slam_pf_resample(slam_pf* h, double u_resample, int32_t force, int32_t* resampled);  /* __resampling :200-224 */
+int slam_pf_predict(slam_pf* h, const double* control, const double* noise);            /* __predict :156-168 */
+int slam_pf_update(slam_pf* h, const double* z, slam_pf_result* res);                    /* __likelihood + estimate :113-117 */
+/* Exact systematic-resampling indices for the CURRENT weights (idx_out: NP int64). */
+int slam_pf_resample_indices(slam_pf* h, double u_resample, int64_t* idx_out, int32_t* n_special);
+/* numpy-order np.sum of the current weights (particle_filter.py:234). */
+int slam_pf_weight_sum(slam_pf* h, double* sum_out);
+
+/* Device-resident multi-step run (bench path): observations for n_steps steps
+ * are uploaded once; steps are enqueued back to back with no host sync. */
+int slam_pf_load_observations(slam_pf* h, int32_t n_steps, const double* z_all);
+int slam_pf_run(slam_pf* h, int32_t first_step, int32_t n_steps, const double* controls,
+                slam_pf_result* results);
+
+/* Kernel timing (HIP events on the handle's stream). kernel: 0 = fused
+ * predict+likelihood, 1 = normalise, 2 = exact-cumsum+search, 3 = whole step. */
+int slam_pf_enable_timing(slam_pf* h, int32_t on);
+int slam_pf_timing(slam_pf* h, int32_t kernel, double* total_ms, int64_t* launches);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SLAM_HIP_H */

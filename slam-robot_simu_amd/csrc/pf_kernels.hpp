@@ -1,0 +1,71 @@
+// pf_kernels.hpp -- particle-filter kernel interfaces (device side).
+#pragma once
+#include "common.hpp"
+
+namespace slam {
+
+constexpr int kMotionNone = 2;     // internal: likelihood-only pass
+constexpr int kSumChunk = 8192;     // np.sum buffer size (particle_filter.py:234 order)
+constexpr int kScanBlock = 2048;    // elements per block of the exact-cumsum passes
+constexpr int kScanThreads = 256;
+constexpr int kScanPer = kScanBlock / kScanThreads;  // 8
+constexpr int kNormThreads = 256;
+constexpr int kNormBlocksMax = 1024;
+
+// particle_filter.py:179-181 + the mlab.bivariate_normal constants
+struct LikConst {
+    double sx2, sy2;        // sigmax**2, sigmay**2 (as numpy squares the sqrt)
+    double rsx2, rsy2;      // RN(1/sx2), RN(1/sy2) for the FMA-refined quotients
+    double rho2;            // 2*rho
+    double sxsy;            // sigmax*sigmay
+    double d2;              // 2*(1-rho**2)
+    double den, rden;       // 2*pi*sx*sy*sqrt(1-rho**2) and RN(1/den)
+    double neg_nl_ln_den;   // -NL*log(den) (log-sum form)
+    int32_t has_rho;
+    int32_t nl;
+};
+
+struct PredictConst {
+    double dt;
+    double v, om;           // control
+    double vdt_om;          // RN(om * dt)             (particle_filter.py:137 (B u)[2])
+    double sv, sw, sg;      // velocity-model stds = sigma**2 (motion_model.py:46-48)
+    double q[9];            // device-RNG noise map for the linear model
+    double np_recip;        // 1/NP (particle_filter.py:32)
+    int64_t n_global;       // global particle count (RNG counter space)
+    int64_t gbase;          // global index of local particle 0
+};
+
+struct BlockPartial {
+    double maxv;
+    int64_t maxi;
+    double sw, sw2;
+    double m1[3];
+    double m2[6];
+};
+
+struct SpecialIn {
+    int64_t idx;            // global element index
+    uint64_t P;             // inclusive prefix of the integer increments
+    double w;
+    int32_t E;              // binade of the run that follows
+    int32_t pad;
+};
+
+struct SpecialOut {
+    double cs;              // exact cumsum at the special element
+    uint64_t P;
+    int32_t E;
+    int32_t pad;
+};
+
+// device flag words
+enum : int {
+    kFlagResample = 0,      // resample at the start of the next step (ESS < ESS_TH)
+    kFlagStatus = 1,        // bit0 clamp (reference IndexError), bit1 scan fallback
+    kFlagNSpecial = 2,
+    kFlagFallback = 3,
+    kFlagWords = 8,
+};
+
+}  // namespace slam

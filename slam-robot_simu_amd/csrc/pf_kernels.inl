@@ -1,0 +1,640 @@
+// pf_kernels.hip -- gfx950 kernels of the particle-filter step.
+//
+// Step = [exact systematic resample] -> fused predict+likelihood ->
+//        numpy-order chunk sums -> normalise+reduce -> finalise.
+// Particles are SoA fp64 (x[], y[], th[]) in HBM, one particle per lane.
+#include "pf_kernels.hpp"
+
+namespace slam {
+
+// ====================================================================
+// wave / block helpers (wave = 64 lanes)
+// ====================================================================
+template <typename T>
+__device__ __forceinline__ T wave_incl_scan(T v) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        T o = __shfl_up(v, d, 64);
+        if (lane >= d) v = v + o;
+    }
+    return v;
+}
+
+// Exclusive block scan over NT threads; sh needs NT/64+1 entries.  Returns the
+// exclusive prefix of v, writes the block total to `total`.
+template <typename T, int NT>
+__device__ __forceinline__ T block_excl_scan(T v, T* sh, T& total) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const T inc = wave_incl_scan(v);
+    T ex = __shfl_up(inc, 1, 64);
+    if (lane == 0) ex = T(0);
+    if (lane == 63) sh[wid] = inc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        T run = T(0);
+        for (int k = 0; k < NT / 64; ++k) {
+            const T t = sh[k];
+            sh[k] = run;
+            run = run + t;
+        }
+        sh[NT / 64] = run;
+    }
+    __syncthreads();
+    const T r = sh[wid] + ex;
+    total = sh[NT / 64];
+    __syncthreads();
+    return r;
+}
+
+// FMA-refined quotient x/d with rd = RN(1/d): q0 = RN(x*rd), r = x - d*q0
+// (exact by FMA), q1 = RN(q0 + r*rd) -- the correctly rounded quotient for
+// normal operands (Markstein); checked against IEEE division in the tests.
+__device__ __forceinline__ double div_refined(double x, double d, double rd) {
+    const double q0 = x * rd;
+    const double r = fma(-q0, d, x);
+    return fma(r, rd, q0);
+}
+
+// ====================================================================
+// fused predict + likelihood     (particle_filter.py:156-198,
+//                                 motion_model.py:31-62)
+// ====================================================================
+template <int MOTION, int LIK, bool HOSTNOISE>
+__global__ __launch_bounds__(256) void pf_fused_kernel(
+    const int64_t n, const double* __restrict__ xs, const double* __restrict__ ys,
+    const double* __restrict__ ts, double* __restrict__ xo, double* __restrict__ yo,
+    double* __restrict__ to, const double* __restrict__ w_in, double* __restrict__ w_un,
+    const int32_t* __restrict__ idx, const int32_t* __restrict__ flags,
+    const double* __restrict__ noise, const double* __restrict__ lm,
+    const double* __restrict__ z, PredictConst pc, LikConst lc, uint64_t seed, uint32_t step) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const bool resampled = flags[kFlagResample] != 0;
+    const int64_t src = resampled ? (int64_t)idx[i] : i;
+    const double pw = resampled ? pc.np_recip : w_in[i];      // particle_filter.py:222
+    const double x = xs[src], y = ys[src], th = ts[src];
+
+    // ---- noise
+    double g0 = 0.0, g1 = 0.0, g2 = 0.0;
+    if (MOTION == kMotionNone) {
+    } else if (HOSTNOISE) {
+        g0 = noise[3 * i + 0];
+        g1 = noise[3 * i + 1];
+        g2 = noise[3 * i + 2];
+    } else {
+        const uint64_t gi = (uint64_t)(pc.gbase + i);
+        const u32x4 c0{(uint32_t)gi, (uint32_t)(gi >> 32), kStreamPredict, step};
+        const u32x4 r0 = philox4x32(c0, (uint32_t)seed, (uint32_t)(seed >> 32));
+        const u32x4 c1{(uint32_t)gi, (uint32_t)(gi >> 32), kStreamPredict | 0x100u, step};
+        const u32x4 r1 = philox4x32(c1, (uint32_t)seed, (uint32_t)(seed >> 32));
+        double h0, h1, h2, h3;
+        normal2(r0, h0, h1);
+        normal2(r1, h2, h3);
+        if (MOTION == SLAM_MOTION_LINEAR) {   // noise_j = sum_k g_k q[k][j]
+            g0 = h0 * pc.q[0] + h1 * pc.q[3] + h2 * pc.q[6];
+            g1 = h0 * pc.q[1] + h1 * pc.q[4] + h2 * pc.q[7];
+            g2 = h0 * pc.q[2] + h1 * pc.q[5] + h2 * pc.q[8];
+        } else {
+            g0 = h0;
+            g1 = h1;
+            g2 = h2;
+        }
+    }
+
+    // ---- predict
+    double xn, yn, tn;
+    if (MOTION == kMotionNone) {           // likelihood-only entry (particle_filter.py:170)
+        xn = x;
+        yn = y;
+        tn = th;
+    } else if (MOTION == SLAM_MOTION_LINEAR) {
+        // particle_filter.py:129-140 then + v (:166); A = I, B = diag(V, V, w)
+        const double a = pc.dt * cos(th);
+        const double b = pc.dt * sin(th);
+        xn = (x + pc.v * a) + g0;
+        yn = (y + pc.v * b) + g1;
+        tn = wrap_angle(th + pc.vdt_om) + g2;
+    } else {
+        // motion_model.py:46-56 (std handed to normal() is sigma**2)
+        const double vh = pc.v + (0.0 + pc.sv * g0);
+        const double wh = pc.om + (0.0 + pc.sw * g1);
+        const double gh = 0.0 + pc.sg * g2;
+        const double a = vh / wh;
+        const double b = wh * pc.dt;
+        double s0, c0, s1, c1;
+        sincos(th, &s0, &c0);
+        sincos(th + b, &s1, &c1);
+        xn = (x - (a * s0)) + (a * s1);
+        yn = (y + (a * c0)) - (a * c1);
+        tn = wrap_angle(th + (wh + gh) * pc.dt);
+    }
+    xo[i] = xn;
+    yo[i] = yn;
+    to[i] = tn;
+
+    // ---- likelihood: world2robot (mylib/transform.py:31-35) per landmark
+    double sp, cp;
+    sincos(kHalfPi - tn, &sp, &cp);
+    const double nsp = -sp;
+    double acc = 0.0;
+    const int nl = lc.nl;
+    for (int j = 0; j < nl; ++j) {
+        const double dxw = lm[2 * j] - xn;
+        const double dyw = lm[2 * j + 1] - yn;
+        // OpenBLAS dgemm order for (rot @ diff.T): fma(r01, d1, r00*d0)
+        const double rx = fma(nsp, dyw, cp * dxw);
+        const double ry = fma(cp, dyw, sp * dxw);
+        const double dx = rx - z[2 * j];
+        const double dy = ry - z[2 * j + 1];
+        double q = div_refined(dx * dx, lc.sx2, lc.rsx2) + div_refined(dy * dy, lc.sy2, lc.rsy2);
+        if (lc.has_rho) q = q - ((lc.rho2 * dx) * dy) / lc.sxsy;
+        if (LIK == SLAM_LIK_PRODUCT) {
+            const double e = lc.has_rho ? exp((-q) / lc.d2) : exp((-q) * 0.5);  // d2 == 2 exactly
+            const double f = div_refined(e, lc.den, lc.rden);
+            acc = (j == 0) ? f : acc * f;                     // ndarray.prod: left to right
+        } else {
+            acc = acc + q;
+        }
+    }
+    double bn;
+    if (LIK == SLAM_LIK_PRODUCT) bn = (nl > 0) ? acc : 1.0;
+    else bn = exp((-acc) / lc.d2 + lc.neg_nl_ln_den);
+    w_un[i] = pw * bn;                                           // particle_filter.py:194
+}
+
+// ====================================================================
+// numpy-order chunk sums (np.sum: 8192-element buffers, pairwise inside)
+// ====================================================================
+// Full chunk: 512 threads = 64 leaves x 8 accumulators; accumulator k of leaf
+// L sums elements L*128 + k + 8m (m = 0..15) left to right; leaves combine as
+// a perfect binary tree, which the xor-butterfly reproduces exactly.
+// Tail chunk (< 8192): host-built leaf table + post-order combine program.
+__global__ __launch_bounds__(512) void chunk_sum_kernel(
+    const double* __restrict__ w, const int64_t n, double* __restrict__ part,
+    const int32_t* __restrict__ tail_leaves, const int32_t* __restrict__ tail_ops,
+    const int32_t n_tail_leaves, const int32_t n_tail_ops) {
+    __shared__ double sh[512];
+    const int64_t base = (int64_t)blockIdx.x * kSumChunk;
+    const int64_t len = (n - base < kSumChunk) ? (n - base) : kSumChunk;
+    const int t = threadIdx.x;
+    if (len == kSumChunk) {
+        const int leaf = t >> 3, k = t & 7;
+        const double* p = w + base + leaf * 128 + k;
+        double r = p[0];
+#pragma unroll
+        for (int m = 1; m < 16; ++m) r = r + p[8 * m];
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) r = r + __shfl_xor(r, d, 64);
+        if ((t & 63) == 0) sh[t >> 6] = r;
+        __syncthreads();
+        if (t == 0) {
+            const double s = ((sh[0] + sh[1]) + (sh[2] + sh[3])) + ((sh[4] + sh[5]) + (sh[6] + sh[7]));
+            part[blockIdx.x] = s;
+        }
+        return;
+    }
+    // tail: leaves of <= 128 elements, one per thread
+    for (int L = t; L < n_tail_leaves; L += blockDim.x) {
+        const int lo = tail_leaves[2 * L], cnt = tail_leaves[2 * L + 1];
+        const double* a = w + base + lo;
+        double res;
+        if (cnt < 8) {
+            res = 0.0;
+            for (int i = 0; i < cnt; ++i) res = res + a[i];
+        } else {
+            double r[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) r[k] = a[k];
+            int i = 8;
+            const int stop = cnt - (cnt % 8);
+            for (; i < stop; i += 8) {
+#pragma unroll
+                for (int k = 0; k < 8; ++k) r[k] = r[k] + a[i + k];
+            }
+            res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+            for (; i < cnt; ++i) res = res + a[i];
+        }
+        sh[L] = res;
+    }
+    __syncthreads();
+    if (t == 0) {
+        double stk[16];
+        int sp = 0;
+        for (int o = 0; o < n_tail_ops; ++o) {
+            const int op = tail_ops[o];
+            if (op >= 0) {
+                stk[sp++] = sh[op];
+            } else {
+                const double b = stk[--sp];
+                const double a = stk[--sp];
+                stk[sp++] = a + b;
+            }
+        }
+        part[blockIdx.x] = stk[0];
+    }
+}
+
+// ====================================================================
+// normalise (particle_filter.py:226-237) + per-block reductions
+// ====================================================================
+__global__ __launch_bounds__(kNormThreads) void normalize_kernel(
+    const int64_t n, const double* __restrict__ w_un, double* __restrict__ w,
+    const double* __restrict__ part, const int32_t nchunks, const double np_recip,
+    const double* __restrict__ xs, const double* __restrict__ ys, const double* __restrict__ ts,
+    const double* __restrict__ refp, BlockPartial* __restrict__ bp, double* __restrict__ s_out,
+    const int64_t gbase) {
+    __shared__ double sh_s;
+    __shared__ BlockPartial shp[kNormThreads / 64];
+    if (threadIdx.x == 0) {
+        double s = 0.0;                       // buffer partials added left to right
+        for (int c = 0; c < nchunks; ++c) s = s + part[c];
+        sh_s = s;
+        if (blockIdx.x == 0) *s_out = s;
+    }
+    __syncthreads();
+    const double s = sh_s;
+    const double r0 = refp[0], r1 = refp[1], r2 = refp[2];
+    BlockPartial a;
+    a.maxv = -1.0;
+    a.maxi = INT64_MAX;
+    a.sw = a.sw2 = 0.0;
+    for (int k = 0; k < 3; ++k) a.m1[k] = 0.0;
+    for (int k = 0; k < 6; ++k) a.m2[k] = 0.0;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        double v = w_un[i] / s;
+        if (isnan(v)) v = np_recip;
+        w[i] = v;
+        if (v > a.maxv) {
+            a.maxv = v;
+            a.maxi = gbase + i;
+        }
+        a.sw += v;
+        a.sw2 += v * v;
+        const double d0 = xs[i] - r0, d1 = ys[i] - r1, d2 = ts[i] - r2;
+        a.m1[0] += v * d0;
+        a.m1[1] += v * d1;
+        a.m1[2] += v * d2;
+        a.m2[0] += v * d0 * d0;
+        a.m2[1] += v * d0 * d1;
+        a.m2[2] += v * d0 * d2;
+        a.m2[3] += v * d1 * d1;
+        a.m2[4] += v * d1 * d2;
+        a.m2[5] += v * d2 * d2;
+    }
+    // wave reduction
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+        const double ov = __shfl_xor(a.maxv, d, 64);
+        const int64_t oi = __shfl_xor(a.maxi, d, 64);
+        if (ov > a.maxv || (ov == a.maxv && oi < a.maxi)) {
+            a.maxv = ov;
+            a.maxi = oi;
+        }
+        a.sw += __shfl_xor(a.sw, d, 64);
+        a.sw2 += __shfl_xor(a.sw2, d, 64);
+        for (int k = 0; k < 3; ++k) a.m1[k] += __shfl_xor(a.m1[k], d, 64);
+        for (int k = 0; k < 6; ++k) a.m2[k] += __shfl_xor(a.m2[k], d, 64);
+    }
+    if ((threadIdx.x & 63) == 0) shp[threadIdx.x >> 6] = a;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        BlockPartial r = shp[0];
+        for (int k = 1; k < kNormThreads / 64; ++k) {
+            const BlockPartial& o = shp[k];
+            if (o.maxv > r.maxv || (o.maxv == r.maxv && o.maxi < r.maxi)) {
+                r.maxv = o.maxv;
+                r.maxi = o.maxi;
+            }
+            r.sw += o.sw;
+            r.sw2 += o.sw2;
+            for (int q = 0; q < 3; ++q) r.m1[q] += o.m1[q];
+            for (int q = 0; q < 6; ++q) r.m2[q] += o.m2[q];
+        }
+        bp[blockIdx.x] = r;
+    }
+}
+
+// combine BlockPartials (fixed order) -> result record; sets the resample flag
+__device__ void combine_partials(const BlockPartial* bp, int nb, BlockPartial& r) {
+    r = bp[0];
+    for (int k = 1; k < nb; ++k) {
+        const BlockPartial& o = bp[k];
+        if (o.maxv > r.maxv || (o.maxv == r.maxv && o.maxi < r.maxi)) {
+            r.maxv = o.maxv;
+            r.maxi = o.maxi;
+        }
+        r.sw += o.sw;
+        r.sw2 += o.sw2;
+        for (int q = 0; q < 3; ++q) r.m1[q] += o.m1[q];
+        for (int q = 0; q < 6; ++q) r.m2[q] += o.m2[q];
+    }
+}
+
+__global__ void finalize_kernel(const BlockPartial* __restrict__ bp, const int32_t nb,
+                                const double* __restrict__ xs, const double* __restrict__ ys,
+                                const double* __restrict__ ts, double* __restrict__ refp,
+                                const double* __restrict__ s_in, int32_t* __restrict__ flags,
+                                const double ess_th, slam_pf_result* __restrict__ res,
+                                const int32_t resampled_known) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    BlockPartial r;
+    combine_partials(bp, nb, r);
+    slam_pf_result o;
+    const int64_t mi = r.maxi;
+    o.max_idx = mi;
+    o.max_val = r.maxv;
+    o.x_est[0] = xs[mi];
+    o.x_est[1] = ys[mi];
+    o.x_est[2] = ts[mi];
+    const double inv = 1.0 / r.sw;
+    const double mu[3] = {r.m1[0] * inv, r.m1[1] * inv, r.m1[2] * inv};
+    const double m2[9] = {r.m2[0], r.m2[1], r.m2[2], r.m2[1], r.m2[3], r.m2[4], r.m2[2], r.m2[4], r.m2[5]};
+    for (int a = 0; a < 3; ++a)
+        for (int b = 0; b < 3; ++b) o.cov[3 * a + b] = m2[3 * a + b] * inv - mu[a] * mu[b];
+    o.ess = 1.0 / r.sw2;
+    o.weight_sum = *s_in;
+    o.resampled = resampled_known >= 0 ? resampled_known : flags[kFlagResample];
+    o.resample_next = (o.ess < ess_th) ? 1 : 0;
+    o.status = flags[kFlagStatus];
+    o.n_special = flags[kFlagNSpecial];
+    flags[kFlagResample] = o.resample_next;
+    flags[kFlagStatus] = 0;
+    refp[0] = o.x_est[0];
+    refp[1] = o.x_est[1];
+    refp[2] = o.x_est[2];
+    *res = o;
+}
+
+// ====================================================================
+// exact sequential cumsum (np.cumsum, particle_filter.py:212)
+// ====================================================================
+// S1: approximate block totals
+__global__ __launch_bounds__(kScanThreads) void scan_bsum_kernel(
+    const double* __restrict__ w, const int64_t n, double* __restrict__ bsum,
+    const int32_t* __restrict__ flags, const int32_t force) {
+    if (!force && flags[kFlagResample] == 0) return;
+    __shared__ double sh[kScanThreads / 64 + 1];
+    const int64_t base = (int64_t)blockIdx.x * kScanBlock + threadIdx.x * kScanPer;
+    double s = 0.0;
+#pragma unroll
+    for (int k = 0; k < kScanPer; ++k)
+        if (base + k < n) s += w[base + k];
+    double tot;
+    block_excl_scan<double, kScanThreads>(s, sh, tot);
+    if (threadIdx.x == 0) bsum[blockIdx.x] = tot;
+}
+
+// S2/S4: single-block exclusive scan of per-block values
+template <typename T>
+__global__ __launch_bounds__(1024) void scan_top_kernel(const T* __restrict__ in, T* __restrict__ out,
+                                                        const int32_t nb, T* __restrict__ total,
+                                                        const int32_t* __restrict__ flags,
+                                                        const int32_t force) {
+    if (!force && flags[kFlagResample] == 0) return;
+    __shared__ T sh[1024 / 64 + 1];
+    const int per = (nb + 1023) / 1024;
+    const int b0 = threadIdx.x * per;
+    T loc = T(0);
+    for (int k = 0; k < per; ++k)
+        if (b0 + k < nb) loc = loc + in[b0 + k];
+    T tot;
+    T ex = block_excl_scan<T, 1024>(loc, sh, tot);
+    for (int k = 0; k < per; ++k)
+        if (b0 + k < nb) {
+            const T v = in[b0 + k];
+            out[b0 + k] = ex;
+            ex = ex + v;
+        }
+    if (threadIdx.x == 0 && total) *total = tot;
+}
+
+// S3: classify every element; k_i = increment on the run's ulp grid
+__global__ __launch_bounds__(kScanThreads) void scan_classify_kernel(
+    const double* __restrict__ w, const int64_t n, const double* __restrict__ boff,
+    double* __restrict__ approx, uint64_t* __restrict__ kincl, int32_t* __restrict__ fexcl,
+    uint64_t* __restrict__ bk, int32_t* __restrict__ bf, const double delta, const int64_t gbase,
+    const int32_t* __restrict__ flags, const int32_t force) {
+    if (!force && flags[kFlagResample] == 0) return;
+    __shared__ double shd[kScanThreads / 64 + 1];
+    __shared__ uint64_t shk[kScanThreads / 64 + 1];
+    __shared__ int32_t shf[kScanThreads / 64 + 1];
+    const int64_t base = (int64_t)blockIdx.x * kScanBlock + threadIdx.x * kScanPer;
+    double v[kScanPer];
+    double loc = 0.0;
+#pragma unroll
+    for (int k = 0; k < kScanPer; ++k) {
+        v[k] = (base + k < n) ? w[base + k] : 0.0;
+        loc += v[k];
+    }
+    double dtot;
+    double run = block_excl_scan<double, kScanThreads>(loc, shd, dtot) + boff[blockIdx.x];
+    uint64_t kk[kScanPer];
+    int32_t ff[kScanPer];
+    uint64_t ksum = 0;
+    int32_t fsum = 0;
+#pragma unroll
+    for (int k = 0; k < kScanPer; ++k) {
+        const double prev = run;
+        run = run + v[k];
+        const int64_t gi = gbase + base + k;
+        bool reg = (gi != 0) && (base + k < n);
+        uint64_t inc = 0;
+        if (reg) {
+            const int E = sum_binade(run);
+            reg = (sum_binade(prev) == E);
+            if (reg && E != -1022) reg = prev >= ldexp(1.0, E) * (1.0 + delta);
+            if (reg) reg = run <= ldexp(1.0, E + 1) * (1.0 - delta);
+            if (reg) {
+                const double t = ldexp(v[k], 52 - E);
+                const double fl = floor(t);
+                reg = (t - fl) != 0.5;
+                inc = (uint64_t)rint(t);
+            }
+        }
+        kk[k] = reg ? inc : 0;
+        ff[k] = (reg || base + k >= n) ? 0 : 1;
+        ksum += kk[k];
+        fsum += ff[k];
+        if (base + k < n) approx[base + k] = run;
+    }
+    uint64_t ktot;
+    int32_t ftot;
+    uint64_t kex = block_excl_scan<uint64_t, kScanThreads>(ksum, shk, ktot);
+    int32_t fex = block_excl_scan<int32_t, kScanThreads>(fsum, shf, ftot);
+#pragma unroll
+    for (int k = 0; k < kScanPer; ++k) {
+        if (base + k < n) {
+            kex += kk[k];
+            kincl[base + k] = kex;
+            fexcl[base + k] = (fex << 1) | ff[k];
+            fex += ff[k];
+        }
+    }
+    if (threadIdx.x == 0) {
+        bk[blockIdx.x] = ktot;
+        bf[blockIdx.x] = ftot;
+    }
+}
+
+// S5: scatter the special elements into an ordered list
+__global__ __launch_bounds__(kScanThreads) void scan_emit_kernel(
+    const double* __restrict__ w, const int64_t n, const double* __restrict__ approx,
+    const uint64_t* __restrict__ kincl, const int32_t* __restrict__ fexcl,
+    const uint64_t* __restrict__ boffk, const int32_t* __restrict__ bofff,
+    SpecialIn* __restrict__ spec, const int64_t gbase, const int32_t* __restrict__ flags,
+    const int32_t force) {
+    if (!force && flags[kFlagResample] == 0) return;
+    const int64_t base = (int64_t)blockIdx.x * kScanBlock + threadIdx.x * kScanPer;
+    for (int k = 0; k < kScanPer; ++k) {
+        const int64_t i = base + k;
+        if (i >= n) break;
+        const int32_t f = fexcl[i];
+        if (f & 1) {
+            const int32_t m = bofff[blockIdx.x] + (f >> 1);
+            SpecialIn s;
+            s.idx = gbase + i;
+            s.P = boffk[blockIdx.x] + kincl[i];
+            s.w = w[i];
+            s.E = sum_binade(approx[i]);
+            s.pad = 0;
+            spec[m] = s;
+        }
+    }
+}
+
+// S6: sequential fold over the special elements (one block, tiles in LDS).
+// Falls back to a fully sequential cumsum if a run check fails.
+__global__ __launch_bounds__(256) void scan_serial_kernel(
+    const SpecialIn* __restrict__ spec, SpecialOut* __restrict__ out,
+    const int32_t* __restrict__ nspec_p, const uint64_t* __restrict__ ktotal_p,
+    const int64_t n_total, const double s_start, int32_t* __restrict__ flags,
+    const double* __restrict__ w, double* __restrict__ c, const int64_t n_local,
+    const int32_t force) {
+    if (!force && flags[kFlagResample] == 0) return;
+    __shared__ SpecialIn tile[257];
+    __shared__ int bad;
+    const int32_t M = *nspec_p;
+    const uint64_t ktot = *ktotal_p;
+    double s = s_start;
+    if (threadIdx.x == 0) {
+        bad = 0;
+        flags[kFlagNSpecial] = M;
+    }
+    for (int32_t t0 = 0; t0 < M; t0 += 256) {
+        __syncthreads();
+        const int32_t cnt = min(257, M - t0);
+        for (int k = threadIdx.x; k < cnt; k += blockDim.x) tile[k] = spec[t0 + k];
+        __syncthreads();
+        if (threadIdx.x == 0 && !bad) {
+            const int lim = min(256, M - t0);
+            for (int k = 0; k < lim; ++k) {
+                const SpecialIn& e = tile[k];
+                s = s + e.w;
+                SpecialOut o;
+                o.cs = s;
+                o.P = e.P;
+                o.E = e.E;
+                o.pad = 0;
+                const bool last = (t0 + k + 1 >= M);
+                const int64_t nxt = last ? n_total : tile[k + 1].idx;
+                if (nxt - e.idx > 1) {
+                    const uint64_t K = (last ? ktot : tile[k + 1].P) - e.P;
+                    const int E = e.E;
+                    if (sum_binade(s) != E) { bad = 1; break; }
+                    const double s2 = s + (double)K * ldexp(1.0, E - 52);
+                    const double hi = (E == -1022) ? 0x1p-1021 : ldexp(1.0, E + 1);
+                    if (!(s2 < hi) || (double)K >= 0x1p53) { bad = 1; break; }
+                    s = s2;
+                }
+                out[t0 + k] = o;
+            }
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0 && bad) {
+        // exact fallback: the plain sequential recurrence
+        flags[kFlagStatus] |= 2;
+        flags[kFlagFallback] = 1;
+        double r = s_start;
+        for (int64_t i = 0; i < n_local; ++i) {
+            r = r + w[i];
+            c[i] = r;
+        }
+    } else if (threadIdx.x == 0) {
+        flags[kFlagFallback] = 0;
+    }
+}
+
+// S7: expand the exact cumsum from the specials
+__global__ __launch_bounds__(kScanThreads) void scan_expand_kernel(
+    const int64_t n, const uint64_t* __restrict__ kincl, const int32_t* __restrict__ fexcl,
+    const uint64_t* __restrict__ boffk, const int32_t* __restrict__ bofff,
+    const SpecialOut* __restrict__ so, double* __restrict__ c, const int32_t* __restrict__ flags,
+    const int32_t force) {
+    if (!force && flags[kFlagResample] == 0) return;
+    if (flags[kFlagFallback]) return;
+    const int64_t base = (int64_t)blockIdx.x * kScanBlock + threadIdx.x * kScanPer;
+    const uint64_t bko = boffk[blockIdx.x];
+    const int32_t bfo = bofff[blockIdx.x];
+#pragma unroll
+    for (int k = 0; k < kScanPer; ++k) {
+        const int64_t i = base + k;
+        if (i >= n) break;
+        const int32_t f = fexcl[i];
+        const int32_t m = bfo + (f >> 1);
+        if (f & 1) {
+            c[i] = so[m].cs;
+        } else {
+            const SpecialOut& p = so[m - 1];
+            const uint64_t K = bko + kincl[i] - p.P;
+            c[i] = p.cs + (double)K * ldexp(1.0, p.E - 52);
+        }
+    }
+}
+
+// gather for the stand-alone resampling stage (particle_filter.py:216-222)
+__global__ __launch_bounds__(256) void gather_kernel(
+    const int64_t n, const int32_t* __restrict__ idx, const double* __restrict__ xs,
+    const double* __restrict__ ys, const double* __restrict__ ts, double* __restrict__ xo,
+    double* __restrict__ yo, double* __restrict__ to, double* __restrict__ w, const double np_recip) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int64_t j = idx[i];
+    xo[i] = xs[j];
+    yo[i] = ys[j];
+    to[i] = ts[j];
+    w[i] = np_recip;
+}
+
+// S8: systematic positions + lower_bound (particle_filter.py:213-221)
+__global__ __launch_bounds__(256) void resample_search_kernel(
+    const int64_t n, const double* __restrict__ c, int32_t* __restrict__ idx, const double step,
+    const double ofs_host, const double np_recip, const uint64_t seed, const uint32_t stepno,
+    int32_t* __restrict__ flags, const int32_t force) {
+    if (!force && flags[kFlagResample] == 0) return;
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    double ofs = ofs_host;
+    if (isnan(ofs)) {
+        const u32x4 ctr{0u, 0u, kStreamResample, stepno};
+        const u32x4 r = philox4x32(ctr, (uint32_t)seed, (uint32_t)(seed >> 32));
+        const uint64_t m = ((uint64_t)(r.x >> 5) << 26) | (uint64_t)(r.y >> 6);
+        ofs = ((double)m * 0x1p-53) * np_recip;              // rand() * NP_RECIP
+    }
+    const double pos = (double)i * step + ofs;               // arange value + ofs
+    int64_t lo = 0, hi = n;                                   // first j with c[j] >= pos
+    while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        if (c[mid] < pos) lo = mid + 1;
+        else hi = mid;
+    }
+    if (lo >= n) {
+        lo = n - 1;
+        atomicOr(&flags[kFlagStatus], 1);
+    }
+    idx[i] = (int32_t)lo;
+}
+
+}  // namespace slam

@@ -1,0 +1,103 @@
+"""Drop-in ParticleFilter backed by the MI355X kernels (libslam_hip.so).
+
+Same constructor and ``main_pf()`` contract as the reference
+(particle_filter.py:21 / :86-119), plus ``step(control, observations)`` that
+returns the estimate and the weighted particle covariance.  The estimator
+(resample -> predict -> likelihood -> normalise -> argmax) runs on the GPU;
+this module only simulates the ground truth and the landmark observation, as
+the reference does on its side of main_pf (:100, :110).
+
+Noise streams
+  noise="numpy" (default): the host draws from NumPy's global RNG in the
+      reference's order -- [rand() if resampling] -> mvn(0, Q, NP) ->
+      observation noise -- so a seeded run reproduces the reference's
+      trajectory (tests/test_gpu_pf.py).
+  noise="device": Philox-4x32-10 on the GPU (no per-step host->device
+      noise traffic); statistically equivalent, not stream-identical.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from mylib import limit
+from mylib import transform as tf
+from slamhip.pf import DeviceParticleFilter
+
+DEFAULT_LANDMARKS = np.array([[5.0, 5.0], [2.0, -3.0], [-3.0, 4.0], [-5.0, -1.0], [0.0, 0.0]])
+
+
+class ParticleFilter(object):
+    """Monte-Carlo localisation against a known landmark map (GPU)."""
+
+    def __init__(self, period_ms, *, n_particles=1000, landmarks=None, noise="numpy",
+                 motion="linear", likelihood="product", alphas=(0.1,) * 6, seed=0, device=0):
+        self.period_ms = period_ms
+        self.dt = period_ms / 1000                                 # :30
+        self.n_particles = int(n_particles)                        # :31
+        self.lm = DEFAULT_LANDMARKS.copy() if landmarks is None else np.asarray(landmarks, float)
+        self.radius = 10.0                                         # :46
+        self.yaw_rate = np.deg2rad(10.0)                           # :47
+        self.vel = self.radius * self.yaw_rate                     # :48
+        self.Q = np.diag([0.03, 0.03, np.deg2rad(2.0)]) ** 2        # :62-65
+        self.R = np.diag([0.3, 0.3]) ** 2                          # :68-70
+        self.x_true = np.array([[self.radius], [0.0], [np.deg2rad(90.0)]])   # :74-79
+        if noise not in ("numpy", "device"):
+            raise ValueError("noise must be 'numpy' or 'device'")
+        self.noise = noise
+        self.motion = motion
+        self.alphas = tuple(alphas)
+        self.dev = DeviceParticleFilter(
+            self.n_particles, self.lm, dt=self.dt, q=self.Q, r=self.R, x0=self.x_true[:, 0],
+            motion=motion, likelihood=likelihood, alphas=alphas, seed=seed, device=device)
+
+    # ------------------------------------------------------------- world
+    def _truth_step(self, x):
+        """Ground-truth motion: particle_filter.py:121-142 for one column
+        (linear model) or motion_model.py:64-86 (velocity model)."""
+        yaw = x[2, 0]
+        if self.motion == "linear":
+            a = self.dt * np.cos(yaw)
+            b = self.dt * np.sin(yaw)
+            return np.array([[x[0, 0] + self.vel * a], [x[1, 0] + self.vel * b],
+                             [limit.limit_angle(yaw + self.yaw_rate * self.dt)]])
+        r = self.vel / self.yaw_rate
+        turn = limit.limit_angle(self.yaw_rate * self.dt)
+        yaw2 = limit.limit_angle(yaw + turn)
+        return np.array([[x[0, 0] + r * (-np.sin(yaw) + np.sin(yaw2))],
+                         [x[1, 0] + r * (np.cos(yaw) - np.cos(yaw2))], [yaw2]])
+
+    def _observe(self, x_true):
+        """particle_filter.py:144-154: landmarks in the robot frame + N(0, R)."""
+        z = tf.world2robot(x_true, self.lm)
+        return z + np.random.multivariate_normal([0.0, 0.0], self.R, z.shape[0])
+
+    def _draw_noise(self):
+        n = self.n_particles
+        if self.motion == "linear":
+            return np.random.multivariate_normal([0.0, 0.0, 0.0], self.Q, n)   # :165
+        return np.random.standard_normal(3 * n).reshape(n, 3)                 # motion_model.py:46-48
+
+    # --------------------------------------------------------- interface
+    def step(self, control, observations, noise=None, u_resample=float("nan")):
+        """One estimator step -> (pose (3,1), covariance (3,3))."""
+        out = self.dev.step(control, observations, noise, u_resample)
+        return out["x_est"].reshape(3, 1), out["cov"]
+
+    def main_pf(self):
+        """particle_filter.py:86-119 -> (LM, x_true, x_est, px, Q, max_idx, max_val)."""
+        self.x_true = self._truth_step(self.x_true)
+        if self.noise == "numpy":
+            u = np.random.rand() if self.dev.resample_next else float("nan")
+            noise = self._draw_noise()
+        else:
+            u, noise = float("nan"), None
+        z = self._observe(self.x_true)
+        out = self.dev.step((self.vel, self.yaw_rate), z, noise, u)
+        x, y, th, _ = self.dev.get_state()
+        px = np.vstack([x, y, th])
+        return (self.lm, self.x_true, out["x_est"].reshape(3, 1), px, self.Q,
+                out["max_idx"], out["max_val"])
+
+    @property
+    def weights(self):
+        return self.dev.get_state()[3]

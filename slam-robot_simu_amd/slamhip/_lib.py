@@ -1,0 +1,111 @@
+"""ctypes binding of libslam_hip.so (include/slam_hip.h).
+
+The shared library is built in-tree (``make -C slam-robot_simu_amd``) and is
+the only compute path: there is no CPU fallback.  Loading fails loudly when the
+library is missing, and every entry point raises on a non-zero return code.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libslam_hip.so")
+
+SLAM_OK = 0
+SLAM_ERR_ARG = -1
+SLAM_ERR_HIP = -2
+SLAM_ERR_INDEX = -3
+SLAM_ERR_STATE = -4
+SLAM_ERR_COMM = -6
+
+MOTION = {"linear": 0, "velocity": 1}
+LIKELIHOOD = {"product": 0, "logsum": 1}
+
+
+class PFConfig(C.Structure):
+    _fields_ = [("dt", C.c_double), ("ess_threshold", C.c_double), ("r_cov", C.c_double * 4),
+                ("q_factor", C.c_double * 9), ("alphas", C.c_double * 6), ("x0", C.c_double * 3),
+                ("seed", C.c_uint64), ("motion", C.c_int32), ("likelihood", C.c_int32)]
+
+
+class PFResult(C.Structure):
+    _fields_ = [("x_est", C.c_double * 3), ("cov", C.c_double * 9), ("max_val", C.c_double),
+                ("ess", C.c_double), ("weight_sum", C.c_double), ("max_idx", C.c_int64),
+                ("resampled", C.c_int32), ("resample_next", C.c_int32), ("status", C.c_int32),
+                ("n_special", C.c_int32)]
+
+
+_P = C.c_void_p
+_D = C.POINTER(C.c_double)
+_I64 = C.POINTER(C.c_int64)
+_I32 = C.POINTER(C.c_int32)
+
+# name -> (restype, argtypes)
+SIGNATURES = {
+    "slam_version": (C.c_int, []),
+    "slam_last_error": (C.c_char_p, []),
+    "slam_device_count": (C.c_int, [C.POINTER(C.c_int)]),
+    "slam_pf_create": (C.c_int, [C.POINTER(PFConfig), C.c_int64, C.c_int32, _D, C.c_int,
+                                 C.POINTER(_P)]),
+    "slam_pf_destroy": (C.c_int, [_P]),
+    "slam_pf_set_landmarks": (C.c_int, [_P, _D]),
+    "slam_pf_set_state": (C.c_int, [_P, _D, _D, _D, _D]),
+    "slam_pf_get_state": (C.c_int, [_P, _D, _D, _D, _D]),
+    "slam_pf_step": (C.c_int, [_P, _D, _D, _D, C.c_double, C.POINTER(PFResult)]),
+    "slam_pf_resample": (C.c_int, [_P, C.c_double, C.c_int32, _I32]),
+    "slam_pf_predict": (C.c_int, [_P, _D, _D]),
+    "slam_pf_update": (C.c_int, [_P, _D, C.POINTER(PFResult)]),
+    "slam_pf_resample_indices": (C.c_int, [_P, C.c_double, _I64, _I32]),
+    "slam_pf_weight_sum": (C.c_int, [_P, _D]),
+    "slam_pf_load_observations": (C.c_int, [_P, C.c_int32, _D]),
+    "slam_pf_run": (C.c_int, [_P, C.c_int32, C.c_int32, _D, C.POINTER(PFResult)]),
+    "slam_pf_enable_timing": (C.c_int, [_P, C.c_int32]),
+    "slam_pf_timing": (C.c_int, [_P, C.c_int32, _D, _I64]),
+}
+
+_lib = None
+
+
+class SlamError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"{msg} (code {code})")
+        self.code = code
+
+
+def load():
+    """Load libslam_hip.so (raises if it has not been built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"{LIB_PATH} not found: build it with `make -C slam-robot_simu_amd` "
+                          "(there is no CPU fallback)")
+    lib = C.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        f = getattr(lib, name)
+        f.restype = res
+        f.argtypes = args
+    _lib = lib
+    return lib
+
+
+def check(rc, what=""):
+    if rc != SLAM_OK:
+        msg = load().slam_last_error().decode(errors="replace")
+        if rc == SLAM_ERR_INDEX:
+            raise IndexError(msg)
+        raise SlamError(rc, f"{what}: {msg}" if what else msg)
+
+
+def device_count() -> int:
+    n = C.c_int(0)
+    check(load().slam_device_count(C.byref(n)), "slam_device_count")
+    return n.value
+
+
+def dptr(a):
+    """Pointer to a C-contiguous float64 numpy array (or NULL for None)."""
+    if a is None:
+        return None
+    return a.ctypes.data_as(_D)

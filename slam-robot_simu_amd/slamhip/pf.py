@@ -1,0 +1,180 @@
+"""Device particle filter: a handle on libslam_hip's slam_pf_* entry points.
+
+State lives in HBM as SoA fp64 arrays; this class only moves control,
+observations and (in NumPy-stream mode) noise across the boundary.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import _lib
+from ._lib import PFConfig, PFResult, check, dptr
+
+
+def _f64(a, shape=None):
+    a = np.ascontiguousarray(a, dtype=np.float64)
+    if shape is not None and a.shape != shape:
+        a = a.reshape(shape)
+    return a
+
+
+def numpy_noise_factor(q):
+    """The matrix numpy.random.multivariate_normal applies to standard
+    normals: sqrt(s)[:, None] * v of svd(Q) (used by the device RNG so that
+    its noise has the reference's covariance)."""
+    _, s, v = np.linalg.svd(np.asarray(q, dtype=np.float64))
+    return np.sqrt(s)[:, None] * v
+
+
+class DeviceParticleFilter:
+    """Particles on one GPU.  Parameters mirror particle_filter.py:21-84."""
+
+    def __init__(self, n_particles, landmarks, *, dt=0.1, q=None, r=None, x0=(10.0, 0.0, np.pi / 2),
+                 motion="linear", likelihood="product", alphas=(0.1,) * 6, ess_threshold=None,
+                 seed=0, device=0):
+        lib = _lib.load()
+        self.n = int(n_particles)
+        self.lm = _f64(landmarks).reshape(-1, 2)
+        self.nl = self.lm.shape[0]
+        q = np.diag([0.03, 0.03, np.deg2rad(2.0)]) ** 2 if q is None else np.asarray(q, float)
+        r = np.diag([0.3, 0.3]) ** 2 if r is None else np.asarray(r, float)
+        cfg = PFConfig()
+        cfg.dt = float(dt)
+        cfg.ess_threshold = self.n / 100.0 if ess_threshold is None else float(ess_threshold)
+        cfg.r_cov[:] = [float(v) for v in r.ravel()]
+        cfg.q_factor[:] = [float(v) for v in numpy_noise_factor(q).ravel()]
+        cfg.alphas[:] = [float(v) for v in alphas]
+        cfg.x0[:] = [float(v) for v in x0]
+        cfg.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
+        cfg.motion = _lib.MOTION[motion]
+        cfg.likelihood = _lib.LIKELIHOOD[likelihood]
+        self.motion = motion
+        self.cfg = cfg
+        h = C.c_void_p()
+        check(lib.slam_pf_create(C.byref(cfg), self.n, self.nl, dptr(self.lm), int(device),
+                                 C.byref(h)), "slam_pf_create")
+        self._h = h
+        self._lib = lib
+        self.resample_next = False
+        self.last = None
+
+    # ------------------------------------------------------------ lifetime
+    def close(self):
+        if getattr(self, "_h", None):
+            self._lib.slam_pf_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    # --------------------------------------------------------------- state
+    def set_state(self, x=None, y=None, th=None, w=None):
+        arrs = [None if a is None else _f64(a, (self.n,)) for a in (x, y, th, w)]
+        check(self._lib.slam_pf_set_state(self._h, *[dptr(a) for a in arrs]), "slam_pf_set_state")
+        if w is not None:
+            ww = arrs[3]
+            self.resample_next = bool(1.0 / float(ww @ ww) < self.cfg.ess_threshold)
+
+    def get_state(self):
+        out = [np.empty(self.n) for _ in range(4)]
+        check(self._lib.slam_pf_get_state(self._h, *[dptr(a) for a in out]), "slam_pf_get_state")
+        return tuple(out)
+
+    def set_landmarks(self, lm):
+        lm = _f64(lm).reshape(-1, 2)
+        if lm.shape[0] != self.nl:
+            raise ValueError("landmark count is fixed at construction")
+        self.lm = lm
+        check(self._lib.slam_pf_set_landmarks(self._h, dptr(lm)), "slam_pf_set_landmarks")
+
+    # ---------------------------------------------------------------- step
+    @staticmethod
+    def _res(r: PFResult):
+        return {"x_est": np.array(r.x_est[:]), "cov": np.array(r.cov[:]).reshape(3, 3),
+                "max_val": r.max_val, "max_idx": int(r.max_idx), "ess": r.ess,
+                "weight_sum": r.weight_sum, "resampled": bool(r.resampled),
+                "resample_next": bool(r.resample_next), "status": r.status,
+                "n_special": r.n_special}
+
+    def step(self, control, z, noise=None, u_resample=float("nan")):
+        ctl = _f64(control, (2,))
+        zz = _f64(z, (self.nl, 2))
+        nz = None if noise is None else _f64(noise, (self.n, 3))
+        res = PFResult()
+        check(self._lib.slam_pf_step(self._h, dptr(ctl), dptr(zz), dptr(nz), float(u_resample),
+                                     C.byref(res)), "slam_pf_step")
+        out = self._res(res)
+        self.resample_next = out["resample_next"]
+        self.last = out
+        return out
+
+    def resample(self, u_resample=float("nan"), force=False):
+        flag = C.c_int32(0)
+        check(self._lib.slam_pf_resample(self._h, float(u_resample), int(bool(force)),
+                                         C.byref(flag)), "slam_pf_resample")
+        if flag.value:
+            self.resample_next = False
+        return bool(flag.value)
+
+    def predict(self, control, noise=None):
+        ctl = _f64(control, (2,))
+        nz = None if noise is None else _f64(noise, (self.n, 3))
+        check(self._lib.slam_pf_predict(self._h, dptr(ctl), dptr(nz)), "slam_pf_predict")
+
+    def update(self, z):
+        zz = _f64(z, (self.nl, 2))
+        res = PFResult()
+        check(self._lib.slam_pf_update(self._h, dptr(zz), C.byref(res)), "slam_pf_update")
+        out = self._res(res)
+        self.resample_next = out["resample_next"]
+        return out
+
+    def resample_indices(self, u_resample):
+        idx = np.empty(self.n, dtype=np.int64)
+        ns = C.c_int32(0)
+        check(self._lib.slam_pf_resample_indices(self._h, float(u_resample),
+                                                 idx.ctypes.data_as(_lib._I64), C.byref(ns)),
+              "slam_pf_resample_indices")
+        return idx, ns.value
+
+    def weight_sum(self):
+        s = C.c_double(0.0)
+        check(self._lib.slam_pf_weight_sum(self._h, C.byref(s)), "slam_pf_weight_sum")
+        return s.value
+
+    # ------------------------------------------------------ device-resident
+    def load_observations(self, z_all):
+        z_all = _f64(z_all).reshape(-1, self.nl, 2)
+        check(self._lib.slam_pf_load_observations(self._h, z_all.shape[0], dptr(z_all)),
+              "slam_pf_load_observations")
+        self._z_steps = z_all.shape[0]
+
+    def run(self, first_step, controls, want_results=True):
+        controls = _f64(controls).reshape(-1, 2)
+        k = controls.shape[0]
+        res = (PFResult * k)()
+        check(self._lib.slam_pf_run(self._h, int(first_step), k, dptr(controls), res),
+              "slam_pf_run")
+        self.resample_next = bool(res[k - 1].resample_next)
+        return [self._res(r) for r in res] if want_results else None
+
+    def enable_timing(self, on=True):
+        check(self._lib.slam_pf_enable_timing(self._h, int(bool(on))), "slam_pf_enable_timing")
+
+    def timing(self, kernel):
+        ms = C.c_double(0.0)
+        cnt = C.c_int64(0)
+        check(self._lib.slam_pf_timing(self._h, int(kernel), C.byref(ms), C.byref(cnt)),
+              "slam_pf_timing")
+        return ms.value, cnt.value

@@ -1,0 +1,174 @@
+"""Parity of the HIP particle filter (through the C-ABI) against the oracle and
+the reference-generated golden fixtures.  Runs on the GPU box (-m gpu).
+
+Tolerances (stated per test):
+  * bit-exact: resampling indices given identical weights and offset, np.sum
+    order, linear-model prediction noise addition;
+  * weights: |w - w_ref| <= 1e-11 |w_ref| + 1e-280 (GPU exp/sin/cos differ from
+    NumPy's by <= 1 ulp; weights below 1e-280 are underflow territory where the
+    reference's own sequential product has already lost precision);
+  * pose / covariance: 1e-6 relative (north_star), with identical max_idx.
+"""
+import numpy as np
+import pytest
+
+from conftest import golden, heavy_weights, rle_decode, stage_weights
+
+import pf_oracle as po
+
+pytestmark = pytest.mark.gpu
+
+
+def _close_w(a, b, rtol=1e-11, atol=1e-280):
+    a, b = np.asarray(a), np.asarray(b)
+    bad = np.abs(a - b) > rtol * np.abs(b) + atol
+    assert not bad.any(), f"{bad.sum()} weights differ; first at {np.argmax(bad)}: {a[bad][:3]} vs {b[bad][:3]}"
+
+
+@pytest.fixture(scope="module")
+def slamhip_pf():
+    from slamhip import pf as dpf
+    return dpf
+
+
+@pytest.mark.parametrize("tag,n", [("r500", 500), ("r1000", 1000), ("r8193", 8193),
+                                   ("r65536", 65536), ("r1m", 1 << 20)])
+def test_resample_indices_bit_exact(slamhip_pf, tag, n):
+    g = golden("pf_stages")
+    w = stage_weights(tag, n, g[f"{tag}_wseed"])
+    ref = rle_decode(g[f"{tag}_idx_vals"], g[f"{tag}_idx_counts"])
+    with slamhip_pf.DeviceParticleFilter(n, np.zeros((1, 2))) as d:
+        d.set_state(w=w)
+        idx, nspec = d.resample_indices(float(g[f"{tag}_u"]))
+    np.testing.assert_array_equal(idx, ref)
+    assert nspec < n // 4 + 64
+
+
+@pytest.mark.parametrize("n", [1, 7, 8, 100, 128, 129, 500, 1000, 8192, 8193, 20000, 100003, 1 << 20])
+def test_weight_sum_numpy_order(slamhip_pf, n):
+    g = golden("units")
+    i = list(g["sum_sizes"]).index(n)
+    a = heavy_weights(np.random.RandomState(n), n)
+    with slamhip_pf.DeviceParticleFilter(n, np.zeros((1, 2))) as d:
+        d.set_state(w=a)
+        s = d.weight_sum()
+    assert s == g["sum_out"][i]
+
+
+@pytest.mark.parametrize("lik", ["product", "logsum"])
+@pytest.mark.parametrize("tag", ["a", "b", "c"])
+def test_likelihood_stage(slamhip_pf, tag, lik):
+    g = golden("pf_stages")
+    px, pw = g[f"lik_{tag}_px"], g[f"lik_{tag}_pw"]
+    ref = g[f"lik_{tag}_out"]
+    n = pw.size
+    with slamhip_pf.DeviceParticleFilter(n, g[f"lik_{tag}_lm"], likelihood=lik) as d:
+        d.set_state(px[0], px[1], px[2], pw)
+        out = d.update(g[f"lik_{tag}_z"])
+        _, _, _, w = d.get_state()
+    _close_w(w, ref)
+    assert out["max_idx"] == int(np.argmax(ref))
+
+
+@pytest.mark.parametrize("tag", ["a", "b", "c"])
+def test_predict_linear_stage(slamhip_pf, tag):
+    g = golden("pf_stages")
+    px = g[f"pred_{tag}_in"]
+    n = px.shape[1]
+    p = po.PFParams(n_particles=n)
+    np.random.seed(int(g[f"pred_{tag}_seed"]))
+    v = np.random.multivariate_normal([0.0, 0.0, 0.0], p.q, n)
+    with slamhip_pf.DeviceParticleFilter(n, np.zeros((1, 2))) as d:
+        d.set_state(px[0], px[1], px[2])
+        d.predict((p.vel, p.omega), v)
+        x, y, th, _ = d.get_state()
+    np.testing.assert_allclose(np.vstack([x, y, th]), g[f"pred_{tag}_out"], rtol=0, atol=1e-14)
+
+
+def test_predict_velocity_model(slamhip_pf):
+    g = golden("motion")
+    poses = g["poses"]
+    n = poses.shape[0]
+    dt, a1, a2, a3, a4, a5, a6, v, w = g["case1"]
+    np.random.seed(int(g["seed1"]))
+    gn = np.random.standard_normal(3 * n).reshape(n, 3)
+    with slamhip_pf.DeviceParticleFilter(n, np.zeros((1, 2)), dt=dt, motion="velocity",
+                                         alphas=(a1, a2, a3, a4, a5, a6)) as d:
+        d.set_state(poses[:, 0], poses[:, 1], poses[:, 2])
+        d.predict((v, w), gn)
+        x, y, th, _ = d.get_state()
+    np.testing.assert_allclose(np.stack([x, y, th], axis=1), g["noisy1"], rtol=1e-12, atol=1e-12)
+
+
+def test_c1_end_to_end_vs_reference():
+    """BASELINE config 1 through the drop-in ParticleFilter: 500 particles x 20
+    landmarks x 1000 steps, seed 0, NumPy noise stream."""
+    from particle_filter import ParticleFilter
+    g = golden("pf_c1")
+    np.random.seed(int(g["seed"]))
+    pf = ParticleFilter(100, n_particles=int(g["n"]), landmarks=g["lm"])
+    steps = len(g["x_est"])
+    x_est = np.zeros((steps, 3))
+    max_idx = np.zeros(steps, dtype=np.int64)
+    res = np.zeros(steps, dtype=bool)
+    keep = {int(k): j for j, k in enumerate(g["keep_steps"])}
+    for k in range(steps):
+        was = pf.dev.resample_next
+        _, xt, xe, px, _, mi, mv = pf.main_pf()
+        x_est[k], max_idx[k], res[k] = xe[:, 0], mi, was
+        np.testing.assert_array_equal(xt[:, 0], g["x_true"][k])
+        if k in keep:
+            j = keep[k]
+            np.testing.assert_allclose(px, g["px_keep"][j], rtol=1e-6, atol=1e-9)
+            _close_w(pf.weights, g["pw_keep"][j], rtol=1e-9, atol=1e-250)
+    np.testing.assert_array_equal(res, g["resampled"])
+    np.testing.assert_array_equal(max_idx, g["max_idx"])
+    np.testing.assert_allclose(x_est, g["x_est"], rtol=1e-6, atol=1e-9)
+
+
+def test_step_covariance_vs_oracle(slamhip_pf):
+    rs = np.random.RandomState(5)
+    n, nl = 3000, 30
+    lm = rs.uniform(-10, 10, (nl, 2))
+    p = po.PFParams(n_particles=n, landmarks=lm)
+    orc = po.PFOracle(p)
+    orc.x += rs.normal(size=n) * 0.3
+    orc.y += rs.normal(size=n) * 0.3
+    with slamhip_pf.DeviceParticleFilter(n, lm) as d:
+        d.set_state(orc.x, orc.y, orc.th, orc.w)
+        world = po.PFWorld(p)
+        np.random.seed(9)
+        for k in range(25):
+            world.advance()
+            ofs_u = np.random.rand() if orc.needs_resample() else None
+            assert d.resample_next == (ofs_u is not None)
+            noise = np.random.multivariate_normal([0.0, 0.0, 0.0], p.q, n)
+            z = world.observe()
+            ro = orc.step(z, noise, None if ofs_u is None else ofs_u * p.np_recip)
+            rd = d.step((p.vel, p.omega), z, noise, np.nan if ofs_u is None else ofs_u)
+            assert rd["max_idx"] == ro["max_idx"]
+            np.testing.assert_allclose(rd["x_est"], ro["x_est"], rtol=1e-6)
+            np.testing.assert_allclose(rd["cov"], ro["cov"], rtol=1e-6, atol=1e-12)
+            assert abs(rd["ess"] - ro["ess"]) <= 1e-9 * ro["ess"]
+
+
+@pytest.mark.parametrize("motion", ["linear", "velocity"])
+def test_device_rng_run_tracks_truth(slamhip_pf, motion):
+    """Device-resident run (bench path): on-device Philox noise, device-decided
+    resampling; the estimate must track the simulated truth."""
+    rs = np.random.RandomState(1)
+    n, nl, steps = 1 << 16, 100, 40
+    lm = rs.uniform(-10, 10, (nl, 2))
+    p = po.PFParams(n_particles=n, landmarks=lm, motion=motion)
+    world = po.PFWorld(p)
+    np.random.seed(3)
+    zs, xs = [], []
+    for _ in range(steps):
+        xs.append(world.advance().copy())
+        zs.append(world.observe())
+    with slamhip_pf.DeviceParticleFilter(n, lm, motion=motion, seed=7) as d:
+        d.load_observations(np.array(zs))
+        out = d.run(0, np.tile([p.vel, p.omega], (steps, 1)))
+    err = np.array([np.hypot(*(o["x_est"][:2] - x[:2])) for o, x in zip(out, xs)])
+    assert np.all(np.isfinite(err)) and np.median(err) < 0.5
+    assert sum(o["resampled"] for o in out) >= 1
