@@ -71,6 +71,7 @@ struct slam_pf {
     double* wsum = nullptr;
     double* refp = nullptr;
     int32_t* flags = nullptr;
+    unsigned* counters = nullptr;   // last-arriver tickets (zeroed by the last block)
     // inputs
     double* lm = nullptr;
     double* z = nullptr;
@@ -226,20 +227,18 @@ int launch_fused(slam_pf* h, const PredictConst& pc, const double* z_dev, bool h
     return SLAM_OK;
 }
 
-// numpy-order sum + normalise + reductions + finalise into res_dev[slot]
+// numpy-order sum + normalise + reductions + result into res_dev[slot]
 int launch_reduce(slam_pf* h, const double* w_src, int slot, int32_t resampled_known) {
     const int64_t n = h->n;
     hipStream_t s = h->stream;
     const int c = h->cur;
     tic(h, 1);
     chunk_sum_kernel<<<h->nchunks, 512, 0, s>>>(w_src, n, h->part, h->tail_leaves, h->tail_ops,
-                                                 h->n_tail_leaves, h->n_tail_ops);
-    normalize_kernel<<<h->nb_norm, kNormThreads, 0, s>>>(n, w_src, h->w, h->part, h->nchunks,
-                                                          1.0 / (double)n, h->x[c], h->y[c],
-                                                          h->th[c], h->refp, h->bp, h->wsum, 0);
-    finalize_kernel<<<1, 64, 0, s>>>(h->bp, h->nb_norm, h->x[c], h->y[c], h->th[c], h->refp,
-                                      h->wsum, h->flags, h->cfg.ess_threshold, h->res_dev + slot,
-                                      resampled_known);
+                                                 h->n_tail_leaves, h->n_tail_ops, h->counters,
+                                                 h->wsum);
+    normalize_kernel<<<h->nb_norm, kNormThreads, 0, s>>>(
+        n, w_src, h->w, h->wsum, 1.0 / (double)n, h->x[c], h->y[c], h->th[c], h->refp, h->bp,
+        h->counters + 1, h->flags, h->cfg.ess_threshold, h->res_dev + slot, resampled_known, 0);
     toc(h, 1);
     SLAM_HIP_TRY(hipGetLastError());
     return SLAM_OK;
@@ -311,7 +310,7 @@ int slam_pf_create(const slam_pf_config* cfg, int64_t n_particles, int32_t n_lan
     const int64_t n = n_particles;
     h->nb_scan = (int32_t)((n + kScanBlock - 1) / kScanBlock);
     h->nchunks = (int32_t)((n + kSumChunk - 1) / kSumChunk);
-    h->nb_norm = (int32_t)std::min<int64_t>(kNormBlocksMax, (n + kNormThreads - 1) / kNormThreads);
+    h->nb_norm = (int32_t)std::min<int64_t>(kNormBlocksMax, (n + 4 * kNormThreads - 1) / (4 * kNormThreads));
     hipError_t e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking);
     if (e != hipSuccess) {
         delete h;
@@ -348,6 +347,7 @@ int slam_pf_create(const slam_pf_config* cfg, int64_t n_particles, int32_t n_lan
     A(h->wsum, 1);
     A(h->refp, 4);
     A(h->flags, kFlagWords);
+    A(h->counters, 4);
     A(h->lm, 2 * std::max<int32_t>(n_landmarks, 1));
     A(h->z, 2 * std::max<int32_t>(n_landmarks, 1));
     A(h->noise, 3 * n);
@@ -381,6 +381,7 @@ int slam_pf_create(const slam_pf_config* cfg, int64_t n_particles, int32_t n_lan
     SLAM_HIP_TRY(hipMemcpy(h->w, tmp.data(), n * sizeof(double), hipMemcpyHostToDevice));
     SLAM_HIP_TRY(hipMemcpy(h->refp, cfg->x0, 3 * sizeof(double), hipMemcpyHostToDevice));
     SLAM_HIP_TRY(hipMemset(h->flags, 0, kFlagWords * sizeof(int32_t)));
+    SLAM_HIP_TRY(hipMemset(h->counters, 0, 4 * sizeof(unsigned)));
     if (n_landmarks > 0)
         SLAM_HIP_TRY(hipMemcpy(h->lm, landmarks, 2 * n_landmarks * sizeof(double), hipMemcpyHostToDevice));
     *out = h;
@@ -394,7 +395,7 @@ int slam_pf_destroy(slam_pf* h) {
     void* ptrs[] = {h->x[0], h->x[1], h->y[0], h->y[1], h->th[0], h->th[1], h->w, h->w_un,
                     h->c, h->kincl, h->fexcl, h->idx, h->bsum, h->boff, h->bk, h->boffk,
                     h->bf, h->bofff, h->ktot, h->nspec, h->spec_in, h->spec_out, h->part,
-                    h->tail_leaves, h->tail_ops, h->bp, h->wsum, h->refp, h->flags, h->lm,
+                    h->tail_leaves, h->tail_ops, h->bp, h->wsum, h->refp, h->flags, h->counters, h->lm,
                     h->z, h->noise, h->z_all, h->res_dev};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
@@ -572,7 +573,7 @@ int slam_pf_weight_sum(slam_pf* h, double* sum_out) {
     SLAM_HIP_TRY(hipSetDevice(h->device));
     chunk_sum_kernel<<<h->nchunks, 512, 0, h->stream>>>(h->w, h->n, h->part, h->tail_leaves,
                                                          h->tail_ops, h->n_tail_leaves,
-                                                         h->n_tail_ops);
+                                                         h->n_tail_ops, h->counters, nullptr);
     SLAM_HIP_TRY(hipGetLastError());
     std::vector<double> p((size_t)h->nchunks);
     SLAM_HIP_TRY(hipMemcpyAsync(p.data(), h->part, h->nchunks * 8, hipMemcpyDeviceToHost, h->stream));

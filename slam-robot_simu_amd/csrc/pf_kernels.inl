@@ -164,17 +164,44 @@ __global__ __launch_bounds__(256) void pf_fused_kernel(
 }
 
 // ====================================================================
+// last-arriver election across the blocks of one launch (Guideline 16):
+// thread 0 of every block stores its partial, releases at agent scope and takes
+// a ticket; the block holding the last ticket acquires and combines.  The
+// ticket counter is re-zeroed by that block (next launch sees it after the
+// kernel boundary).
+// ====================================================================
+__device__ __forceinline__ bool arrive_last(unsigned* counter) {
+    __shared__ int last;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const unsigned t = atomicAdd(counter, 1u);
+        last = (t == gridDim.x - 1) ? 1 : 0;
+        if (last) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            *counter = 0u;
+        }
+    }
+    __syncthreads();
+    return last != 0;
+}
+
+// ====================================================================
 // numpy-order chunk sums (np.sum: 8192-element buffers, pairwise inside)
 // ====================================================================
 // Full chunk: 512 threads = 64 leaves x 8 accumulators; accumulator k of leaf
 // L sums elements L*128 + k + 8m (m = 0..15) left to right; leaves combine as
 // a perfect binary tree, which the xor-butterfly reproduces exactly.
 // Tail chunk (< 8192): host-built leaf table + post-order combine program.
+// The last block folds the buffer partials left to right into *s_out.
 __global__ __launch_bounds__(512) void chunk_sum_kernel(
     const double* __restrict__ w, const int64_t n, double* __restrict__ part,
     const int32_t* __restrict__ tail_leaves, const int32_t* __restrict__ tail_ops,
-    const int32_t n_tail_leaves, const int32_t n_tail_ops) {
-    __shared__ double sh[512];
+    const int32_t n_tail_leaves, const int32_t n_tail_ops, unsigned* __restrict__ counter,
+    double* __restrict__ s_out) {
+    __shared__ double sh[1024];
     const int64_t base = (int64_t)blockIdx.x * kSumChunk;
     const int64_t len = (n - base < kSumChunk) ? (n - base) : kSumChunk;
     const int t = threadIdx.x;
@@ -188,83 +215,165 @@ __global__ __launch_bounds__(512) void chunk_sum_kernel(
         for (int d = 1; d < 64; d <<= 1) r = r + __shfl_xor(r, d, 64);
         if ((t & 63) == 0) sh[t >> 6] = r;
         __syncthreads();
-        if (t == 0) {
-            const double s = ((sh[0] + sh[1]) + (sh[2] + sh[3])) + ((sh[4] + sh[5]) + (sh[6] + sh[7]));
-            part[blockIdx.x] = s;
-        }
-        return;
-    }
-    // tail: leaves of <= 128 elements, one per thread
-    for (int L = t; L < n_tail_leaves; L += blockDim.x) {
-        const int lo = tail_leaves[2 * L], cnt = tail_leaves[2 * L + 1];
-        const double* a = w + base + lo;
-        double res;
-        if (cnt < 8) {
-            res = 0.0;
-            for (int i = 0; i < cnt; ++i) res = res + a[i];
-        } else {
-            double r[8];
-#pragma unroll
-            for (int k = 0; k < 8; ++k) r[k] = a[k];
-            int i = 8;
-            const int stop = cnt - (cnt % 8);
-            for (; i < stop; i += 8) {
-#pragma unroll
-                for (int k = 0; k < 8; ++k) r[k] = r[k] + a[i + k];
-            }
-            res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
-            for (; i < cnt; ++i) res = res + a[i];
-        }
-        sh[L] = res;
-    }
-    __syncthreads();
-    if (t == 0) {
-        double stk[16];
-        int sp = 0;
-        for (int o = 0; o < n_tail_ops; ++o) {
-            const int op = tail_ops[o];
-            if (op >= 0) {
-                stk[sp++] = sh[op];
+        if (t == 0)
+            part[blockIdx.x] = ((sh[0] + sh[1]) + (sh[2] + sh[3])) + ((sh[4] + sh[5]) + (sh[6] + sh[7]));
+    } else {
+        // tail: leaves of <= 128 elements, one per thread
+        for (int L = t; L < n_tail_leaves; L += blockDim.x) {
+            const int lo = tail_leaves[2 * L], cnt = tail_leaves[2 * L + 1];
+            const double* a = w + base + lo;
+            double res;
+            if (cnt < 8) {
+                res = 0.0;
+                for (int i = 0; i < cnt; ++i) res = res + a[i];
             } else {
-                const double b = stk[--sp];
-                const double a = stk[--sp];
-                stk[sp++] = a + b;
+                double r[8];
+#pragma unroll
+                for (int k = 0; k < 8; ++k) r[k] = a[k];
+                int i = 8;
+                const int stop = cnt - (cnt % 8);
+                for (; i < stop; i += 8) {
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) r[k] = r[k] + a[i + k];
+                }
+                res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+                for (; i < cnt; ++i) res = res + a[i];
             }
+            sh[L] = res;
         }
-        part[blockIdx.x] = stk[0];
+        __syncthreads();
+        if (t == 0) {
+            double stk[16];
+            int sp = 0;
+            for (int o = 0; o < n_tail_ops; ++o) {
+                const int op = tail_ops[o];
+                if (op >= 0) {
+                    stk[sp++] = sh[op];
+                } else {
+                    const double b = stk[--sp];
+                    const double a = stk[--sp];
+                    stk[sp++] = a + b;
+                }
+            }
+            part[blockIdx.x] = stk[0];
+        }
     }
+    if (!s_out) return;
+    if (!arrive_last(counter)) return;
+    double s = 0.0;                                   // buffer partials left to right
+    const int nc = gridDim.x;
+    for (int c0 = 0; c0 < nc; c0 += 1024) {
+        const int cnt = min(1024, nc - c0);
+        __syncthreads();
+        for (int k = t; k < cnt; k += blockDim.x) sh[k] = part[c0 + k];
+        __syncthreads();
+        if (t == 0)
+            for (int k = 0; k < cnt; ++k) s = s + sh[k];
+    }
+    if (t == 0) *s_out = s;
 }
 
 // ====================================================================
-// normalise (particle_filter.py:226-237) + per-block reductions
+// normalise (particle_filter.py:226-237) + reductions; the last block
+// combines the block partials in block order and writes the step result.
 // ====================================================================
-__global__ __launch_bounds__(kNormThreads) void normalize_kernel(
-    const int64_t n, const double* __restrict__ w_un, double* __restrict__ w,
-    const double* __restrict__ part, const int32_t nchunks, const double np_recip,
-    const double* __restrict__ xs, const double* __restrict__ ys, const double* __restrict__ ts,
-    const double* __restrict__ refp, BlockPartial* __restrict__ bp, double* __restrict__ s_out,
-    const int64_t gbase) {
-    __shared__ double sh_s;
-    __shared__ BlockPartial shp[kNormThreads / 64];
-    if (threadIdx.x == 0) {
-        double s = 0.0;                       // buffer partials added left to right
-        for (int c = 0; c < nchunks; ++c) s = s + part[c];
-        sh_s = s;
-        if (blockIdx.x == 0) *s_out = s;
-    }
-    __syncthreads();
-    const double s = sh_s;
-    const double r0 = refp[0], r1 = refp[1], r2 = refp[2];
-    BlockPartial a;
+__device__ __forceinline__ void bp_zero(BlockPartial& a) {
     a.maxv = -1.0;
     a.maxi = INT64_MAX;
     a.sw = a.sw2 = 0.0;
     for (int k = 0; k < 3; ++k) a.m1[k] = 0.0;
     for (int k = 0; k < 6; ++k) a.m2[k] = 0.0;
+}
+
+__device__ __forceinline__ void bp_merge(BlockPartial& r, const BlockPartial& o) {
+    if (o.maxv > r.maxv || (o.maxv == r.maxv && o.maxi < r.maxi)) {
+        r.maxv = o.maxv;
+        r.maxi = o.maxi;
+    }
+    r.sw += o.sw;
+    r.sw2 += o.sw2;
+    for (int q = 0; q < 3; ++q) r.m1[q] += o.m1[q];
+    for (int q = 0; q < 6; ++q) r.m2[q] += o.m2[q];
+}
+
+__device__ __forceinline__ void bp_wave_reduce(BlockPartial& a) {
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+        BlockPartial o;
+        o.maxv = __shfl_xor(a.maxv, d, 64);
+        o.maxi = __shfl_xor(a.maxi, d, 64);
+        o.sw = __shfl_xor(a.sw, d, 64);
+        o.sw2 = __shfl_xor(a.sw2, d, 64);
+        for (int k = 0; k < 3; ++k) o.m1[k] = __shfl_xor(a.m1[k], d, 64);
+        for (int k = 0; k < 6; ++k) o.m2[k] = __shfl_xor(a.m2[k], d, 64);
+        // keep the lower lane on the left so every lane holds the same value
+        if ((threadIdx.x & d) == 0) bp_merge(a, o);
+        else {
+            bp_merge(o, a);
+            a = o;
+        }
+    }
+}
+
+// block-level reduction of per-thread partials in a fixed order -> thread 0
+__device__ __forceinline__ BlockPartial bp_block_reduce(BlockPartial a, BlockPartial* shp) {
+    bp_wave_reduce(a);
+    if ((threadIdx.x & 63) == 0) shp[threadIdx.x >> 6] = a;
+    __syncthreads();
+    BlockPartial r = shp[0];
+    if (threadIdx.x == 0)
+        for (int k = 1; k < (int)(blockDim.x >> 6); ++k) bp_merge(r, shp[k]);
+    __syncthreads();
+    return r;
+}
+
+// result record from the combined partial (x_est = particle at the argmax)
+__device__ void write_result(const BlockPartial& r, const double* xs, const double* ys,
+                             const double* ts, const int64_t gbase, double* refp,
+                             const double s, int32_t* flags, const double ess_th,
+                             slam_pf_result* res, const int32_t resampled_known) {
+    slam_pf_result o;
+    const int64_t mi = r.maxi;
+    o.max_idx = mi;
+    o.max_val = r.maxv;
+    o.x_est[0] = xs[mi - gbase];
+    o.x_est[1] = ys[mi - gbase];
+    o.x_est[2] = ts[mi - gbase];
+    const double inv = 1.0 / r.sw;
+    const double mu[3] = {r.m1[0] * inv, r.m1[1] * inv, r.m1[2] * inv};
+    const double m2[9] = {r.m2[0], r.m2[1], r.m2[2], r.m2[1], r.m2[3], r.m2[4], r.m2[2], r.m2[4], r.m2[5]};
+    for (int a = 0; a < 3; ++a)
+        for (int b = 0; b < 3; ++b) o.cov[3 * a + b] = m2[3 * a + b] * inv - mu[a] * mu[b];
+    o.ess = 1.0 / r.sw2;
+    o.weight_sum = s;
+    o.resampled = resampled_known >= 0 ? resampled_known : flags[kFlagResample];
+    o.resample_next = (o.ess < ess_th) ? 1 : 0;
+    o.status = flags[kFlagStatus];
+    o.n_special = flags[kFlagNSpecial];
+    flags[kFlagResample] = o.resample_next;
+    flags[kFlagStatus] = 0;
+    refp[0] = o.x_est[0];
+    refp[1] = o.x_est[1];
+    refp[2] = o.x_est[2];
+    *res = o;
+}
+
+__global__ __launch_bounds__(kNormThreads) void normalize_kernel(
+    const int64_t n, const double* __restrict__ w_un, double* __restrict__ w,
+    const double* __restrict__ s_in, const double np_recip, const double* __restrict__ xs,
+    const double* __restrict__ ys, const double* __restrict__ ts, double* __restrict__ refp,
+    BlockPartial* __restrict__ bp, unsigned* __restrict__ counter, int32_t* __restrict__ flags,
+    const double ess_th, slam_pf_result* __restrict__ res, const int32_t resampled_known,
+    const int64_t gbase) {
+    __shared__ BlockPartial shp[kNormThreads / 64];
+    const double s = *s_in;
+    const double r0 = refp[0], r1 = refp[1], r2 = refp[2];
+    BlockPartial a;
+    bp_zero(a);
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
          i += (int64_t)gridDim.x * blockDim.x) {
-        double v = w_un[i] / s;
-        if (isnan(v)) v = np_recip;
+        double v = w_un[i] / s;                          // particle_filter.py:235
+        if (isnan(v)) v = np_recip;                      // :236
         w[i] = v;
         if (v > a.maxv) {
             a.maxv = v;
@@ -283,88 +392,18 @@ __global__ __launch_bounds__(kNormThreads) void normalize_kernel(
         a.m2[4] += v * d1 * d2;
         a.m2[5] += v * d2 * d2;
     }
-    // wave reduction
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) {
-        const double ov = __shfl_xor(a.maxv, d, 64);
-        const int64_t oi = __shfl_xor(a.maxi, d, 64);
-        if (ov > a.maxv || (ov == a.maxv && oi < a.maxi)) {
-            a.maxv = ov;
-            a.maxi = oi;
-        }
-        a.sw += __shfl_xor(a.sw, d, 64);
-        a.sw2 += __shfl_xor(a.sw2, d, 64);
-        for (int k = 0; k < 3; ++k) a.m1[k] += __shfl_xor(a.m1[k], d, 64);
-        for (int k = 0; k < 6; ++k) a.m2[k] += __shfl_xor(a.m2[k], d, 64);
-    }
-    if ((threadIdx.x & 63) == 0) shp[threadIdx.x >> 6] = a;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        BlockPartial r = shp[0];
-        for (int k = 1; k < kNormThreads / 64; ++k) {
-            const BlockPartial& o = shp[k];
-            if (o.maxv > r.maxv || (o.maxv == r.maxv && o.maxi < r.maxi)) {
-                r.maxv = o.maxv;
-                r.maxi = o.maxi;
-            }
-            r.sw += o.sw;
-            r.sw2 += o.sw2;
-            for (int q = 0; q < 3; ++q) r.m1[q] += o.m1[q];
-            for (int q = 0; q < 6; ++q) r.m2[q] += o.m2[q];
-        }
-        bp[blockIdx.x] = r;
-    }
-}
-
-// combine BlockPartials (fixed order) -> result record; sets the resample flag
-__device__ void combine_partials(const BlockPartial* bp, int nb, BlockPartial& r) {
-    r = bp[0];
-    for (int k = 1; k < nb; ++k) {
-        const BlockPartial& o = bp[k];
-        if (o.maxv > r.maxv || (o.maxv == r.maxv && o.maxi < r.maxi)) {
-            r.maxv = o.maxv;
-            r.maxi = o.maxi;
-        }
-        r.sw += o.sw;
-        r.sw2 += o.sw2;
-        for (int q = 0; q < 3; ++q) r.m1[q] += o.m1[q];
-        for (int q = 0; q < 6; ++q) r.m2[q] += o.m2[q];
-    }
-}
-
-__global__ void finalize_kernel(const BlockPartial* __restrict__ bp, const int32_t nb,
-                                const double* __restrict__ xs, const double* __restrict__ ys,
-                                const double* __restrict__ ts, double* __restrict__ refp,
-                                const double* __restrict__ s_in, int32_t* __restrict__ flags,
-                                const double ess_th, slam_pf_result* __restrict__ res,
-                                const int32_t resampled_known) {
-    if (threadIdx.x != 0 || blockIdx.x != 0) return;
-    BlockPartial r;
-    combine_partials(bp, nb, r);
-    slam_pf_result o;
-    const int64_t mi = r.maxi;
-    o.max_idx = mi;
-    o.max_val = r.maxv;
-    o.x_est[0] = xs[mi];
-    o.x_est[1] = ys[mi];
-    o.x_est[2] = ts[mi];
-    const double inv = 1.0 / r.sw;
-    const double mu[3] = {r.m1[0] * inv, r.m1[1] * inv, r.m1[2] * inv};
-    const double m2[9] = {r.m2[0], r.m2[1], r.m2[2], r.m2[1], r.m2[3], r.m2[4], r.m2[2], r.m2[4], r.m2[5]};
-    for (int a = 0; a < 3; ++a)
-        for (int b = 0; b < 3; ++b) o.cov[3 * a + b] = m2[3 * a + b] * inv - mu[a] * mu[b];
-    o.ess = 1.0 / r.sw2;
-    o.weight_sum = *s_in;
-    o.resampled = resampled_known >= 0 ? resampled_known : flags[kFlagResample];
-    o.resample_next = (o.ess < ess_th) ? 1 : 0;
-    o.status = flags[kFlagStatus];
-    o.n_special = flags[kFlagNSpecial];
-    flags[kFlagResample] = o.resample_next;
-    flags[kFlagStatus] = 0;
-    refp[0] = o.x_est[0];
-    refp[1] = o.x_est[1];
-    refp[2] = o.x_est[2];
-    *res = o;
+    const BlockPartial r = bp_block_reduce(a, shp);
+    if (threadIdx.x == 0) bp[blockIdx.x] = r;
+    if (!res) return;
+    if (!arrive_last(counter)) return;
+    // fixed-order combine: thread t merges blocks t, t+T, ... ; then tree
+    BlockPartial c;
+    bp_zero(c);
+    const int nb = gridDim.x;
+    for (int k = threadIdx.x; k < nb; k += blockDim.x) bp_merge(c, bp[k]);
+    const BlockPartial tot = bp_block_reduce(c, shp);
+    if (threadIdx.x == 0)
+        write_result(tot, xs, ys, ts, gbase, refp, s, flags, ess_th, res, resampled_known);
 }
 
 // ====================================================================

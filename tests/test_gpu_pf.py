@@ -100,13 +100,14 @@ def test_predict_velocity_model(slamhip_pf):
     np.testing.assert_allclose(np.stack([x, y, th], axis=1), g["noisy1"], rtol=1e-12, atol=1e-12)
 
 
-def test_c1_end_to_end_vs_reference():
+@pytest.mark.parametrize("lik", ["product", "logsum"])
+def test_c1_end_to_end_vs_reference(lik):
     """BASELINE config 1 through the drop-in ParticleFilter: 500 particles x 20
     landmarks x 1000 steps, seed 0, NumPy noise stream."""
     from particle_filter import ParticleFilter
     g = golden("pf_c1")
     np.random.seed(int(g["seed"]))
-    pf = ParticleFilter(100, n_particles=int(g["n"]), landmarks=g["lm"])
+    pf = ParticleFilter(100, n_particles=int(g["n"]), landmarks=g["lm"], likelihood=lik)
     steps = len(g["x_est"])
     x_est = np.zeros((steps, 3))
     max_idx = np.zeros(steps, dtype=np.int64)
@@ -149,7 +150,9 @@ def test_step_covariance_vs_oracle(slamhip_pf):
             assert rd["max_idx"] == ro["max_idx"]
             np.testing.assert_allclose(rd["x_est"], ro["x_est"], rtol=1e-6)
             np.testing.assert_allclose(rd["cov"], ro["cov"], rtol=1e-6, atol=1e-12)
-            assert abs(rd["ess"] - ro["ess"]) <= 1e-9 * ro["ess"]
+            ess_after = po.ess_of(orc.w)       # device reports the post-step ESS
+            assert abs(rd["ess"] - ess_after) <= 1e-9 * ess_after
+            assert rd["resample_next"] == (ess_after < p.ess_th)
 
 
 @pytest.mark.parametrize("motion", ["linear", "velocity"])

@@ -19,7 +19,7 @@ if [ "${SKIP_BENCH:-0}" != 1 ]; then
   if [ $rc != 0 ]; then exit $rc; fi
 fi
 if [ "${SKIP_PROF:-0}" != 1 ]; then
-  timeout -k 10 ${PROF_TIMEOUT:-300} rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run -- python bench.py --steps 20 --warmup 3 --no-cpu-baseline ${BENCH_ARGS:-} > "$OUT/prof_bench.json" 2> "$OUT/prof.err"
+  timeout -k 10 ${PROF_TIMEOUT:-300} rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python bench.py --steps 20 --warmup 3 --no-cpu-baseline ${BENCH_ARGS:-} > "$OUT/prof_bench.json" 2> "$OUT/prof.err"
   rc=$?; echo "rocprof rc=$rc"; find "$OUT/prof" -name "*stats*" | head
   if [ $rc != 0 ]; then tail -20 "$OUT/prof.err"; exit $rc; fi
 fi
