@@ -113,7 +113,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--likelihood", default="product", choices=["product", "logsum"])
+    ap.add_argument("--likelihood", default="logsum", choices=["product", "logsum"])
     ap.add_argument("--mode", default="replicas", choices=["replicas", "sharded"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()

@@ -117,6 +117,10 @@ int make_lik_const(slam_pf* h) {
     lc.nl = h->nl;
     lc.neg_nl_ln_den = -(double)h->nl * std::log(lc.den);
     lc.has_rho = (rho != 0.0) ? 1 : 0;
+    lc.rsxsy = 1.0 / lc.sxsy;
+    lc.rd2 = 1.0 / lc.d2;
+    lc.iso = (lc.sx2 == lc.sy2 && !lc.has_rho) ? 1 : 0;
+    lc.pad = 0;
     return SLAM_OK;
 }
 
@@ -171,16 +175,16 @@ int launch_resample(slam_pf* h, double u, int32_t force) {
     hipStream_t s = h->stream;
     const double delta = 4.0 * (double)n * 0x1p-53 + 0x1p-45;
     tic(h, 2);
-    scan_bsum_kernel<<<nb, kScanThreads, 0, s>>>(h->w, n, h->bsum, h->flags, force);
-    scan_top_kernel<double><<<1, 1024, 0, s>>>(h->bsum, h->boff, nb, (double*)nullptr, h->flags, force);
+    scan_bsum_kernel<<<nb, kScanThreads, 0, s>>>(h->w, n, h->bsum, h->boff, 0.0, h->counters + 2,
+                                                 h->flags, force);
     scan_classify_kernel<<<nb, kScanThreads, 0, s>>>(h->w, n, h->boff, h->c, h->kincl, h->fexcl,
-                                                     h->bk, h->bf, delta, 0, h->flags, force);
-    scan_top_kernel<uint64_t><<<1, 1024, 0, s>>>(h->bk, h->boffk, nb, h->ktot, h->flags, force);
-    scan_top_kernel<int32_t><<<1, 1024, 0, s>>>(h->bf, h->bofff, nb, h->nspec, h->flags, force);
+                                                     h->bk, h->bf, h->boffk, h->bofff, h->ktot,
+                                                     h->nspec, delta, 0, h->counters + 2, h->flags,
+                                                     force);
     scan_emit_kernel<<<nb, kScanThreads, 0, s>>>(h->w, n, h->c, h->kincl, h->fexcl, h->boffk,
-                                                 h->bofff, h->spec_in, 0, h->flags, force);
-    scan_serial_kernel<<<1, 256, 0, s>>>(h->spec_in, h->spec_out, h->nspec, h->ktot, n, 0.0,
-                                         h->flags, h->w, h->c, n, force);
+                                                 h->bofff, h->spec_in, 0, h->spec_out, h->nspec,
+                                                 h->ktot, 1, h->c, h->counters + 2, h->flags,
+                                                 force);
     scan_expand_kernel<<<nb, kScanThreads, 0, s>>>(n, h->kincl, h->fexcl, h->boffk, h->bofff,
                                                    h->spec_out, h->c, h->flags, force);
     const double step = 1.0 / (double)n;                      // particle_filter.py:213
@@ -310,7 +314,7 @@ int slam_pf_create(const slam_pf_config* cfg, int64_t n_particles, int32_t n_lan
     const int64_t n = n_particles;
     h->nb_scan = (int32_t)((n + kScanBlock - 1) / kScanBlock);
     h->nchunks = (int32_t)((n + kSumChunk - 1) / kSumChunk);
-    h->nb_norm = (int32_t)std::min<int64_t>(kNormBlocksMax, (n + 4 * kNormThreads - 1) / (4 * kNormThreads));
+    h->nb_norm = (int32_t)std::min<int64_t>(kNormBlocksMax, (n + 2 * kNormThreads - 1) / (2 * kNormThreads));
     hipError_t e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking);
     if (e != hipSuccess) {
         delete h;

@@ -21,8 +21,11 @@ struct LikConst {
     double d2;              // 2*(1-rho**2)
     double den, rden;       // 2*pi*sx*sy*sqrt(1-rho**2) and RN(1/den)
     double neg_nl_ln_den;   // -NL*log(den) (log-sum form)
+    double rsxsy, rd2;      // RN(1/(sx*sy)), RN(1/d2) (log-sum form)
     int32_t has_rho;
+    int32_t iso;            // sx2 == sy2 and rho == 0 (log-sum shortcut)
     int32_t nl;
+    int32_t pad;
 };
 
 struct PredictConst {

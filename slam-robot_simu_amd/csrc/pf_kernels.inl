@@ -136,30 +136,60 @@ __global__ __launch_bounds__(256) void pf_fused_kernel(
     // ---- likelihood: world2robot (mylib/transform.py:31-35) per landmark
     double sp, cp;
     sincos(kHalfPi - tn, &sp, &cp);
-    const double nsp = -sp;
-    double acc = 0.0;
     const int nl = lc.nl;
-    for (int j = 0; j < nl; ++j) {
-        const double dxw = lm[2 * j] - xn;
-        const double dyw = lm[2 * j + 1] - yn;
-        // OpenBLAS dgemm order for (rot @ diff.T): fma(r01, d1, r00*d0)
-        const double rx = fma(nsp, dyw, cp * dxw);
-        const double ry = fma(cp, dyw, sp * dxw);
-        const double dx = rx - z[2 * j];
-        const double dy = ry - z[2 * j + 1];
-        double q = div_refined(dx * dx, lc.sx2, lc.rsx2) + div_refined(dy * dy, lc.sy2, lc.rsy2);
-        if (lc.has_rho) q = q - ((lc.rho2 * dx) * dy) / lc.sxsy;
-        if (LIK == SLAM_LIK_PRODUCT) {
+    double bn;
+    if (LIK == SLAM_LIK_PRODUCT) {
+        // particle_filter.py:185-192 factor by factor, in NumPy's rounding order
+        double acc = 1.0;
+        for (int j = 0; j < nl; ++j) {
+            const double dxw = lm[2 * j] - xn;
+            const double dyw = lm[2 * j + 1] - yn;
+            // OpenBLAS dgemm order for (rot @ diff.T): fma(r01, d1, r00*d0)
+            const double rx = fma(-sp, dyw, cp * dxw);
+            const double ry = fma(cp, dyw, sp * dxw);
+            const double dx = rx - z[2 * j];
+            const double dy = ry - z[2 * j + 1];
+            double q = div_refined(dx * dx, lc.sx2, lc.rsx2) + div_refined(dy * dy, lc.sy2, lc.rsy2);
+            if (lc.has_rho) q = q - ((lc.rho2 * dx) * dy) / lc.sxsy;
             const double e = lc.has_rho ? exp((-q) / lc.d2) : exp((-q) * 0.5);  // d2 == 2 exactly
             const double f = div_refined(e, lc.den, lc.rden);
-            acc = (j == 0) ? f : acc * f;                     // ndarray.prod: left to right
-        } else {
-            acc = acc + q;
+            acc = (j == 0) ? f : acc * f;                 // ndarray.prod: left to right
+            // a zero running product stays zero (every factor is finite): stop
+            // once the whole wave has underflowed
+            if ((j & 7) == 7 && __all(acc == 0.0)) break;
         }
+        bn = acc;
+    } else {
+        // one exp per particle: prod_j exp(-q_j/d2)/den = exp(-sum_j q_j/d2 - NL ln den)
+        double S;
+        if (lc.iso) {
+            double acc = 0.0;
+#pragma unroll 4
+            for (int j = 0; j < nl; ++j) {
+                const double dxw = lm[2 * j] - xn;
+                const double dyw = lm[2 * j + 1] - yn;
+                const double dx = fma(cp, dxw, fma(-sp, dyw, -z[2 * j]));
+                const double dy = fma(sp, dxw, fma(cp, dyw, -z[2 * j + 1]));
+                acc = fma(dx, dx, acc);
+                acc = fma(dy, dy, acc);
+            }
+            S = acc * lc.rsx2;
+        } else {
+            double acc = 0.0;
+#pragma unroll 2
+            for (int j = 0; j < nl; ++j) {
+                const double dxw = lm[2 * j] - xn;
+                const double dyw = lm[2 * j + 1] - yn;
+                const double dx = fma(cp, dxw, fma(-sp, dyw, -z[2 * j]));
+                const double dy = fma(sp, dxw, fma(cp, dyw, -z[2 * j + 1]));
+                double q = fma(dx * lc.rsx2, dx, (dy * lc.rsy2) * dy);
+                if (lc.has_rho) q = q - ((lc.rho2 * dx) * dy) * lc.rsxsy;
+                acc = acc + q;
+            }
+            S = acc;
+        }
+        bn = exp(lc.has_rho ? fma(-S, lc.rd2, lc.neg_nl_ln_den) : fma(-0.5, S, lc.neg_nl_ln_den));
     }
-    double bn;
-    if (LIK == SLAM_LIK_PRODUCT) bn = (nl > 0) ? acc : 1.0;
-    else bn = exp((-acc) / lc.d2 + lc.neg_nl_ln_den);
     w_un[i] = pw * bn;                                           // particle_filter.py:194
 }
 
@@ -370,27 +400,44 @@ __global__ __launch_bounds__(kNormThreads) void normalize_kernel(
     const double r0 = refp[0], r1 = refp[1], r2 = refp[2];
     BlockPartial a;
     bp_zero(a);
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
-         i += (int64_t)gridDim.x * blockDim.x) {
-        double v = w_un[i] / s;                          // particle_filter.py:235
-        if (isnan(v)) v = np_recip;                      // :236
-        w[i] = v;
-        if (v > a.maxv) {
-            a.maxv = v;
-            a.maxi = gbase + i;
+    constexpr int U = 4;                                 // loads in flight per lane
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i0 < n; i0 += U * stride) {
+        double wu[U], xv[U], yv[U], tv[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t i = i0 + u * stride;
+            const bool ok = i < n;
+            wu[u] = ok ? w_un[i] : 0.0;
+            xv[u] = ok ? xs[i] : r0;
+            yv[u] = ok ? ys[i] : r1;
+            tv[u] = ok ? ts[i] : r2;
         }
-        a.sw += v;
-        a.sw2 += v * v;
-        const double d0 = xs[i] - r0, d1 = ys[i] - r1, d2 = ts[i] - r2;
-        a.m1[0] += v * d0;
-        a.m1[1] += v * d1;
-        a.m1[2] += v * d2;
-        a.m2[0] += v * d0 * d0;
-        a.m2[1] += v * d0 * d1;
-        a.m2[2] += v * d0 * d2;
-        a.m2[3] += v * d1 * d1;
-        a.m2[4] += v * d1 * d2;
-        a.m2[5] += v * d2 * d2;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t i = i0 + u * stride;
+            if (i >= n) break;
+            double v = wu[u] / s;                        // particle_filter.py:235
+            if (isnan(v)) v = np_recip;                  // :236
+            w[i] = v;
+            if (v > a.maxv) {
+                a.maxv = v;
+                a.maxi = gbase + i;
+            }
+            a.sw += v;
+            a.sw2 += v * v;
+            const double d0 = xv[u] - r0, d1 = yv[u] - r1, d2 = tv[u] - r2;
+            const double v0 = v * d0, v1 = v * d1, v2 = v * d2;
+            a.m1[0] += v0;
+            a.m1[1] += v1;
+            a.m1[2] += v2;
+            a.m2[0] += v0 * d0;
+            a.m2[1] += v0 * d1;
+            a.m2[2] += v0 * d2;
+            a.m2[3] += v1 * d1;
+            a.m2[4] += v1 * d2;
+            a.m2[5] += v2 * d2;
+        }
     }
     const BlockPartial r = bp_block_reduce(a, shp);
     if (threadIdx.x == 0) bp[blockIdx.x] = r;
@@ -409,9 +456,29 @@ __global__ __launch_bounds__(kNormThreads) void normalize_kernel(
 // ====================================================================
 // exact sequential cumsum (np.cumsum, particle_filter.py:212)
 // ====================================================================
-// S1: approximate block totals
+// exclusive scan of a small per-block array by one block of NT threads
+template <typename T, int NT>
+__device__ void block_scan_array(const T* in, T* out, const int nb, T* total, T* sh) {
+    const int per = (nb + NT - 1) / NT;
+    const int b0 = threadIdx.x * per;
+    T loc = T(0);
+    for (int k = 0; k < per; ++k)
+        if (b0 + k < nb) loc = loc + in[b0 + k];
+    T tot;
+    T ex = block_excl_scan<T, NT>(loc, sh, tot);
+    for (int k = 0; k < per; ++k)
+        if (b0 + k < nb) {
+            const T v = in[b0 + k];
+            out[b0 + k] = ex;
+            ex = ex + v;
+        }
+    if (threadIdx.x == 0 && total) *total = tot;
+}
+
+// S1: approximate block totals; the last block scans them into boff
 __global__ __launch_bounds__(kScanThreads) void scan_bsum_kernel(
     const double* __restrict__ w, const int64_t n, double* __restrict__ bsum,
+    double* __restrict__ boff, const double base_off, unsigned* __restrict__ counter,
     const int32_t* __restrict__ flags, const int32_t force) {
     if (!force && flags[kFlagResample] == 0) return;
     __shared__ double sh[kScanThreads / 64 + 1];
@@ -423,37 +490,22 @@ __global__ __launch_bounds__(kScanThreads) void scan_bsum_kernel(
     double tot;
     block_excl_scan<double, kScanThreads>(s, sh, tot);
     if (threadIdx.x == 0) bsum[blockIdx.x] = tot;
+    if (!arrive_last(counter)) return;
+    block_scan_array<double, kScanThreads>(bsum, boff, gridDim.x, (double*)nullptr, sh);
+    if (base_off != 0.0) {
+        __syncthreads();
+        for (int k = threadIdx.x; k < (int)gridDim.x; k += blockDim.x) boff[k] += base_off;
+    }
 }
 
-// S2/S4: single-block exclusive scan of per-block values
-template <typename T>
-__global__ __launch_bounds__(1024) void scan_top_kernel(const T* __restrict__ in, T* __restrict__ out,
-                                                        const int32_t nb, T* __restrict__ total,
-                                                        const int32_t* __restrict__ flags,
-                                                        const int32_t force) {
-    if (!force && flags[kFlagResample] == 0) return;
-    __shared__ T sh[1024 / 64 + 1];
-    const int per = (nb + 1023) / 1024;
-    const int b0 = threadIdx.x * per;
-    T loc = T(0);
-    for (int k = 0; k < per; ++k)
-        if (b0 + k < nb) loc = loc + in[b0 + k];
-    T tot;
-    T ex = block_excl_scan<T, 1024>(loc, sh, tot);
-    for (int k = 0; k < per; ++k)
-        if (b0 + k < nb) {
-            const T v = in[b0 + k];
-            out[b0 + k] = ex;
-            ex = ex + v;
-        }
-    if (threadIdx.x == 0 && total) *total = tot;
-}
-
-// S3: classify every element; k_i = increment on the run's ulp grid
+// S3: classify every element; k_i = increment on the run's ulp grid.  The last
+// block scans the per-block special counts and increment sums.
 __global__ __launch_bounds__(kScanThreads) void scan_classify_kernel(
     const double* __restrict__ w, const int64_t n, const double* __restrict__ boff,
     double* __restrict__ approx, uint64_t* __restrict__ kincl, int32_t* __restrict__ fexcl,
-    uint64_t* __restrict__ bk, int32_t* __restrict__ bf, const double delta, const int64_t gbase,
+    uint64_t* __restrict__ bk, int32_t* __restrict__ bf, uint64_t* __restrict__ boffk,
+    int32_t* __restrict__ bofff, uint64_t* __restrict__ ktot, int32_t* __restrict__ nspec,
+    const double delta, const int64_t gbase, unsigned* __restrict__ counter,
     const int32_t* __restrict__ flags, const int32_t force) {
     if (!force && flags[kFlagResample] == 0) return;
     __shared__ double shd[kScanThreads / 64 + 1];
@@ -498,10 +550,10 @@ __global__ __launch_bounds__(kScanThreads) void scan_classify_kernel(
         fsum += ff[k];
         if (base + k < n) approx[base + k] = run;
     }
-    uint64_t ktot;
-    int32_t ftot;
-    uint64_t kex = block_excl_scan<uint64_t, kScanThreads>(ksum, shk, ktot);
-    int32_t fex = block_excl_scan<int32_t, kScanThreads>(fsum, shf, ftot);
+    uint64_t ktot_b;
+    int32_t ftot_b;
+    uint64_t kex = block_excl_scan<uint64_t, kScanThreads>(ksum, shk, ktot_b);
+    int32_t fex = block_excl_scan<int32_t, kScanThreads>(fsum, shf, ftot_b);
 #pragma unroll
     for (int k = 0; k < kScanPer; ++k) {
         if (base + k < n) {
@@ -512,50 +564,25 @@ __global__ __launch_bounds__(kScanThreads) void scan_classify_kernel(
         }
     }
     if (threadIdx.x == 0) {
-        bk[blockIdx.x] = ktot;
-        bf[blockIdx.x] = ftot;
+        bk[blockIdx.x] = ktot_b;
+        bf[blockIdx.x] = ftot_b;
     }
+    if (!arrive_last(counter)) return;
+    block_scan_array<uint64_t, kScanThreads>(bk, boffk, gridDim.x, ktot, shk);
+    __syncthreads();
+    block_scan_array<int32_t, kScanThreads>(bf, bofff, gridDim.x, nspec, shf);
 }
 
-// S5: scatter the special elements into an ordered list
-__global__ __launch_bounds__(kScanThreads) void scan_emit_kernel(
-    const double* __restrict__ w, const int64_t n, const double* __restrict__ approx,
-    const uint64_t* __restrict__ kincl, const int32_t* __restrict__ fexcl,
-    const uint64_t* __restrict__ boffk, const int32_t* __restrict__ bofff,
-    SpecialIn* __restrict__ spec, const int64_t gbase, const int32_t* __restrict__ flags,
-    const int32_t force) {
-    if (!force && flags[kFlagResample] == 0) return;
-    const int64_t base = (int64_t)blockIdx.x * kScanBlock + threadIdx.x * kScanPer;
-    for (int k = 0; k < kScanPer; ++k) {
-        const int64_t i = base + k;
-        if (i >= n) break;
-        const int32_t f = fexcl[i];
-        if (f & 1) {
-            const int32_t m = bofff[blockIdx.x] + (f >> 1);
-            SpecialIn s;
-            s.idx = gbase + i;
-            s.P = boffk[blockIdx.x] + kincl[i];
-            s.w = w[i];
-            s.E = sum_binade(approx[i]);
-            s.pad = 0;
-            spec[m] = s;
-        }
-    }
-}
-
-// S6: sequential fold over the special elements (one block, tiles in LDS).
-// Falls back to a fully sequential cumsum if a run check fails.
-__global__ __launch_bounds__(256) void scan_serial_kernel(
-    const SpecialIn* __restrict__ spec, SpecialOut* __restrict__ out,
-    const int32_t* __restrict__ nspec_p, const uint64_t* __restrict__ ktotal_p,
-    const int64_t n_total, const double s_start, int32_t* __restrict__ flags,
-    const double* __restrict__ w, double* __restrict__ c, const int64_t n_local,
-    const int32_t force) {
-    if (!force && flags[kFlagResample] == 0) return;
+// S5: scatter the special elements into an ordered list; the last block then
+// folds them sequentially (S6) unless a separate serial pass follows
+// (multi-GPU: the list is gathered across ranks first).
+__device__ void serial_fold(const SpecialIn* __restrict__ spec, SpecialOut* __restrict__ out,
+                            const int32_t M, const uint64_t ktot, const int64_t n_total,
+                            const double s_start, int32_t* __restrict__ flags,
+                            const double* __restrict__ w, double* __restrict__ c,
+                            const int64_t n_local) {
     __shared__ SpecialIn tile[257];
     __shared__ int bad;
-    const int32_t M = *nspec_p;
-    const uint64_t ktot = *ktotal_p;
     double s = s_start;
     if (threadIdx.x == 0) {
         bad = 0;
@@ -604,6 +631,36 @@ __global__ __launch_bounds__(256) void scan_serial_kernel(
     } else if (threadIdx.x == 0) {
         flags[kFlagFallback] = 0;
     }
+}
+
+__global__ __launch_bounds__(kScanThreads) void scan_emit_kernel(
+    const double* __restrict__ w, const int64_t n, const double* __restrict__ approx,
+    const uint64_t* __restrict__ kincl, const int32_t* __restrict__ fexcl,
+    const uint64_t* __restrict__ boffk, const int32_t* __restrict__ bofff,
+    SpecialIn* __restrict__ spec, const int64_t gbase, SpecialOut* __restrict__ spec_out,
+    const int32_t* __restrict__ nspec_p, const uint64_t* __restrict__ ktot_p,
+    const int32_t do_fold, double* __restrict__ c, unsigned* __restrict__ counter,
+    int32_t* __restrict__ flags, const int32_t force) {
+    if (!force && flags[kFlagResample] == 0) return;
+    const int64_t base = (int64_t)blockIdx.x * kScanBlock + threadIdx.x * kScanPer;
+    for (int k = 0; k < kScanPer; ++k) {
+        const int64_t i = base + k;
+        if (i >= n) break;
+        const int32_t f = fexcl[i];
+        if (f & 1) {
+            const int32_t m = bofff[blockIdx.x] + (f >> 1);
+            SpecialIn s;
+            s.idx = gbase + i;
+            s.P = boffk[blockIdx.x] + kincl[i];
+            s.w = w[i];
+            s.E = sum_binade(approx[i]);
+            s.pad = 0;
+            spec[m] = s;
+        }
+    }
+    if (!do_fold) return;
+    if (!arrive_last(counter)) return;
+    serial_fold(spec, spec_out, *nspec_p, *ktot_p, n, 0.0, flags, w, c, n);
 }
 
 // S7: expand the exact cumsum from the specials
