@@ -111,10 +111,49 @@ int slam_pf_load_observations(slam_pf* h, int32_t n_steps, const double* z_all);
 int slam_pf_run(slam_pf* h, int32_t first_step, int32_t n_steps, const double* controls,
                 slam_pf_result* results);
 
-/* Kernel timing (HIP events on the handle's stream). kernel: 0 = fused
- * predict+likelihood, 1 = normalise, 2 = exact-cumsum+search, 3 = whole step. */
+/* Kernel timing (HIP events on the handle's stream; disables step graphs).
+ * kernel: 0 = fused resample-gather+predict+likelihood, 1 = np.sum order
+ * sums + normalise + reductions, 2 = exact-cumsum passes, 3 = whole step. */
 int slam_pf_enable_timing(slam_pf* h, int32_t on);
 int slam_pf_timing(slam_pf* h, int32_t kernel, double* total_ms, int64_t* launches);
+/* slam_pf_run replays one captured hipGraph per step (default on). */
+int slam_pf_set_graphs(slam_pf* h, int32_t on);
+/* Run on the caller's HIP stream (e.g. torch.cuda.current_stream()); NULL
+ * restores a private stream. */
+int slam_pf_set_stream(slam_pf* h, void* hip_stream);
+
+/* ====================================================================
+ * Sharded particle filter (BASELINE config 3): one handle per GPU holds
+ * particles [gbase, gbase + n_local) of a filter of n_global particles.
+ * The caller runs the phases in order and exchanges the small device
+ * buffers between ranks (slamhip/shard.py: torch.distributed / RCCL):
+ *   begin -> [scan_local -> A -> classify -> B(meta) -> export_specials ->
+ *   B(lists) -> fold -> plan -> export_items -> C -> import_items] ->
+ *   predict_update -> D -> normalize -> E -> finish
+ * Every rank ends with the same result, bit-identical to one GPU holding
+ * all n_global particles.  d_* arguments are device pointers.
+ * ==================================================================== */
+int slam_pf_create_shard(const slam_pf_config* cfg, int64_t n_local, int64_t n_global,
+                         int64_t gbase, int32_t n_landmarks, const double* landmarks, int device,
+                         slam_pf** out);
+/* out[4] = {np.sum buffers held locally, record bytes, special bytes, item bytes} */
+int slam_pf_shard_sizes(slam_pf* h, int64_t* out);
+int slam_pf_shard_begin(slam_pf* h, const double* control, const double* z, const double* noise,
+                        double u_resample, int32_t resample);
+int slam_pf_shard_scan_local(slam_pf* h, double* d_total);
+int slam_pf_shard_classify(slam_pf* h, const double* d_totals, int32_t rank, int32_t world,
+                           int64_t* d_meta);
+int slam_pf_shard_export_specials(slam_pf* h, int64_t count, void* d_dst);
+int slam_pf_shard_fold(slam_pf* h, const void* d_lists, int64_t cap, const int64_t* meta,
+                       int32_t world, int32_t rank);
+int slam_pf_shard_plan(slam_pf* h, const int64_t* gb, int32_t world, int64_t* send_counts);
+int slam_pf_shard_export_items(slam_pf* h, void* d_send);
+int slam_pf_shard_import_items(slam_pf* h, const void* d_recv, int64_t n_items);
+int slam_pf_shard_predict_update(slam_pf* h, double* d_partials);
+int slam_pf_shard_normalize(slam_pf* h, const double* d_all_partials, int64_t nparts,
+                            void* d_record);
+int slam_pf_shard_finish(slam_pf* h, const void* d_all_records, int32_t world,
+                         slam_pf_result* res);
 
 #ifdef __cplusplus
 }

@@ -1,15 +1,16 @@
 // pf_api.hip -- C-ABI of the particle filter (include/slam_hip.h).
 //
-// Replaces ParticleFilter (particle_filter.py:18-237).  One handle = one GPU,
-// one HIP stream, SoA particle state resident in HBM.
+// Replaces ParticleFilter (particle_filter.py:18-237).  One handle = one GPU
+// (or one shard of a multi-GPU filter), one HIP stream, SoA particle state
+// resident in HBM.
+#include <algorithm>
 #include <cmath>
 #include <cstring>
 #include <limits>
 #include <vector>
 
-#include "pf_kernels.hpp"
-
 #include "pf_kernels.inl"
+#include "pf_shard.inl"
 
 namespace slam {
 
@@ -40,16 +41,20 @@ using namespace slam;
 struct slam_pf {
     slam_pf_config cfg;
     int device = 0;
-    int64_t n = 0;
+    int64_t n = 0;            // local particles
+    int64_t n_global = 0;     // particles of the whole filter
+    int64_t gbase = 0;        // global index of local particle 0
     int32_t nl = 0;
     hipStream_t stream = nullptr;
+    bool own_stream = true;
+    std::vector<void*> allocs;
     // state (ping-pong)
     double* x[2] = {nullptr, nullptr};
     double* y[2] = {nullptr, nullptr};
     double* th[2] = {nullptr, nullptr};
     int cur = 0;
     double *w = nullptr, *w_un = nullptr;
-    // resample scratch
+    // exact cumsum scratch
     double* c = nullptr;
     uint64_t* kincl = nullptr;
     int32_t* fexcl = nullptr;
@@ -71,30 +76,41 @@ struct slam_pf {
     double* wsum = nullptr;
     double* refp = nullptr;
     int32_t* flags = nullptr;
-    unsigned* counters = nullptr;   // last-arriver tickets (zeroed by the last block)
-    // inputs
+    unsigned* counters = nullptr;   // last-arriver tickets (re-zeroed by the last block)
+    // inputs / step context
     double* lm = nullptr;
-    double* z = nullptr;
     double* noise = nullptr;
+    int32_t cap = 0;                // steps the StepIO arrays hold
+    double* ctl = nullptr;
     double* z_all = nullptr;
-    int32_t z_steps = 0;
+    double* ofs = nullptr;
     slam_pf_result* res_dev = nullptr;
-    int32_t res_cap = 0;
     slam_pf_result* res_host = nullptr;   // pinned
+    int32_t* ctr = nullptr;               // [0] step in batch, [1] RNG step
+    int32_t z_steps = 0;
     LikConst lc;
-    uint32_t stepno = 0;
+    PredictConst pc;
+    uint32_t stepno = 0;                  // host mirror of ctr[1]
     int32_t resample_next = 0;            // host mirror of the device flag
     bool timing = false;
+    bool use_graph = true;
+    hipGraphExec_t graph[2] = {nullptr, nullptr};
     Timer tm;
+    ShardScratch sh;
 };
 
 namespace {
 
-template <typename T>
-int dalloc(T** p, size_t count) {
-    if (count == 0) count = 1;
-    SLAM_HIP_TRY(hipMalloc((void**)p, count * sizeof(T)));
+int halloc(slam_pf* h, void** p, size_t bytes) {
+    if (bytes == 0) bytes = 8;
+    SLAM_HIP_TRY(hipMalloc(p, bytes));
+    h->allocs.push_back(*p);
     return SLAM_OK;
+}
+
+template <typename T>
+int dalloc(slam_pf* h, T** p, size_t count) {
+    return halloc(h, (void**)p, count * sizeof(T));
 }
 
 int make_lik_const(slam_pf* h) {
@@ -124,26 +140,26 @@ int make_lik_const(slam_pf* h) {
     return SLAM_OK;
 }
 
-PredictConst make_predict_const(slam_pf* h, const double* control) {
-    PredictConst pc;
+void make_predict_const(slam_pf* h) {
+    PredictConst& pc = h->pc;
     const slam_pf_config& c = h->cfg;
     pc.dt = c.dt;
-    pc.v = control[0];
-    pc.om = control[1];
-    pc.vdt_om = control[1] * c.dt;
-    // motion_model.py:40-45 (the std passed to normal() is the squared "sigma")
-    const double v2 = pc.v * pc.v, w2 = pc.om * pc.om;
-    const double sv = (c.alphas[0] * v2) + (c.alphas[1] * w2);
-    const double sw = (c.alphas[2] * v2) + (c.alphas[3] * w2);
-    const double sg = (c.alphas[4] * v2) + (c.alphas[5] * w2);
-    pc.sv = sv * sv;
-    pc.sw = sw * sw;
-    pc.sg = sg * sg;
+    for (int k = 0; k < 6; ++k) pc.alphas[k] = c.alphas[k];
     for (int k = 0; k < 9; ++k) pc.q[k] = c.q_factor[k];
-    pc.np_recip = 1.0 / (double)h->n;
-    pc.n_global = h->n;
-    pc.gbase = 0;
-    return pc;
+    pc.np_recip = 1.0 / (double)h->n_global;             // particle_filter.py:32
+    pc.rstep = 1.0 / (double)h->n_global;                // :213 arange step (= NP_RECIP)
+    pc.n_global = h->n_global;
+    pc.gbase = h->gbase;
+}
+
+StepIO step_io(slam_pf* h) {
+    StepIO io;
+    io.ctl = h->ctl;
+    io.z = h->z_all;
+    io.ofs = h->ofs;
+    io.res = h->res_dev;
+    io.ctr = h->ctr;
+    return io;
 }
 
 void tic(slam_pf* h, int k) {
@@ -167,51 +183,91 @@ void toc(slam_pf* h, int k) {
 
 inline unsigned grid_for(int64_t n, int bs) { return (unsigned)((n + bs - 1) / bs); }
 
-// Launch the exact-cumsum + search passes.  force=1: run regardless of the
-// device resample flag (stage/test entry points).
-int launch_resample(slam_pf* h, double u, int32_t force) {
+void drop_graphs(slam_pf* h) {
+    for (auto& g : h->graph)
+        if (g) {
+            (void)hipGraphExecDestroy(g);
+            g = nullptr;
+        }
+}
+
+void release(slam_pf* h, void* p) {
+    if (!p) return;
+    (void)hipFree(p);
+    h->allocs.erase(std::remove(h->allocs.begin(), h->allocs.end(), p), h->allocs.end());
+}
+
+// (Re)allocate the StepIO arrays for `steps` steps.
+int ensure_steps(slam_pf* h, int32_t steps) {
+    if (steps <= h->cap) return SLAM_OK;
+    drop_graphs(h);
+    release(h, h->ctl);
+    release(h, h->z_all);
+    release(h, h->ofs);
+    release(h, h->res_dev);
+    if (h->res_host) (void)hipHostFree(h->res_host);
+    h->res_host = nullptr;
+    int rc;
+    const size_t nlz = 2 * (size_t)std::max<int32_t>(h->nl, 1);
+    if ((rc = dalloc(h, &h->ctl, 2 * (size_t)steps)) || (rc = dalloc(h, &h->z_all, nlz * steps)) ||
+        (rc = dalloc(h, &h->ofs, (size_t)steps)) || (rc = dalloc(h, &h->res_dev, (size_t)steps)))
+        return rc;
+    SLAM_HIP_TRY(hipHostMalloc((void**)&h->res_host, sizeof(slam_pf_result) * steps));
+    h->cap = steps;
+    h->z_steps = 0;
+    return SLAM_OK;
+}
+
+int set_ctr(slam_pf* h, int32_t step) {
+    const int32_t v[2] = {step, (int32_t)h->stepno};
+    SLAM_HIP_TRY(hipMemcpyAsync(h->ctr, v, sizeof(v), hipMemcpyHostToDevice, h->stream));
+    return SLAM_OK;
+}
+
+int set_flag(slam_pf* h, int word, int32_t v) {
+    SLAM_HIP_TRY(hipMemcpyAsync(h->flags + word, &v, sizeof(int32_t), hipMemcpyHostToDevice,
+                                h->stream));
+    return SLAM_OK;
+}
+
+// Exact-cumsum passes S1..S7.  force=0: they gate on the device resample flag.
+int launch_scans(slam_pf* h, int32_t force) {
     const int64_t n = h->n;
     const int nb = h->nb_scan;
     hipStream_t s = h->stream;
-    const double delta = 4.0 * (double)n * 0x1p-53 + 0x1p-45;
-    tic(h, 2);
-    scan_bsum_kernel<<<nb, kScanThreads, 0, s>>>(h->w, n, h->bsum, h->boff, 0.0, h->counters + 2,
+    const double delta = 4.0 * (double)h->n_global * 0x1p-53 + 0x1p-45;
+    scan_bsum_kernel<<<nb, kScanThreads, 0, s>>>(h->w, n, h->bsum, h->boff, h->counters + 2,
                                                  h->flags, force);
-    scan_classify_kernel<<<nb, kScanThreads, 0, s>>>(h->w, n, h->boff, h->c, h->kincl, h->fexcl,
-                                                     h->bk, h->bf, h->boffk, h->bofff, h->ktot,
-                                                     h->nspec, delta, 0, h->counters + 2, h->flags,
-                                                     force);
+    scan_classify_kernel<<<nb, kScanThreads, 0, s>>>(
+        h->w, n, h->boff, nullptr, h->c, h->kincl, h->fexcl, h->bk, h->bf, h->boffk, h->bofff,
+        h->ktot, h->nspec, delta, 0, h->counters + 2, h->flags, force);
     scan_emit_kernel<<<nb, kScanThreads, 0, s>>>(h->w, n, h->c, h->kincl, h->fexcl, h->boffk,
                                                  h->bofff, h->spec_in, 0, h->spec_out, h->nspec,
                                                  h->ktot, 1, h->c, h->counters + 2, h->flags,
                                                  force);
     scan_expand_kernel<<<nb, kScanThreads, 0, s>>>(n, h->kincl, h->fexcl, h->boffk, h->bofff,
-                                                   h->spec_out, h->c, h->flags, force);
-    const double step = 1.0 / (double)n;                      // particle_filter.py:213
-    const double ofs = std::isnan(u) ? u : u * (1.0 / (double)n);   // :214
-    resample_search_kernel<<<grid_for(n, 256), 256, 0, s>>>(n, h->c, h->idx, step, ofs,
-                                                           1.0 / (double)n, h->cfg.seed,
-                                                           h->stepno, h->flags, force);
-    toc(h, 2);
+                                                   h->spec_out, h->c, h->flags, nullptr,
+                                                   nullptr, force);
     SLAM_HIP_TRY(hipGetLastError());
     return SLAM_OK;
 }
 
-int launch_fused(slam_pf* h, const PredictConst& pc, const double* z_dev, bool host_noise) {
+int launch_fused(slam_pf* h, int motion, bool host_noise) {
     const int64_t n = h->n;
     const int src = h->cur, dst = 1 - h->cur;
     hipStream_t s = h->stream;
     const unsigned g = grid_for(n, 256);
-    const int mot = h->cfg.motion, lik = h->cfg.likelihood;
+    const int lik = h->cfg.likelihood;
+    const StepIO io = step_io(h);
     tic(h, 0);
 #define SLAM_FUSED(M, L, HN)                                                                     \
     pf_fused_kernel<M, L, HN><<<g, 256, 0, s>>>(n, h->x[src], h->y[src], h->th[src], h->x[dst], \
-                                                h->y[dst], h->th[dst], h->w, h->w_un, h->idx,    \
-                                                h->flags, h->noise, h->lm, z_dev, pc, h->lc,     \
-                                                h->cfg.seed, h->stepno)
-    if (mot == kMotionNone) {
+                                                h->y[dst], h->th[dst], h->w, h->w_un, h->c,      \
+                                                h->flags, h->noise, h->lm, io, h->pc, h->lc,     \
+                                                h->cfg.seed)
+    if (motion == kMotionNone) {
         if (lik == SLAM_LIK_PRODUCT) SLAM_FUSED(2, 0, false); else SLAM_FUSED(2, 1, false);
-    } else if (mot == SLAM_MOTION_LINEAR) {
+    } else if (motion == SLAM_MOTION_LINEAR) {
         if (lik == SLAM_LIK_PRODUCT) {
             if (host_noise) SLAM_FUSED(0, 0, true); else SLAM_FUSED(0, 0, false);
         } else {
@@ -231,37 +287,35 @@ int launch_fused(slam_pf* h, const PredictConst& pc, const double* z_dev, bool h
     return SLAM_OK;
 }
 
-// numpy-order sum + normalise + reductions + result into res_dev[slot]
-int launch_reduce(slam_pf* h, const double* w_src, int slot, int32_t resampled_known) {
+// numpy-order sum + normalise + reductions + result record res[ctr[0]]
+int launch_reduce(slam_pf* h, int32_t resampled_known) {
     const int64_t n = h->n;
     hipStream_t s = h->stream;
     const int c = h->cur;
     tic(h, 1);
-    chunk_sum_kernel<<<h->nchunks, 512, 0, s>>>(w_src, n, h->part, h->tail_leaves, h->tail_ops,
+    chunk_sum_kernel<<<h->nchunks, 512, 0, s>>>(h->w_un, n, h->part, h->tail_leaves, h->tail_ops,
                                                  h->n_tail_leaves, h->n_tail_ops, h->counters,
                                                  h->wsum);
     normalize_kernel<<<h->nb_norm, kNormThreads, 0, s>>>(
-        n, w_src, h->w, h->wsum, 1.0 / (double)n, h->x[c], h->y[c], h->th[c], h->refp, h->bp,
-        h->counters + 1, h->flags, h->cfg.ess_threshold, h->res_dev + slot, resampled_known, 0);
+        n, h->w_un, h->w, h->wsum, h->pc.np_recip, h->x[c], h->y[c], h->th[c], h->refp, h->bp,
+        h->counters + 1, h->flags, h->cfg.ess_threshold, step_io(h), 1, resampled_known, 0);
     toc(h, 1);
     SLAM_HIP_TRY(hipGetLastError());
     return SLAM_OK;
 }
 
-int ensure_results(slam_pf* h, int32_t cap) {
-    if (cap <= h->res_cap) return SLAM_OK;
-    if (h->res_dev) (void)hipFree(h->res_dev);
-    if (h->res_host) (void)hipHostFree(h->res_host);
-    h->res_dev = nullptr;
-    h->res_host = nullptr;
-    SLAM_HIP_TRY(hipMalloc((void**)&h->res_dev, sizeof(slam_pf_result) * cap));
-    SLAM_HIP_TRY(hipHostMalloc((void**)&h->res_host, sizeof(slam_pf_result) * cap));
-    h->res_cap = cap;
-    return SLAM_OK;
+// One whole device-decided step (scans gate on the flag; no host decision).
+int launch_step(slam_pf* h, bool host_noise) {
+    int rc;
+    tic(h, 2);
+    if ((rc = launch_scans(h, 0))) return rc;
+    toc(h, 2);
+    if ((rc = launch_fused(h, h->cfg.motion, host_noise))) return rc;
+    return launch_reduce(h, -1);
 }
 
-int sync_and_status(slam_pf* h, int32_t count, slam_pf_result* out) {
-    SLAM_HIP_TRY(hipMemcpyAsync(h->res_host, h->res_dev, sizeof(slam_pf_result) * count,
+int sync_results(slam_pf* h, int32_t first, int32_t count, slam_pf_result* out) {
+    SLAM_HIP_TRY(hipMemcpyAsync(h->res_host, h->res_dev + first, sizeof(slam_pf_result) * count,
                                 hipMemcpyDeviceToHost, h->stream));
     SLAM_HIP_TRY(hipStreamSynchronize(h->stream));
     int rc = SLAM_OK;
@@ -275,21 +329,12 @@ int sync_and_status(slam_pf* h, int32_t count, slam_pf_result* out) {
     return rc;
 }
 
-int set_flag(slam_pf* h, int word, int32_t v) {
-    SLAM_HIP_TRY(hipMemcpyAsync(h->flags + word, &v, sizeof(int32_t), hipMemcpyHostToDevice,
-                                h->stream));
-    return SLAM_OK;
-}
-
-}  // namespace
-
-extern "C" {
-
-int slam_pf_create(const slam_pf_config* cfg, int64_t n_particles, int32_t n_landmarks,
-                   const double* landmarks, int device, slam_pf** out) {
+int create_impl(const slam_pf_config* cfg, int64_t n_local, int64_t n_global, int64_t gbase,
+                int32_t n_landmarks, const double* landmarks, int device, slam_pf** out) {
     SLAM_ARG_CHECK(cfg && out, "slam_pf_create: NULL argument");
-    SLAM_ARG_CHECK(n_particles > 0 && n_particles < (int64_t(1) << 31),
-                   "slam_pf_create: n_particles must be in [1, 2^31)");
+    SLAM_ARG_CHECK(n_local > 0 && n_global < (int64_t(1) << 31) && gbase >= 0 &&
+                       gbase + n_local <= n_global,
+                   "slam_pf_create: need 0 < n_local, gbase + n_local <= n_global < 2^31");
     SLAM_ARG_CHECK(n_landmarks >= 0, "slam_pf_create: n_landmarks < 0");
     SLAM_ARG_CHECK(n_landmarks == 0 || landmarks, "slam_pf_create: landmarks is NULL");
     SLAM_ARG_CHECK(cfg->motion == SLAM_MOTION_LINEAR || cfg->motion == SLAM_MOTION_VELOCITY,
@@ -304,14 +349,17 @@ int slam_pf_create(const slam_pf_config* cfg, int64_t n_particles, int32_t n_lan
     slam_pf* h = new slam_pf();
     h->cfg = *cfg;
     h->device = device;
-    h->n = n_particles;
+    h->n = n_local;
+    h->n_global = n_global;
+    h->gbase = gbase;
     h->nl = n_landmarks;
     int rc = make_lik_const(h);
     if (rc) {
         delete h;
         return rc;
     }
-    const int64_t n = n_particles;
+    make_predict_const(h);
+    const int64_t n = n_local;
     h->nb_scan = (int32_t)((n + kScanBlock - 1) / kScanBlock);
     h->nchunks = (int32_t)((n + kSumChunk - 1) / kSumChunk);
     h->nb_norm = (int32_t)std::min<int64_t>(kNormBlocksMax, (n + 2 * kNormThreads - 1) / (2 * kNormThreads));
@@ -320,10 +368,10 @@ int slam_pf_create(const slam_pf_config* cfg, int64_t n_particles, int32_t n_lan
         delete h;
         return fail(SLAM_ERR_HIP, std::string("hipStreamCreate: ") + hipGetErrorString(e));
     }
-#define A(p, cnt)                                   \
-    if ((rc = dalloc(&(p), (size_t)(cnt))) != 0) { \
-        slam_pf_destroy(h);                         \
-        return rc;                                  \
+#define A(p, cnt)                                         \
+    if ((rc = dalloc(h, &(p), (size_t)(cnt))) != 0) {     \
+        slam_pf_destroy(h);                               \
+        return rc;                                        \
     }
     for (int k = 0; k < 2; ++k) {
         A(h->x[k], n);
@@ -337,7 +385,7 @@ int slam_pf_create(const slam_pf_config* cfg, int64_t n_particles, int32_t n_lan
     A(h->fexcl, n);
     A(h->idx, n);
     A(h->bsum, h->nb_scan);
-    A(h->boff, h->nb_scan);
+    A(h->boff, h->nb_scan + 1);
     A(h->bk, h->nb_scan);
     A(h->boffk, h->nb_scan);
     A(h->bf, h->nb_scan);
@@ -351,28 +399,24 @@ int slam_pf_create(const slam_pf_config* cfg, int64_t n_particles, int32_t n_lan
     A(h->wsum, 1);
     A(h->refp, 4);
     A(h->flags, kFlagWords);
-    A(h->counters, 4);
+    A(h->counters, 8);
     A(h->lm, 2 * std::max<int32_t>(n_landmarks, 1));
-    A(h->z, 2 * std::max<int32_t>(n_landmarks, 1));
     A(h->noise, 3 * n);
+    A(h->ctr, 4);
 #undef A
-    // tail program for the last np.sum buffer
     std::vector<int32_t> leaves, ops;
     const int tail = (int)(n % kSumChunk);
     if (tail) build_tail(0, tail, leaves, ops);
     h->n_tail_leaves = (int32_t)(leaves.size() / 2);
     h->n_tail_ops = (int32_t)ops.size();
-    if ((rc = dalloc(&h->tail_leaves, leaves.size() + 2)) || (rc = dalloc(&h->tail_ops, ops.size() + 1))) {
+    if ((rc = dalloc(h, &h->tail_leaves, leaves.size() + 2)) ||
+        (rc = dalloc(h, &h->tail_ops, ops.size() + 1)) || (rc = ensure_steps(h, 1))) {
         slam_pf_destroy(h);
         return rc;
     }
     if (tail) {
         SLAM_HIP_TRY(hipMemcpy(h->tail_leaves, leaves.data(), leaves.size() * 4, hipMemcpyHostToDevice));
         SLAM_HIP_TRY(hipMemcpy(h->tail_ops, ops.data(), ops.size() * 4, hipMemcpyHostToDevice));
-    }
-    if ((rc = ensure_results(h, 1))) {
-        slam_pf_destroy(h);
-        return rc;
     }
     // initial state: particle_filter.py:81-84
     std::vector<double> tmp((size_t)n);
@@ -381,36 +425,84 @@ int slam_pf_create(const slam_pf_config* cfg, int64_t n_particles, int32_t n_lan
         double* d = (k == 0) ? h->x[0] : (k == 1) ? h->y[0] : h->th[0];
         SLAM_HIP_TRY(hipMemcpy(d, tmp.data(), n * sizeof(double), hipMemcpyHostToDevice));
     }
-    std::fill(tmp.begin(), tmp.end(), 1.0 / (double)n);
+    std::fill(tmp.begin(), tmp.end(), 1.0 / (double)n_global);
     SLAM_HIP_TRY(hipMemcpy(h->w, tmp.data(), n * sizeof(double), hipMemcpyHostToDevice));
     SLAM_HIP_TRY(hipMemcpy(h->refp, cfg->x0, 3 * sizeof(double), hipMemcpyHostToDevice));
     SLAM_HIP_TRY(hipMemset(h->flags, 0, kFlagWords * sizeof(int32_t)));
-    SLAM_HIP_TRY(hipMemset(h->counters, 0, 4 * sizeof(unsigned)));
+    SLAM_HIP_TRY(hipMemset(h->counters, 0, 8 * sizeof(unsigned)));
+    SLAM_HIP_TRY(hipMemset(h->ctr, 0, 4 * sizeof(int32_t)));
     if (n_landmarks > 0)
         SLAM_HIP_TRY(hipMemcpy(h->lm, landmarks, 2 * n_landmarks * sizeof(double), hipMemcpyHostToDevice));
     *out = h;
     return SLAM_OK;
 }
 
+// stage one sync-mode step's inputs into StepIO slot 0
+int stage_inputs(slam_pf* h, const double* control, const double* z, const double* noise,
+                 double u) {
+    if (h->nl && z)
+        SLAM_HIP_TRY(hipMemcpyAsync(h->z_all, z, 2 * h->nl * sizeof(double), hipMemcpyHostToDevice,
+                                    h->stream));
+    SLAM_HIP_TRY(hipMemcpyAsync(h->ctl, control, 2 * sizeof(double), hipMemcpyHostToDevice, h->stream));
+    h->sh.ofs_host = std::isnan(u) ? u : u * h->pc.np_recip;           // particle_filter.py:214
+    SLAM_HIP_TRY(hipMemcpyAsync(h->ofs, &h->sh.ofs_host, sizeof(double), hipMemcpyHostToDevice, h->stream));
+    if (noise)
+        SLAM_HIP_TRY(hipMemcpyAsync(h->noise, noise, 3 * h->n * sizeof(double),
+                                    hipMemcpyHostToDevice, h->stream));
+    h->z_steps = 0;   // slot 0 now holds a single staged step
+    return set_ctr(h, 0);
+}
+
+}  // namespace
+
+#include "pf_shard_api.inl"
+
+extern "C" {
+
+int slam_pf_create(const slam_pf_config* cfg, int64_t n_particles, int32_t n_landmarks,
+                   const double* landmarks, int device, slam_pf** out) {
+    return create_impl(cfg, n_particles, n_particles, 0, n_landmarks, landmarks, device, out);
+}
+
+int slam_pf_create_shard(const slam_pf_config* cfg, int64_t n_local, int64_t n_global,
+                         int64_t gbase, int32_t n_landmarks, const double* landmarks, int device,
+                         slam_pf** out) {
+    SLAM_ARG_CHECK(n_local % kSumChunk == 0 || gbase + n_local == n_global,
+                   "slam_pf_create_shard: every shard but the last must hold a multiple of 8192 "
+                   "particles (np.sum buffer alignment)");
+    return create_impl(cfg, n_local, n_global, gbase, n_landmarks, landmarks, device, out);
+}
+
 int slam_pf_destroy(slam_pf* h) {
     if (!h) return SLAM_OK;
     (void)hipSetDevice(h->device);
     if (h->stream) (void)hipStreamSynchronize(h->stream);
-    void* ptrs[] = {h->x[0], h->x[1], h->y[0], h->y[1], h->th[0], h->th[1], h->w, h->w_un,
-                    h->c, h->kincl, h->fexcl, h->idx, h->bsum, h->boff, h->bk, h->boffk,
-                    h->bf, h->bofff, h->ktot, h->nspec, h->spec_in, h->spec_out, h->part,
-                    h->tail_leaves, h->tail_ops, h->bp, h->wsum, h->refp, h->flags, h->counters, h->lm,
-                    h->z, h->noise, h->z_all, h->res_dev};
-    for (void* p : ptrs)
-        if (p) (void)hipFree(p);
+    drop_graphs(h);
+    for (void* p : h->allocs) (void)hipFree(p);
     if (h->res_host) (void)hipHostFree(h->res_host);
     for (int k = 0; k < 4; ++k)
         for (auto& pr : h->tm.ev[k]) {
             (void)hipEventDestroy(pr.first);
             (void)hipEventDestroy(pr.second);
         }
-    if (h->stream) (void)hipStreamDestroy(h->stream);
+    if (h->stream && h->own_stream) (void)hipStreamDestroy(h->stream);
     delete h;
+    return SLAM_OK;
+}
+
+int slam_pf_set_stream(slam_pf* h, void* stream) {
+    SLAM_ARG_CHECK(h, "slam_pf_set_stream: NULL handle");
+    SLAM_HIP_TRY(hipSetDevice(h->device));
+    SLAM_HIP_TRY(hipStreamSynchronize(h->stream));
+    drop_graphs(h);
+    if (h->own_stream) (void)hipStreamDestroy(h->stream);
+    if (stream) {
+        h->stream = (hipStream_t)stream;
+        h->own_stream = false;
+    } else {
+        SLAM_HIP_TRY(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
+        h->own_stream = true;
+    }
     return SLAM_OK;
 }
 
@@ -435,12 +527,15 @@ int slam_pf_set_state(slam_pf* h, const double* x, const double* y, const double
     if (th) SLAM_HIP_TRY(hipMemcpyAsync(h->th[c], th, b, hipMemcpyHostToDevice, h->stream));
     if (w) {
         SLAM_HIP_TRY(hipMemcpyAsync(h->w, w, b, hipMemcpyHostToDevice, h->stream));
-        // particle_filter.py:210-211: recompute the resample decision from these weights
-        double s2 = 0.0;
-        for (int64_t i = 0; i < h->n; ++i) s2 += w[i] * w[i];
-        h->resample_next = (1.0 / s2 < h->cfg.ess_threshold) ? 1 : 0;
-        int rc = set_flag(h, kFlagResample, h->resample_next);
-        if (rc) return rc;
+        // particle_filter.py:210-211: the resample decision from these weights
+        // (single GPU; a shard's caller decides from the global ESS)
+        if (h->n == h->n_global) {
+            double s2 = 0.0;
+            for (int64_t i = 0; i < h->n; ++i) s2 += w[i] * w[i];
+            h->resample_next = (1.0 / s2 < h->cfg.ess_threshold) ? 1 : 0;
+            int rc = set_flag(h, kFlagResample, h->resample_next);
+            if (rc) return rc;
+        }
     }
     SLAM_HIP_TRY(hipStreamSynchronize(h->stream));
     return SLAM_OK;
@@ -462,38 +557,40 @@ int slam_pf_get_state(slam_pf* h, double* x, double* y, double* th, double* w) {
 int slam_pf_step(slam_pf* h, const double* control, const double* z, const double* noise,
                  double u_resample, slam_pf_result* res) {
     SLAM_ARG_CHECK(h && control && (z || h->nl == 0), "slam_pf_step: NULL argument");
+    SLAM_ARG_CHECK(h->n == h->n_global, "slam_pf_step: sharded handle (use the shard entry points)");
     SLAM_HIP_TRY(hipSetDevice(h->device));
     int rc;
-    if ((rc = ensure_results(h, 1))) return rc;
+    if ((rc = stage_inputs(h, control, z, noise, u_resample))) return rc;
     tic(h, 3);
-    if (h->nl)
-        SLAM_HIP_TRY(hipMemcpyAsync(h->z, z, 2 * h->nl * sizeof(double), hipMemcpyHostToDevice,
-                                    h->stream));
-    if (noise)
-        SLAM_HIP_TRY(hipMemcpyAsync(h->noise, noise, 3 * h->n * sizeof(double),
-                                    hipMemcpyHostToDevice, h->stream));
     const int32_t resampling = h->resample_next;
-    if (resampling && (rc = launch_resample(h, u_resample, 0))) return rc;
-    PredictConst pc = make_predict_const(h, control);
-    if ((rc = launch_fused(h, pc, h->z, noise != nullptr))) return rc;
-    if ((rc = launch_reduce(h, h->w_un, 0, resampling))) return rc;
+    if (resampling) {
+        tic(h, 2);
+        if ((rc = launch_scans(h, 1))) return rc;
+        toc(h, 2);
+    }
+    if ((rc = launch_fused(h, h->cfg.motion, noise != nullptr))) return rc;
+    if ((rc = launch_reduce(h, resampling))) return rc;
     toc(h, 3);
     h->stepno++;
-    return sync_and_status(h, 1, res);
+    return sync_results(h, 0, 1, res);
 }
 
 int slam_pf_resample(slam_pf* h, double u_resample, int32_t force, int32_t* resampled) {
     SLAM_ARG_CHECK(h, "slam_pf_resample: NULL handle");
+    SLAM_ARG_CHECK(h->n == h->n_global, "slam_pf_resample: sharded handle");
     SLAM_HIP_TRY(hipSetDevice(h->device));
     const int32_t go = force ? 1 : h->resample_next;
     if (resampled) *resampled = go;
     if (!go) return SLAM_OK;
-    int rc = launch_resample(h, u_resample, 1);
+    int rc = launch_scans(h, 1);
     if (rc) return rc;
+    const double ofs = std::isnan(u_resample) ? u_resample : u_resample * h->pc.np_recip;
+    resample_search_kernel<<<grid_for(h->n, 256), 256, 0, h->stream>>>(
+        h->n, h->c, h->idx, h->pc.rstep, ofs, h->pc.np_recip, h->cfg.seed, h->stepno, h->flags);
     const int src = h->cur, dst = 1 - h->cur;
     gather_kernel<<<grid_for(h->n, 256), 256, 0, h->stream>>>(
         h->n, h->idx, h->x[src], h->y[src], h->th[src], h->x[dst], h->y[dst], h->th[dst], h->w,
-        1.0 / (double)h->n);
+        h->pc.np_recip);
     SLAM_HIP_TRY(hipGetLastError());
     h->cur = dst;
     int32_t st = 0;
@@ -510,9 +607,14 @@ int slam_pf_resample(slam_pf* h, double u_resample, int32_t force, int32_t* resa
 
 int slam_pf_resample_indices(slam_pf* h, double u_resample, int64_t* idx_out, int32_t* n_special) {
     SLAM_ARG_CHECK(h && idx_out, "slam_pf_resample_indices: NULL argument");
+    SLAM_ARG_CHECK(h->n == h->n_global, "slam_pf_resample_indices: sharded handle");
     SLAM_HIP_TRY(hipSetDevice(h->device));
-    int rc = launch_resample(h, u_resample, 1);
+    int rc = launch_scans(h, 1);
     if (rc) return rc;
+    const double ofs = std::isnan(u_resample) ? u_resample : u_resample * h->pc.np_recip;
+    resample_search_kernel<<<grid_for(h->n, 256), 256, 0, h->stream>>>(
+        h->n, h->c, h->idx, h->pc.rstep, ofs, h->pc.np_recip, h->cfg.seed, h->stepno, h->flags);
+    SLAM_HIP_TRY(hipGetLastError());
     std::vector<int32_t> idx((size_t)h->n);
     int32_t fl[kFlagWords];
     SLAM_HIP_TRY(hipMemcpyAsync(idx.data(), h->idx, h->n * 4, hipMemcpyDeviceToHost, h->stream));
@@ -531,17 +633,14 @@ int slam_pf_resample_indices(slam_pf* h, double u_resample, int64_t* idx_out, in
 int slam_pf_predict(slam_pf* h, const double* control, const double* noise) {
     SLAM_ARG_CHECK(h && control, "slam_pf_predict: NULL argument");
     SLAM_HIP_TRY(hipSetDevice(h->device));
-    // predict-only = fused kernel with zero landmarks and no resample gather;
-    // weights are carried through unchanged (w_un = w * 1).
-    if (noise)
-        SLAM_HIP_TRY(hipMemcpyAsync(h->noise, noise, 3 * h->n * sizeof(double),
-                                    hipMemcpyHostToDevice, h->stream));
-    int rc = set_flag(h, kFlagResample, 0);
-    if (rc) return rc;
+    // predict only: fused kernel with zero landmarks and no resample gather;
+    // the weights pass through unchanged (w_un = w * 1).
+    int rc;
+    if ((rc = stage_inputs(h, control, nullptr, noise, std::nan("")))) return rc;
+    if ((rc = set_flag(h, kFlagResample, 0))) return rc;
     const int32_t nl = h->lc.nl;
     h->lc.nl = 0;
-    PredictConst pc = make_predict_const(h, control);
-    rc = launch_fused(h, pc, h->z, noise != nullptr);
+    rc = launch_fused(h, h->cfg.motion, noise != nullptr);
     h->lc.nl = nl;
     if (rc) return rc;
     SLAM_HIP_TRY(hipMemcpyAsync(h->w, h->w_un, h->n * 8, hipMemcpyDeviceToDevice, h->stream));
@@ -554,22 +653,15 @@ int slam_pf_predict(slam_pf* h, const double* control, const double* noise) {
 int slam_pf_update(slam_pf* h, const double* z, slam_pf_result* res) {
     // __likelihood + estimate on the current particles (no motion, no resample)
     SLAM_ARG_CHECK(h && (z || h->nl == 0), "slam_pf_update: NULL argument");
+    SLAM_ARG_CHECK(h->n == h->n_global, "slam_pf_update: sharded handle");
     SLAM_HIP_TRY(hipSetDevice(h->device));
     int rc;
-    if ((rc = ensure_results(h, 1))) return rc;
-    if (h->nl)
-        SLAM_HIP_TRY(hipMemcpyAsync(h->z, z, 2 * h->nl * sizeof(double), hipMemcpyHostToDevice,
-                                    h->stream));
-    if ((rc = set_flag(h, kFlagResample, 0))) return rc;
-    const int32_t saved = h->cfg.motion;
-    h->cfg.motion = kMotionNone;
     const double ctl[2] = {0.0, 0.0};
-    PredictConst pc = make_predict_const(h, ctl);
-    rc = launch_fused(h, pc, h->z, false);
-    h->cfg.motion = saved;
-    if (rc) return rc;
-    if ((rc = launch_reduce(h, h->w_un, 0, 0))) return rc;
-    return sync_and_status(h, 1, res);
+    if ((rc = stage_inputs(h, ctl, z, nullptr, std::nan("")))) return rc;
+    if ((rc = set_flag(h, kFlagResample, 0))) return rc;
+    if ((rc = launch_fused(h, kMotionNone, false))) return rc;
+    if ((rc = launch_reduce(h, 0))) return rc;
+    return sync_results(h, 0, 1, res);
 }
 
 int slam_pf_weight_sum(slam_pf* h, double* sum_out) {
@@ -577,27 +669,25 @@ int slam_pf_weight_sum(slam_pf* h, double* sum_out) {
     SLAM_HIP_TRY(hipSetDevice(h->device));
     chunk_sum_kernel<<<h->nchunks, 512, 0, h->stream>>>(h->w, h->n, h->part, h->tail_leaves,
                                                          h->tail_ops, h->n_tail_leaves,
-                                                         h->n_tail_ops, h->counters, nullptr);
+                                                         h->n_tail_ops, h->counters, h->wsum);
     SLAM_HIP_TRY(hipGetLastError());
-    std::vector<double> p((size_t)h->nchunks);
-    SLAM_HIP_TRY(hipMemcpyAsync(p.data(), h->part, h->nchunks * 8, hipMemcpyDeviceToHost, h->stream));
+    SLAM_HIP_TRY(hipMemcpyAsync(sum_out, h->wsum, 8, hipMemcpyDeviceToHost, h->stream));
     SLAM_HIP_TRY(hipStreamSynchronize(h->stream));
-    double s = 0.0;
-    for (double v : p) s = s + v;
-    *sum_out = s;
     return SLAM_OK;
 }
 
 int slam_pf_load_observations(slam_pf* h, int32_t n_steps, const double* z_all) {
     SLAM_ARG_CHECK(h && n_steps > 0 && (z_all || h->nl == 0), "slam_pf_load_observations: bad argument");
     SLAM_HIP_TRY(hipSetDevice(h->device));
-    if (h->z_all) (void)hipFree(h->z_all);
-    h->z_all = nullptr;
-    const size_t cnt = (size_t)n_steps * 2 * std::max<int32_t>(h->nl, 1);
-    SLAM_HIP_TRY(hipMalloc((void**)&h->z_all, cnt * sizeof(double)));
+    int rc = ensure_steps(h, n_steps);
+    if (rc) return rc;
     if (h->nl)
-        SLAM_HIP_TRY(hipMemcpy(h->z_all, z_all, (size_t)n_steps * 2 * h->nl * sizeof(double),
-                               hipMemcpyHostToDevice));
+        SLAM_HIP_TRY(hipMemcpyAsync(h->z_all, z_all, (size_t)n_steps * 2 * h->nl * sizeof(double),
+                                    hipMemcpyHostToDevice, h->stream));
+    std::vector<double> nan((size_t)n_steps, std::nan(""));
+    SLAM_HIP_TRY(hipMemcpyAsync(h->ofs, nan.data(), n_steps * sizeof(double), hipMemcpyHostToDevice,
+                                h->stream));
+    SLAM_HIP_TRY(hipStreamSynchronize(h->stream));
     h->z_steps = n_steps;
     return SLAM_OK;
 }
@@ -605,30 +695,53 @@ int slam_pf_load_observations(slam_pf* h, int32_t n_steps, const double* z_all) 
 int slam_pf_run(slam_pf* h, int32_t first_step, int32_t n_steps, const double* controls,
                 slam_pf_result* results) {
     SLAM_ARG_CHECK(h && controls && n_steps > 0, "slam_pf_run: bad argument");
+    SLAM_ARG_CHECK(h->n == h->n_global, "slam_pf_run: sharded handle");
     SLAM_ARG_CHECK(first_step >= 0 && first_step + n_steps <= h->z_steps,
                    "slam_pf_run: steps outside the loaded observations");
     SLAM_HIP_TRY(hipSetDevice(h->device));
     int rc;
-    if ((rc = ensure_results(h, n_steps))) return rc;
-    // device-decided resampling: every pass is launched and gates on the flag
-    if ((rc = set_flag(h, kFlagResample, h->resample_next))) return rc;
+    SLAM_HIP_TRY(hipMemcpyAsync(h->ctl + 2 * first_step, controls, 2 * n_steps * sizeof(double),
+                                hipMemcpyHostToDevice, h->stream));
+    if ((rc = set_ctr(h, first_step)) || (rc = set_flag(h, kFlagResample, h->resample_next))) return rc;
+    const bool graphs = h->use_graph && !h->timing;
     for (int32_t k = 0; k < n_steps; ++k) {
-        tic(h, 3);
-        if ((rc = launch_resample(h, std::numeric_limits<double>::quiet_NaN(), 0))) return rc;
-        PredictConst pc = make_predict_const(h, controls + 2 * k);
-        const double* zk = h->z_all + (size_t)(first_step + k) * 2 * std::max<int32_t>(h->nl, 1);
-        if ((rc = launch_fused(h, pc, zk, false))) return rc;
-        if ((rc = launch_reduce(h, h->w_un, k, -1))) return rc;
-        toc(h, 3);
+        if (graphs) {
+            hipGraphExec_t& ge = h->graph[h->cur];
+            if (!ge) {
+                // capture one device-decided step for this ping-pong parity
+                const int cur0 = h->cur;
+                hipGraph_t g;
+                SLAM_HIP_TRY(hipStreamBeginCapture(h->stream, hipStreamCaptureModeThreadLocal));
+                rc = launch_step(h, false);
+                hipError_t e = hipStreamEndCapture(h->stream, &g);
+                h->cur = cur0;
+                if (rc) return rc;
+                if (e != hipSuccess) return fail(SLAM_ERR_HIP, "hipStreamEndCapture failed");
+                SLAM_HIP_TRY(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
+                (void)hipGraphDestroy(g);
+            }
+            SLAM_HIP_TRY(hipGraphLaunch(ge, h->stream));
+            h->cur = 1 - h->cur;
+        } else {
+            tic(h, 3);
+            if ((rc = launch_step(h, false))) return rc;
+            toc(h, 3);
+        }
         h->stepno++;
     }
-    return sync_and_status(h, n_steps, results);
+    return sync_results(h, first_step, n_steps, results);
 }
 
 int slam_pf_enable_timing(slam_pf* h, int32_t on) {
     SLAM_ARG_CHECK(h, "slam_pf_enable_timing: NULL handle");
     h->timing = on != 0;
     for (int k = 0; k < 4; ++k) h->tm.used[k] = 0;
+    return SLAM_OK;
+}
+
+int slam_pf_set_graphs(slam_pf* h, int32_t on) {
+    SLAM_ARG_CHECK(h, "slam_pf_set_graphs: NULL handle");
+    h->use_graph = on != 0;
     return SLAM_OK;
 }
 

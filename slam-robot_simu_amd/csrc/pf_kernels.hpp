@@ -30,13 +30,23 @@ struct LikConst {
 
 struct PredictConst {
     double dt;
-    double v, om;           // control
-    double vdt_om;          // RN(om * dt)             (particle_filter.py:137 (B u)[2])
-    double sv, sw, sg;      // velocity-model stds = sigma**2 (motion_model.py:46-48)
+    double alphas[6];       // motion_model.py:20-29 a1..a6
     double q[9];            // device-RNG noise map for the linear model
-    double np_recip;        // 1/NP (particle_filter.py:32)
+    double np_recip;        // 1/NP (particle_filter.py:32), NP = global particle count
+    double rstep;           // arange step 1/NP (particle_filter.py:213)
     int64_t n_global;       // global particle count (RNG counter space)
     int64_t gbase;          // global index of local particle 0
+};
+
+// Device-resident per-step inputs/outputs of a loaded batch.  Kernels read the
+// step index from ctr[0] (advanced by the last block of normalize_kernel), so
+// one captured step graph replays unchanged for every step.
+struct StepIO {
+    const double* ctl;      // [cap][2] control (v, omega)
+    const double* z;        // [cap][2*NL] robot-frame observations
+    const double* ofs;      // [cap] host resample offset (NaN: device RNG)
+    slam_pf_result* res;    // [cap] result records
+    int32_t* ctr;           // [0] step within the batch, [1] global RNG step
 };
 
 struct BlockPartial {

@@ -1,7 +1,10 @@
-// pf_kernels.hip -- gfx950 kernels of the particle-filter step.
+// pf_kernels.inl -- gfx950 kernels of the particle-filter step (included by pf_api.hip).
 //
-// Step = [exact systematic resample] -> fused predict+likelihood ->
-//        numpy-order chunk sums -> normalise+reduce -> finalise.
+// Step = fused [systematic-resample gather +] predict + likelihood ->
+//        numpy-order chunk sums -> normalise + reductions + result record.
+// The exact sequential cumsum that feeds the resample gather is computed by
+// the scan_* passes (launched at the start of a step; they gate on the
+// device resample flag, so a device-resident run needs no host decisions).
 // Particles are SoA fp64 (x[], y[], th[]) in HBM, one particle per lane.
 #include "pf_kernels.hpp"
 
@@ -56,24 +59,112 @@ __device__ __forceinline__ double div_refined(double x, double d, double rd) {
     return fma(r, rd, q0);
 }
 
+// ---- write-through (sc1) hand-off words, MI355X_MICROARCH "Valid forms" row 1:
+// the bytes one block hands to the last-arriving block are stored and loaded
+// with agent-scope relaxed atomics (global_store/load ... sc1), the storing
+// waves drain (vmcnt(0)) before the block barrier, one lane takes the ticket.
+__device__ __forceinline__ void st_wt(void* p, uint64_t v) {
+    __hip_atomic_store((uint64_t*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t ld_wt(const void* p) {
+    return __hip_atomic_load((uint64_t*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_wt_d(double* p, double v) { st_wt(p, (uint64_t)__double_as_longlong(v)); }
+__device__ __forceinline__ double ld_wt_d(const double* p) { return __longlong_as_double((long long)ld_wt(p)); }
+__device__ __forceinline__ void st_wt_i(int32_t* p, int32_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ int32_t ld_wt_i(const int32_t* p) {
+    return __hip_atomic_load((int32_t*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <typename S>
+__device__ __forceinline__ void st_wt_struct(S* dst, const S& v) {
+    static_assert(sizeof(S) % 8 == 0, "8-byte granules");
+    const uint64_t* src = reinterpret_cast<const uint64_t*>(&v);
+#pragma unroll
+    for (int k = 0; k < (int)(sizeof(S) / 8); ++k) st_wt(reinterpret_cast<uint64_t*>(dst) + k, src[k]);
+}
+template <typename S>
+__device__ __forceinline__ S ld_wt_struct(const S* p) {
+    S v;
+    uint64_t* d = reinterpret_cast<uint64_t*>(&v);
+#pragma unroll
+    for (int k = 0; k < (int)(sizeof(S) / 8); ++k) d[k] = ld_wt(reinterpret_cast<const uint64_t*>(p) + k);
+    return v;
+}
+
+// Last-arriver election: true in exactly one block, after every block has
+// published its write-through partials.  The ticket word is re-zeroed by the
+// winner (the next launch sees it after the kernel boundary).
+__device__ __forceinline__ bool arrive_last(unsigned* counter) {
+    __shared__ int last;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");     // every storing wave drains
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const unsigned t =
+            __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        last = (t == gridDim.x - 1) ? 1 : 0;
+        if (last) __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    return last != 0;
+}
+
+// ---- systematic resampling positions (particle_filter.py:213-215)
+__device__ __forceinline__ double resample_offset(const double ofs_host, const double np_recip,
+                                                  const uint64_t seed, const uint32_t stepno) {
+    if (!isnan(ofs_host)) return ofs_host;
+    const u32x4 ctr{0u, 0u, kStreamResample, stepno};
+    const u32x4 r = philox4x32(ctr, (uint32_t)seed, (uint32_t)(seed >> 32));
+    const uint64_t m = ((uint64_t)(r.x >> 5) << 26) | (uint64_t)(r.y >> 6);
+    return ((double)m * 0x1p-53) * np_recip;                 // rand() * NP_RECIP
+}
+
+// first j in [0, n) with c[j] >= pos (the while loop of :218-220); n if none
+__device__ __forceinline__ int64_t lower_bound_c(const double* __restrict__ c, const int64_t n,
+                                                 const double pos) {
+    int64_t lo = 0, hi = n;
+    while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        if (c[mid] < pos) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+
 // ====================================================================
-// fused predict + likelihood     (particle_filter.py:156-198,
-//                                 motion_model.py:31-62)
+// fused [resample gather +] predict + likelihood
+//      (particle_filter.py:156-198, :216-222; motion_model.py:31-62)
 // ====================================================================
 template <int MOTION, int LIK, bool HOSTNOISE>
 __global__ __launch_bounds__(256) void pf_fused_kernel(
     const int64_t n, const double* __restrict__ xs, const double* __restrict__ ys,
     const double* __restrict__ ts, double* __restrict__ xo, double* __restrict__ yo,
     double* __restrict__ to, const double* __restrict__ w_in, double* __restrict__ w_un,
-    const int32_t* __restrict__ idx, const int32_t* __restrict__ flags,
-    const double* __restrict__ noise, const double* __restrict__ lm,
-    const double* __restrict__ z, PredictConst pc, LikConst lc, uint64_t seed, uint32_t step) {
+    const double* __restrict__ c, int32_t* __restrict__ flags, const double* __restrict__ noise,
+    const double* __restrict__ lm, StepIO io, PredictConst pc, LikConst lc, uint64_t seed) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    const bool resampled = flags[kFlagResample] != 0;
-    const int64_t src = resampled ? (int64_t)idx[i] : i;
-    const double pw = resampled ? pc.np_recip : w_in[i];      // particle_filter.py:222
+    const int32_t st = io.ctr[0];
+    const uint32_t rstep = (uint32_t)io.ctr[1];
+    const int32_t rflag = flags[kFlagResample];
+
+    // ---- resample gather (1: search the exact cumsum here; 2: already gathered)
+    int64_t src = i;
+    if (rflag == 1) {
+        const double ofs = resample_offset(io.ofs[st], pc.np_recip, seed, rstep);
+        const double pos = (double)i * pc.rstep + ofs;           // arange value + ofs
+        src = lower_bound_c(c, n, pos);
+        if (src >= n) {
+            src = n - 1;                                          // IndexError in the reference
+            atomicOr(&flags[kFlagStatus], 1);
+        }
+    }
+    const double pw = rflag ? pc.np_recip : w_in[i];              // particle_filter.py:222
     const double x = xs[src], y = ys[src], th = ts[src];
+
+    // ---- control of this step (particle_filter.py:46-58 / motion_model.py:40-45)
+    const double v = io.ctl[2 * st], om = io.ctl[2 * st + 1];
 
     // ---- noise
     double g0 = 0.0, g1 = 0.0, g2 = 0.0;
@@ -84,9 +175,9 @@ __global__ __launch_bounds__(256) void pf_fused_kernel(
         g2 = noise[3 * i + 2];
     } else {
         const uint64_t gi = (uint64_t)(pc.gbase + i);
-        const u32x4 c0{(uint32_t)gi, (uint32_t)(gi >> 32), kStreamPredict, step};
+        const u32x4 c0{(uint32_t)gi, (uint32_t)(gi >> 32), kStreamPredict, rstep};
         const u32x4 r0 = philox4x32(c0, (uint32_t)seed, (uint32_t)(seed >> 32));
-        const u32x4 c1{(uint32_t)gi, (uint32_t)(gi >> 32), kStreamPredict | 0x100u, step};
+        const u32x4 c1{(uint32_t)gi, (uint32_t)(gi >> 32), kStreamPredict | 0x100u, rstep};
         const u32x4 r1 = philox4x32(c1, (uint32_t)seed, (uint32_t)(seed >> 32));
         double h0, h1, h2, h3;
         normal2(r0, h0, h1);
@@ -112,14 +203,18 @@ __global__ __launch_bounds__(256) void pf_fused_kernel(
         // particle_filter.py:129-140 then + v (:166); A = I, B = diag(V, V, w)
         const double a = pc.dt * cos(th);
         const double b = pc.dt * sin(th);
-        xn = (x + pc.v * a) + g0;
-        yn = (y + pc.v * b) + g1;
-        tn = wrap_angle(th + pc.vdt_om) + g2;
+        xn = (x + v * a) + g0;
+        yn = (y + v * b) + g1;
+        tn = wrap_angle(th + om * pc.dt) + g2;
     } else {
-        // motion_model.py:46-56 (std handed to normal() is sigma**2)
-        const double vh = pc.v + (0.0 + pc.sv * g0);
-        const double wh = pc.om + (0.0 + pc.sw * g1);
-        const double gh = 0.0 + pc.sg * g2;
+        // motion_model.py:40-56 (the std handed to normal() is sigma**2)
+        const double v2 = v * v, w2 = om * om;
+        const double sv = (pc.alphas[0] * v2) + (pc.alphas[1] * w2);
+        const double sw = (pc.alphas[2] * v2) + (pc.alphas[3] * w2);
+        const double sg = (pc.alphas[4] * v2) + (pc.alphas[5] * w2);
+        const double vh = v + (0.0 + (sv * sv) * g0);
+        const double wh = om + (0.0 + (sw * sw) * g1);
+        const double gh = 0.0 + (sg * sg) * g2;
         const double a = vh / wh;
         const double b = wh * pc.dt;
         double s0, c0, s1, c1;
@@ -134,9 +229,10 @@ __global__ __launch_bounds__(256) void pf_fused_kernel(
     to[i] = tn;
 
     // ---- likelihood: world2robot (mylib/transform.py:31-35) per landmark
+    const int nl = lc.nl;
+    const double* __restrict__ z = io.z + (size_t)st * 2 * (size_t)(nl > 0 ? nl : 1);
     double sp, cp;
     sincos(kHalfPi - tn, &sp, &cp);
-    const int nl = lc.nl;
     double bn;
     if (LIK == SLAM_LIK_PRODUCT) {
         // particle_filter.py:185-192 factor by factor, in NumPy's rounding order
@@ -154,9 +250,6 @@ __global__ __launch_bounds__(256) void pf_fused_kernel(
             const double e = lc.has_rho ? exp((-q) / lc.d2) : exp((-q) * 0.5);  // d2 == 2 exactly
             const double f = div_refined(e, lc.den, lc.rden);
             acc = (j == 0) ? f : acc * f;                 // ndarray.prod: left to right
-            // a zero running product stays zero (every factor is finite): stop
-            // once the whole wave has underflowed
-            if ((j & 7) == 7 && __all(acc == 0.0)) break;
         }
         bn = acc;
     } else {
@@ -194,38 +287,13 @@ __global__ __launch_bounds__(256) void pf_fused_kernel(
 }
 
 // ====================================================================
-// last-arriver election across the blocks of one launch (Guideline 16):
-// thread 0 of every block stores its partial, releases at agent scope and takes
-// a ticket; the block holding the last ticket acquires and combines.  The
-// ticket counter is re-zeroed by that block (next launch sees it after the
-// kernel boundary).
-// ====================================================================
-__device__ __forceinline__ bool arrive_last(unsigned* counter) {
-    __shared__ int last;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const unsigned t = atomicAdd(counter, 1u);
-        last = (t == gridDim.x - 1) ? 1 : 0;
-        if (last) {
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            *counter = 0u;
-        }
-    }
-    __syncthreads();
-    return last != 0;
-}
-
-// ====================================================================
 // numpy-order chunk sums (np.sum: 8192-element buffers, pairwise inside)
 // ====================================================================
 // Full chunk: 512 threads = 64 leaves x 8 accumulators; accumulator k of leaf
 // L sums elements L*128 + k + 8m (m = 0..15) left to right; leaves combine as
 // a perfect binary tree, which the xor-butterfly reproduces exactly.
 // Tail chunk (< 8192): host-built leaf table + post-order combine program.
-// The last block folds the buffer partials left to right into *s_out.
+// With s_out != null the last block folds the partials left to right.
 __global__ __launch_bounds__(512) void chunk_sum_kernel(
     const double* __restrict__ w, const int64_t n, double* __restrict__ part,
     const int32_t* __restrict__ tail_leaves, const int32_t* __restrict__ tail_ops,
@@ -235,6 +303,7 @@ __global__ __launch_bounds__(512) void chunk_sum_kernel(
     const int64_t base = (int64_t)blockIdx.x * kSumChunk;
     const int64_t len = (n - base < kSumChunk) ? (n - base) : kSumChunk;
     const int t = threadIdx.x;
+    double blk = 0.0;
     if (len == kSumChunk) {
         const int leaf = t >> 3, k = t & 7;
         const double* p = w + base + leaf * 128 + k;
@@ -245,8 +314,7 @@ __global__ __launch_bounds__(512) void chunk_sum_kernel(
         for (int d = 1; d < 64; d <<= 1) r = r + __shfl_xor(r, d, 64);
         if ((t & 63) == 0) sh[t >> 6] = r;
         __syncthreads();
-        if (t == 0)
-            part[blockIdx.x] = ((sh[0] + sh[1]) + (sh[2] + sh[3])) + ((sh[4] + sh[5]) + (sh[6] + sh[7]));
+        if (t == 0) blk = ((sh[0] + sh[1]) + (sh[2] + sh[3])) + ((sh[4] + sh[5]) + (sh[6] + sh[7]));
     } else {
         // tail: leaves of <= 128 elements, one per thread
         for (int L = t; L < n_tail_leaves; L += blockDim.x) {
@@ -285,9 +353,10 @@ __global__ __launch_bounds__(512) void chunk_sum_kernel(
                     stk[sp++] = a + b;
                 }
             }
-            part[blockIdx.x] = stk[0];
+            blk = stk[0];
         }
     }
+    if (t == 0) st_wt_d(&part[blockIdx.x], blk);
     if (!s_out) return;
     if (!arrive_last(counter)) return;
     double s = 0.0;                                   // buffer partials left to right
@@ -295,7 +364,7 @@ __global__ __launch_bounds__(512) void chunk_sum_kernel(
     for (int c0 = 0; c0 < nc; c0 += 1024) {
         const int cnt = min(1024, nc - c0);
         __syncthreads();
-        for (int k = t; k < cnt; k += blockDim.x) sh[k] = part[c0 + k];
+        for (int k = t; k < cnt; k += blockDim.x) sh[k] = ld_wt_d(&part[c0 + k]);
         __syncthreads();
         if (t == 0)
             for (int k = 0; k < cnt; ++k) s = s + sh[k];
@@ -326,33 +395,15 @@ __device__ __forceinline__ void bp_merge(BlockPartial& r, const BlockPartial& o)
     for (int q = 0; q < 6; ++q) r.m2[q] += o.m2[q];
 }
 
-__device__ __forceinline__ void bp_wave_reduce(BlockPartial& a) {
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) {
-        BlockPartial o;
-        o.maxv = __shfl_xor(a.maxv, d, 64);
-        o.maxi = __shfl_xor(a.maxi, d, 64);
-        o.sw = __shfl_xor(a.sw, d, 64);
-        o.sw2 = __shfl_xor(a.sw2, d, 64);
-        for (int k = 0; k < 3; ++k) o.m1[k] = __shfl_xor(a.m1[k], d, 64);
-        for (int k = 0; k < 6; ++k) o.m2[k] = __shfl_xor(a.m2[k], d, 64);
-        // keep the lower lane on the left so every lane holds the same value
-        if ((threadIdx.x & d) == 0) bp_merge(a, o);
-        else {
-            bp_merge(o, a);
-            a = o;
-        }
-    }
-}
-
-// block-level reduction of per-thread partials in a fixed order -> thread 0
-__device__ __forceinline__ BlockPartial bp_block_reduce(BlockPartial a, BlockPartial* shp) {
-    bp_wave_reduce(a);
-    if ((threadIdx.x & 63) == 0) shp[threadIdx.x >> 6] = a;
+// block-level fixed-order reduction of per-thread partials (result in thread 0)
+__device__ __forceinline__ BlockPartial bp_block_reduce(const BlockPartial& a, BlockPartial* shp) {
+    shp[threadIdx.x] = a;
     __syncthreads();
-    BlockPartial r = shp[0];
-    if (threadIdx.x == 0)
-        for (int k = 1; k < (int)(blockDim.x >> 6); ++k) bp_merge(r, shp[k]);
+    for (int half = blockDim.x >> 1; half >= 1; half >>= 1) {
+        if ((int)threadIdx.x < half) bp_merge(shp[threadIdx.x], shp[threadIdx.x + half]);
+        __syncthreads();
+    }
+    const BlockPartial r = shp[0];
     __syncthreads();
     return r;
 }
@@ -376,7 +427,7 @@ __device__ void write_result(const BlockPartial& r, const double* xs, const doub
         for (int b = 0; b < 3; ++b) o.cov[3 * a + b] = m2[3 * a + b] * inv - mu[a] * mu[b];
     o.ess = 1.0 / r.sw2;
     o.weight_sum = s;
-    o.resampled = resampled_known >= 0 ? resampled_known : flags[kFlagResample];
+    o.resampled = resampled_known >= 0 ? resampled_known : (flags[kFlagResample] != 0);
     o.resample_next = (o.ess < ess_th) ? 1 : 0;
     o.status = flags[kFlagStatus];
     o.n_special = flags[kFlagNSpecial];
@@ -393,82 +444,80 @@ __global__ __launch_bounds__(kNormThreads) void normalize_kernel(
     const double* __restrict__ s_in, const double np_recip, const double* __restrict__ xs,
     const double* __restrict__ ys, const double* __restrict__ ts, double* __restrict__ refp,
     BlockPartial* __restrict__ bp, unsigned* __restrict__ counter, int32_t* __restrict__ flags,
-    const double ess_th, slam_pf_result* __restrict__ res, const int32_t resampled_known,
+    const double ess_th, StepIO io, const int32_t write_res, const int32_t resampled_known,
     const int64_t gbase) {
-    __shared__ BlockPartial shp[kNormThreads / 64];
+    __shared__ BlockPartial shp[kNormThreads];
     const double s = *s_in;
     const double r0 = refp[0], r1 = refp[1], r2 = refp[2];
     BlockPartial a;
     bp_zero(a);
-    constexpr int U = 4;                                 // loads in flight per lane
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i0 < n; i0 += U * stride) {
-        double wu[U], xv[U], yv[U], tv[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int64_t i = i0 + u * stride;
-            const bool ok = i < n;
-            wu[u] = ok ? w_un[i] : 0.0;
-            xv[u] = ok ? xs[i] : r0;
-            yv[u] = ok ? ys[i] : r1;
-            tv[u] = ok ? ts[i] : r2;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        double v = w_un[i] / s;                          // particle_filter.py:235
+        if (isnan(v)) v = np_recip;                      // :236
+        w[i] = v;
+        if (v > a.maxv) {
+            a.maxv = v;
+            a.maxi = gbase + i;
         }
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int64_t i = i0 + u * stride;
-            if (i >= n) break;
-            double v = wu[u] / s;                        // particle_filter.py:235
-            if (isnan(v)) v = np_recip;                  // :236
-            w[i] = v;
-            if (v > a.maxv) {
-                a.maxv = v;
-                a.maxi = gbase + i;
-            }
-            a.sw += v;
-            a.sw2 += v * v;
-            const double d0 = xv[u] - r0, d1 = yv[u] - r1, d2 = tv[u] - r2;
-            const double v0 = v * d0, v1 = v * d1, v2 = v * d2;
-            a.m1[0] += v0;
-            a.m1[1] += v1;
-            a.m1[2] += v2;
-            a.m2[0] += v0 * d0;
-            a.m2[1] += v0 * d1;
-            a.m2[2] += v0 * d2;
-            a.m2[3] += v1 * d1;
-            a.m2[4] += v1 * d2;
-            a.m2[5] += v2 * d2;
-        }
+        a.sw += v;
+        a.sw2 += v * v;
+        const double d0 = xs[i] - r0, d1 = ys[i] - r1, d2 = ts[i] - r2;
+        const double v0 = v * d0, v1 = v * d1, v2 = v * d2;
+        a.m1[0] += v0;
+        a.m1[1] += v1;
+        a.m1[2] += v2;
+        a.m2[0] += v0 * d0;
+        a.m2[1] += v0 * d1;
+        a.m2[2] += v0 * d2;
+        a.m2[3] += v1 * d1;
+        a.m2[4] += v1 * d2;
+        a.m2[5] += v2 * d2;
     }
     const BlockPartial r = bp_block_reduce(a, shp);
-    if (threadIdx.x == 0) bp[blockIdx.x] = r;
-    if (!res) return;
+    if (threadIdx.x == 0) st_wt_struct(&bp[blockIdx.x], r);
+    if (!write_res) return;
     if (!arrive_last(counter)) return;
-    // fixed-order combine: thread t merges blocks t, t+T, ... ; then tree
+    // fixed-order combine: thread t merges blocks t, t+T, ... ; then the tree
     BlockPartial c;
     bp_zero(c);
     const int nb = gridDim.x;
-    for (int k = threadIdx.x; k < nb; k += blockDim.x) bp_merge(c, bp[k]);
+    for (int k = threadIdx.x; k < nb; k += blockDim.x) bp_merge(c, ld_wt_struct(&bp[k]));
     const BlockPartial tot = bp_block_reduce(c, shp);
-    if (threadIdx.x == 0)
-        write_result(tot, xs, ys, ts, gbase, refp, s, flags, ess_th, res, resampled_known);
+    if (threadIdx.x == 0) {
+        const int32_t st = io.ctr[0];
+        write_result(tot, xs, ys, ts, gbase, refp, s, flags, ess_th, io.res + st, resampled_known);
+        io.ctr[0] = st + 1;                              // advance the step context
+        io.ctr[1] = io.ctr[1] + 1;
+    }
 }
 
 // ====================================================================
 // exact sequential cumsum (np.cumsum, particle_filter.py:212)
 // ====================================================================
-// exclusive scan of a small per-block array by one block of NT threads
+// exclusive scan of a small per-block array (write-through words) by one block
 template <typename T, int NT>
 __device__ void block_scan_array(const T* in, T* out, const int nb, T* total, T* sh) {
     const int per = (nb + NT - 1) / NT;
     const int b0 = threadIdx.x * per;
+    auto ld = [](const T* p) -> T {
+        if constexpr (sizeof(T) == 8) {
+            const uint64_t u = ld_wt(p);
+            T v;
+            __builtin_memcpy(&v, &u, 8);
+            return v;
+        } else {
+            return (T)ld_wt_i((const int32_t*)p);
+        }
+    };
     T loc = T(0);
     for (int k = 0; k < per; ++k)
-        if (b0 + k < nb) loc = loc + in[b0 + k];
+        if (b0 + k < nb) loc = loc + ld(in + b0 + k);
     T tot;
     T ex = block_excl_scan<T, NT>(loc, sh, tot);
     for (int k = 0; k < per; ++k)
         if (b0 + k < nb) {
-            const T v = in[b0 + k];
+            const T v = ld(in + b0 + k);
             out[b0 + k] = ex;
             ex = ex + v;
         }
@@ -478,9 +527,9 @@ __device__ void block_scan_array(const T* in, T* out, const int nb, T* total, T*
 // S1: approximate block totals; the last block scans them into boff
 __global__ __launch_bounds__(kScanThreads) void scan_bsum_kernel(
     const double* __restrict__ w, const int64_t n, double* __restrict__ bsum,
-    double* __restrict__ boff, const double base_off, unsigned* __restrict__ counter,
+    double* __restrict__ boff, unsigned* __restrict__ counter,
     const int32_t* __restrict__ flags, const int32_t force) {
-    if (!force && flags[kFlagResample] == 0) return;
+    if (!force && flags[kFlagResample] != 1) return;
     __shared__ double sh[kScanThreads / 64 + 1];
     const int64_t base = (int64_t)blockIdx.x * kScanBlock + threadIdx.x * kScanPer;
     double s = 0.0;
@@ -489,25 +538,23 @@ __global__ __launch_bounds__(kScanThreads) void scan_bsum_kernel(
         if (base + k < n) s += w[base + k];
     double tot;
     block_excl_scan<double, kScanThreads>(s, sh, tot);
-    if (threadIdx.x == 0) bsum[blockIdx.x] = tot;
+    if (threadIdx.x == 0) st_wt_d(&bsum[blockIdx.x], tot);
     if (!arrive_last(counter)) return;
-    block_scan_array<double, kScanThreads>(bsum, boff, gridDim.x, (double*)nullptr, sh);
-    if (base_off != 0.0) {
-        __syncthreads();
-        for (int k = threadIdx.x; k < (int)gridDim.x; k += blockDim.x) boff[k] += base_off;
-    }
+    block_scan_array<double, kScanThreads>(bsum, boff, gridDim.x, boff + gridDim.x, sh);
 }
 
 // S3: classify every element; k_i = increment on the run's ulp grid.  The last
 // block scans the per-block special counts and increment sums.
+// base_off: approximate cumsum before local element 0 (other ranks' weight).
 __global__ __launch_bounds__(kScanThreads) void scan_classify_kernel(
     const double* __restrict__ w, const int64_t n, const double* __restrict__ boff,
-    double* __restrict__ approx, uint64_t* __restrict__ kincl, int32_t* __restrict__ fexcl,
-    uint64_t* __restrict__ bk, int32_t* __restrict__ bf, uint64_t* __restrict__ boffk,
-    int32_t* __restrict__ bofff, uint64_t* __restrict__ ktot, int32_t* __restrict__ nspec,
-    const double delta, const int64_t gbase, unsigned* __restrict__ counter,
-    const int32_t* __restrict__ flags, const int32_t force) {
-    if (!force && flags[kFlagResample] == 0) return;
+    const double* __restrict__ base_off, double* __restrict__ approx,
+    uint64_t* __restrict__ kincl, int32_t* __restrict__ fexcl, uint64_t* __restrict__ bk,
+    int32_t* __restrict__ bf, uint64_t* __restrict__ boffk, int32_t* __restrict__ bofff,
+    uint64_t* __restrict__ ktot, int32_t* __restrict__ nspec, const double delta,
+    const int64_t gbase, unsigned* __restrict__ counter, const int32_t* __restrict__ flags,
+    const int32_t force) {
+    if (!force && flags[kFlagResample] != 1) return;
     __shared__ double shd[kScanThreads / 64 + 1];
     __shared__ uint64_t shk[kScanThreads / 64 + 1];
     __shared__ int32_t shf[kScanThreads / 64 + 1];
@@ -520,7 +567,8 @@ __global__ __launch_bounds__(kScanThreads) void scan_classify_kernel(
         loc += v[k];
     }
     double dtot;
-    double run = block_excl_scan<double, kScanThreads>(loc, shd, dtot) + boff[blockIdx.x];
+    double run = block_excl_scan<double, kScanThreads>(loc, shd, dtot) + boff[blockIdx.x] +
+                 (base_off ? *base_off : 0.0);
     uint64_t kk[kScanPer];
     int32_t ff[kScanPer];
     uint64_t ksum = 0;
@@ -564,8 +612,8 @@ __global__ __launch_bounds__(kScanThreads) void scan_classify_kernel(
         }
     }
     if (threadIdx.x == 0) {
-        bk[blockIdx.x] = ktot_b;
-        bf[blockIdx.x] = ftot_b;
+        st_wt(&bk[blockIdx.x], ktot_b);
+        st_wt_i(&bf[blockIdx.x], ftot_b);
     }
     if (!arrive_last(counter)) return;
     block_scan_array<uint64_t, kScanThreads>(bk, boffk, gridDim.x, ktot, shk);
@@ -573,17 +621,17 @@ __global__ __launch_bounds__(kScanThreads) void scan_classify_kernel(
     block_scan_array<int32_t, kScanThreads>(bf, bofff, gridDim.x, nspec, shf);
 }
 
-// S5: scatter the special elements into an ordered list; the last block then
-// folds them sequentially (S6) unless a separate serial pass follows
-// (multi-GPU: the list is gathered across ranks first).
+// S6: sequential fold over the ordered special elements (one block; tiles in
+// LDS).  Runs of regular elements are added as one exact integer multiple of
+// their binade's ulp.  Falls back to the plain sequential recurrence if a
+// run check fails (flags status bit 1).
 __device__ void serial_fold(const SpecialIn* __restrict__ spec, SpecialOut* __restrict__ out,
                             const int32_t M, const uint64_t ktot, const int64_t n_total,
-                            const double s_start, int32_t* __restrict__ flags,
-                            const double* __restrict__ w, double* __restrict__ c,
-                            const int64_t n_local) {
+                            int32_t* __restrict__ flags, const double* __restrict__ w,
+                            double* __restrict__ c, const int64_t n_local, const bool wt_loads) {
     __shared__ SpecialIn tile[257];
     __shared__ int bad;
-    double s = s_start;
+    double s = 0.0;
     if (threadIdx.x == 0) {
         bad = 0;
         flags[kFlagNSpecial] = M;
@@ -591,7 +639,8 @@ __device__ void serial_fold(const SpecialIn* __restrict__ spec, SpecialOut* __re
     for (int32_t t0 = 0; t0 < M; t0 += 256) {
         __syncthreads();
         const int32_t cnt = min(257, M - t0);
-        for (int k = threadIdx.x; k < cnt; k += blockDim.x) tile[k] = spec[t0 + k];
+        for (int k = threadIdx.x; k < cnt; k += blockDim.x)
+            tile[k] = wt_loads ? ld_wt_struct(&spec[t0 + k]) : spec[t0 + k];
         __syncthreads();
         if (threadIdx.x == 0 && !bad) {
             const int lim = min(256, M - t0);
@@ -620,10 +669,9 @@ __device__ void serial_fold(const SpecialIn* __restrict__ spec, SpecialOut* __re
     }
     __syncthreads();
     if (threadIdx.x == 0 && bad) {
-        // exact fallback: the plain sequential recurrence
         flags[kFlagStatus] |= 2;
         flags[kFlagFallback] = 1;
-        double r = s_start;
+        double r = 0.0;
         for (int64_t i = 0; i < n_local; ++i) {
             r = r + w[i];
             c[i] = r;
@@ -633,6 +681,9 @@ __device__ void serial_fold(const SpecialIn* __restrict__ spec, SpecialOut* __re
     }
 }
 
+// S5: scatter the special elements into an ordered list (write-through); the
+// last block folds them (single GPU).  Multi-GPU gathers the lists first and
+// runs scan_fold_kernel on the concatenation.
 __global__ __launch_bounds__(kScanThreads) void scan_emit_kernel(
     const double* __restrict__ w, const int64_t n, const double* __restrict__ approx,
     const uint64_t* __restrict__ kincl, const int32_t* __restrict__ fexcl,
@@ -641,7 +692,7 @@ __global__ __launch_bounds__(kScanThreads) void scan_emit_kernel(
     const int32_t* __restrict__ nspec_p, const uint64_t* __restrict__ ktot_p,
     const int32_t do_fold, double* __restrict__ c, unsigned* __restrict__ counter,
     int32_t* __restrict__ flags, const int32_t force) {
-    if (!force && flags[kFlagResample] == 0) return;
+    if (!force && flags[kFlagResample] != 1) return;
     const int64_t base = (int64_t)blockIdx.x * kScanBlock + threadIdx.x * kScanPer;
     for (int k = 0; k < kScanPer; ++k) {
         const int64_t i = base + k;
@@ -655,25 +706,35 @@ __global__ __launch_bounds__(kScanThreads) void scan_emit_kernel(
             s.w = w[i];
             s.E = sum_binade(approx[i]);
             s.pad = 0;
-            spec[m] = s;
+            st_wt_struct(&spec[m], s);
         }
     }
     if (!do_fold) return;
     if (!arrive_last(counter)) return;
-    serial_fold(spec, spec_out, *nspec_p, *ktot_p, n, 0.0, flags, w, c, n);
+    serial_fold(spec, spec_out, *nspec_p, *ktot_p, n, flags, w, c, n, true);
 }
 
-// S7: expand the exact cumsum from the specials
+// S6 stand-alone (multi-GPU: over the gathered global list)
+__global__ __launch_bounds__(256) void scan_fold_kernel(
+    const SpecialIn* __restrict__ spec, SpecialOut* __restrict__ out, const int32_t* __restrict__ M,
+    const uint64_t* __restrict__ ktot, const int64_t n_total, int32_t* __restrict__ flags,
+    const double* __restrict__ w, double* __restrict__ c, const int64_t n_local) {
+    serial_fold(spec, out, *M, *ktot, n_total, flags, w, c, n_local, false);
+}
+
+// S7: expand the exact cumsum from the specials.  spec_base / k_base: global
+// special count and increment prefix before local element 0 (multi-GPU).
 __global__ __launch_bounds__(kScanThreads) void scan_expand_kernel(
     const int64_t n, const uint64_t* __restrict__ kincl, const int32_t* __restrict__ fexcl,
     const uint64_t* __restrict__ boffk, const int32_t* __restrict__ bofff,
     const SpecialOut* __restrict__ so, double* __restrict__ c, const int32_t* __restrict__ flags,
+    const int32_t* __restrict__ spec_base, const uint64_t* __restrict__ k_base,
     const int32_t force) {
-    if (!force && flags[kFlagResample] == 0) return;
+    if (!force && flags[kFlagResample] != 1) return;
     if (flags[kFlagFallback]) return;
     const int64_t base = (int64_t)blockIdx.x * kScanBlock + threadIdx.x * kScanPer;
-    const uint64_t bko = boffk[blockIdx.x];
-    const int32_t bfo = bofff[blockIdx.x];
+    const uint64_t bko = boffk[blockIdx.x] + (k_base ? *k_base : 0);
+    const int32_t bfo = bofff[blockIdx.x] + (spec_base ? *spec_base : 0);
 #pragma unroll
     for (int k = 0; k < kScanPer; ++k) {
         const int64_t i = base + k;
@@ -704,28 +765,16 @@ __global__ __launch_bounds__(256) void gather_kernel(
     w[i] = np_recip;
 }
 
-// S8: systematic positions + lower_bound (particle_filter.py:213-221)
+// stand-alone systematic positions + lower_bound (particle_filter.py:213-221)
 __global__ __launch_bounds__(256) void resample_search_kernel(
     const int64_t n, const double* __restrict__ c, int32_t* __restrict__ idx, const double step,
     const double ofs_host, const double np_recip, const uint64_t seed, const uint32_t stepno,
-    int32_t* __restrict__ flags, const int32_t force) {
-    if (!force && flags[kFlagResample] == 0) return;
+    int32_t* __restrict__ flags) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    double ofs = ofs_host;
-    if (isnan(ofs)) {
-        const u32x4 ctr{0u, 0u, kStreamResample, stepno};
-        const u32x4 r = philox4x32(ctr, (uint32_t)seed, (uint32_t)(seed >> 32));
-        const uint64_t m = ((uint64_t)(r.x >> 5) << 26) | (uint64_t)(r.y >> 6);
-        ofs = ((double)m * 0x1p-53) * np_recip;              // rand() * NP_RECIP
-    }
-    const double pos = (double)i * step + ofs;               // arange value + ofs
-    int64_t lo = 0, hi = n;                                   // first j with c[j] >= pos
-    while (lo < hi) {
-        const int64_t mid = (lo + hi) >> 1;
-        if (c[mid] < pos) lo = mid + 1;
-        else hi = mid;
-    }
+    const double ofs = resample_offset(ofs_host, np_recip, seed, stepno);
+    const double pos = (double)i * step + ofs;
+    int64_t lo = lower_bound_c(c, n, pos);
     if (lo >= n) {
         lo = n - 1;
         atomicOr(&flags[kFlagStatus], 1);

@@ -62,6 +62,22 @@ SIGNATURES = {
     "slam_pf_run": (C.c_int, [_P, C.c_int32, C.c_int32, _D, C.POINTER(PFResult)]),
     "slam_pf_enable_timing": (C.c_int, [_P, C.c_int32]),
     "slam_pf_timing": (C.c_int, [_P, C.c_int32, _D, _I64]),
+    "slam_pf_set_graphs": (C.c_int, [_P, C.c_int32]),
+    "slam_pf_set_stream": (C.c_int, [_P, _P]),
+    "slam_pf_create_shard": (C.c_int, [C.POINTER(PFConfig), C.c_int64, C.c_int64, C.c_int64,
+                                       C.c_int32, _D, C.c_int, C.POINTER(_P)]),
+    "slam_pf_shard_sizes": (C.c_int, [_P, _I64]),
+    "slam_pf_shard_begin": (C.c_int, [_P, _D, _D, _D, C.c_double, C.c_int32]),
+    "slam_pf_shard_scan_local": (C.c_int, [_P, _P]),
+    "slam_pf_shard_classify": (C.c_int, [_P, _P, C.c_int32, C.c_int32, _P]),
+    "slam_pf_shard_export_specials": (C.c_int, [_P, C.c_int64, _P]),
+    "slam_pf_shard_fold": (C.c_int, [_P, _P, C.c_int64, _I64, C.c_int32, C.c_int32]),
+    "slam_pf_shard_plan": (C.c_int, [_P, _I64, C.c_int32, _I64]),
+    "slam_pf_shard_export_items": (C.c_int, [_P, _P]),
+    "slam_pf_shard_import_items": (C.c_int, [_P, _P, C.c_int64]),
+    "slam_pf_shard_predict_update": (C.c_int, [_P, _P]),
+    "slam_pf_shard_normalize": (C.c_int, [_P, _P, C.c_int64, _P]),
+    "slam_pf_shard_finish": (C.c_int, [_P, _P, C.c_int32, C.POINTER(PFResult)]),
 }
 
 _lib = None
