@@ -230,14 +230,26 @@ int set_flag(slam_pf* h, int word, int32_t v) {
     return SLAM_OK;
 }
 
-// Exact-cumsum passes S1..S7.  force=0: they gate on the device resample flag.
-int launch_scans(slam_pf* h, int32_t force) {
+// S1 stand-alone: 256-block totals of w and their prefix (normalize_kernel
+// leaves the same arrays behind whenever the next step resamples).
+int launch_bsum(slam_pf* h) {
+    scan_bsum_kernel<<<h->nb_norm, kNormThreads, 0, h->stream>>>(h->w, h->n, h->bsum, h->boff,
+                                                                  h->counters + 2);
+    SLAM_HIP_TRY(hipGetLastError());
+    return SLAM_OK;
+}
+
+// Exact-cumsum passes S3..S7 (S1 with with_s1).  force=0: they gate on the
+// device resample flag.
+int launch_scans(slam_pf* h, int32_t force, bool with_s1) {
     const int64_t n = h->n;
     const int nb = h->nb_scan;
     hipStream_t s = h->stream;
     const double delta = 4.0 * (double)h->n_global * 0x1p-53 + 0x1p-45;
-    scan_bsum_kernel<<<nb, kScanThreads, 0, s>>>(h->w, n, h->bsum, h->boff, h->counters + 2,
-                                                 h->flags, force);
+    if (with_s1) {
+        const int rc = launch_bsum(h);
+        if (rc) return rc;
+    }
     scan_classify_kernel<<<nb, kScanThreads, 0, s>>>(
         h->w, n, h->boff, nullptr, h->c, h->kincl, h->fexcl, h->bk, h->bf, h->boffk, h->bofff,
         h->ktot, h->nspec, delta, 0, h->counters + 2, h->flags, force);
@@ -298,7 +310,8 @@ int launch_reduce(slam_pf* h, int32_t resampled_known) {
                                                  h->wsum);
     normalize_kernel<<<h->nb_norm, kNormThreads, 0, s>>>(
         n, h->w_un, h->w, h->wsum, h->pc.np_recip, h->x[c], h->y[c], h->th[c], h->refp, h->bp,
-        h->counters + 1, h->flags, h->cfg.ess_threshold, step_io(h), 1, resampled_known, 0);
+        h->bsum, h->boff, h->counters + 1, h->flags, h->cfg.ess_threshold, step_io(h), 1,
+        resampled_known, 0);
     toc(h, 1);
     SLAM_HIP_TRY(hipGetLastError());
     return SLAM_OK;
@@ -308,7 +321,7 @@ int launch_reduce(slam_pf* h, int32_t resampled_known) {
 int launch_step(slam_pf* h, bool host_noise) {
     int rc;
     tic(h, 2);
-    if ((rc = launch_scans(h, 0))) return rc;
+    if ((rc = launch_scans(h, 0, false))) return rc;
     toc(h, 2);
     if ((rc = launch_fused(h, h->cfg.motion, host_noise))) return rc;
     return launch_reduce(h, -1);
@@ -362,7 +375,7 @@ int create_impl(const slam_pf_config* cfg, int64_t n_local, int64_t n_global, in
     const int64_t n = n_local;
     h->nb_scan = (int32_t)((n + kScanBlock - 1) / kScanBlock);
     h->nchunks = (int32_t)((n + kSumChunk - 1) / kSumChunk);
-    h->nb_norm = (int32_t)std::min<int64_t>(kNormBlocksMax, (n + 2 * kNormThreads - 1) / (2 * kNormThreads));
+    h->nb_norm = (int32_t)((n + kNormThreads - 1) / kNormThreads);   // one particle per lane
     hipError_t e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking);
     if (e != hipSuccess) {
         delete h;
@@ -384,8 +397,8 @@ int create_impl(const slam_pf_config* cfg, int64_t n_local, int64_t n_global, in
     A(h->kincl, n);
     A(h->fexcl, n);
     A(h->idx, n);
-    A(h->bsum, h->nb_scan);
-    A(h->boff, h->nb_scan + 1);
+    A(h->bsum, h->nb_norm);
+    A(h->boff, h->nb_norm + 1);
     A(h->bk, h->nb_scan);
     A(h->boffk, h->nb_scan);
     A(h->bf, h->nb_scan);
@@ -565,7 +578,7 @@ int slam_pf_step(slam_pf* h, const double* control, const double* z, const doubl
     const int32_t resampling = h->resample_next;
     if (resampling) {
         tic(h, 2);
-        if ((rc = launch_scans(h, 1))) return rc;
+        if ((rc = launch_scans(h, 1, true))) return rc;
         toc(h, 2);
     }
     if ((rc = launch_fused(h, h->cfg.motion, noise != nullptr))) return rc;
@@ -582,7 +595,7 @@ int slam_pf_resample(slam_pf* h, double u_resample, int32_t force, int32_t* resa
     const int32_t go = force ? 1 : h->resample_next;
     if (resampled) *resampled = go;
     if (!go) return SLAM_OK;
-    int rc = launch_scans(h, 1);
+    int rc = launch_scans(h, 1, true);
     if (rc) return rc;
     const double ofs = std::isnan(u_resample) ? u_resample : u_resample * h->pc.np_recip;
     resample_search_kernel<<<grid_for(h->n, 256), 256, 0, h->stream>>>(
@@ -609,7 +622,7 @@ int slam_pf_resample_indices(slam_pf* h, double u_resample, int64_t* idx_out, in
     SLAM_ARG_CHECK(h && idx_out, "slam_pf_resample_indices: NULL argument");
     SLAM_ARG_CHECK(h->n == h->n_global, "slam_pf_resample_indices: sharded handle");
     SLAM_HIP_TRY(hipSetDevice(h->device));
-    int rc = launch_scans(h, 1);
+    int rc = launch_scans(h, 1, true);
     if (rc) return rc;
     const double ofs = std::isnan(u_resample) ? u_resample : u_resample * h->pc.np_recip;
     resample_search_kernel<<<grid_for(h->n, 256), 256, 0, h->stream>>>(
@@ -703,6 +716,7 @@ int slam_pf_run(slam_pf* h, int32_t first_step, int32_t n_steps, const double* c
     SLAM_HIP_TRY(hipMemcpyAsync(h->ctl + 2 * first_step, controls, 2 * n_steps * sizeof(double),
                                 hipMemcpyHostToDevice, h->stream));
     if ((rc = set_ctr(h, first_step)) || (rc = set_flag(h, kFlagResample, h->resample_next))) return rc;
+    if (h->resample_next && (rc = launch_bsum(h))) return rc;   // prefix for the first step's scan
     const bool graphs = h->use_graph && !h->timing;
     for (int32_t k = 0; k < n_steps; ++k) {
         if (graphs) {

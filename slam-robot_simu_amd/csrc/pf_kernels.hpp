@@ -10,7 +10,6 @@ constexpr int kScanBlock = 2048;    // elements per block of the exact-cumsum pa
 constexpr int kScanThreads = 256;
 constexpr int kScanPer = kScanBlock / kScanThreads;  // 8
 constexpr int kNormThreads = 256;
-constexpr int kNormBlocksMax = 512;
 
 // particle_filter.py:179-181 + the mlab.bivariate_normal constants
 struct LikConst {

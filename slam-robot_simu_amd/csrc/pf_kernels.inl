@@ -372,6 +372,35 @@ __global__ __launch_bounds__(512) void chunk_sum_kernel(
     if (t == 0) *s_out = s;
 }
 
+// exclusive scan of a small per-block array (write-through words) by one block
+template <typename T, int NT>
+__device__ void block_scan_array(const T* in, T* out, const int nb, T* total, T* sh) {
+    const int per = (nb + NT - 1) / NT;
+    const int b0 = threadIdx.x * per;
+    auto ld = [](const T* p) -> T {
+        if constexpr (sizeof(T) == 8) {
+            const uint64_t u = ld_wt(p);
+            T v;
+            __builtin_memcpy(&v, &u, 8);
+            return v;
+        } else {
+            return (T)ld_wt_i((const int32_t*)p);
+        }
+    };
+    T loc = T(0);
+    for (int k = 0; k < per; ++k)
+        if (b0 + k < nb) loc = loc + ld(in + b0 + k);
+    T tot;
+    T ex = block_excl_scan<T, NT>(loc, sh, tot);
+    for (int k = 0; k < per; ++k)
+        if (b0 + k < nb) {
+            const T v = ld(in + b0 + k);
+            out[b0 + k] = ex;
+            ex = ex + v;
+        }
+    if (threadIdx.x == 0 && total) *total = tot;
+}
+
 // ====================================================================
 // normalise (particle_filter.py:226-237) + reductions; the last block
 // combines the block partials in block order and writes the step result.
@@ -443,39 +472,42 @@ __global__ __launch_bounds__(kNormThreads) void normalize_kernel(
     const int64_t n, const double* __restrict__ w_un, double* __restrict__ w,
     const double* __restrict__ s_in, const double np_recip, const double* __restrict__ xs,
     const double* __restrict__ ys, const double* __restrict__ ts, double* __restrict__ refp,
-    BlockPartial* __restrict__ bp, unsigned* __restrict__ counter, int32_t* __restrict__ flags,
-    const double ess_th, StepIO io, const int32_t write_res, const int32_t resampled_known,
-    const int64_t gbase) {
+    BlockPartial* __restrict__ bp, double* __restrict__ bsum, double* __restrict__ boff,
+    unsigned* __restrict__ counter, int32_t* __restrict__ flags, const double ess_th, StepIO io,
+    const int32_t write_res, const int32_t resampled_known, const int64_t gbase) {
+    // one particle per lane: the loads of the whole grid are in flight at once
     __shared__ BlockPartial shp[kNormThreads];
+    __shared__ int32_t want_scan;
     const double s = *s_in;
     const double r0 = refp[0], r1 = refp[1], r2 = refp[2];
     BlockPartial a;
     bp_zero(a);
-    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) {
         double v = w_un[i] / s;                          // particle_filter.py:235
         if (isnan(v)) v = np_recip;                      // :236
         w[i] = v;
-        if (v > a.maxv) {
-            a.maxv = v;
-            a.maxi = gbase + i;
-        }
-        a.sw += v;
-        a.sw2 += v * v;
+        a.maxv = v;
+        a.maxi = gbase + i;
+        a.sw = v;
+        a.sw2 = v * v;
         const double d0 = xs[i] - r0, d1 = ys[i] - r1, d2 = ts[i] - r2;
         const double v0 = v * d0, v1 = v * d1, v2 = v * d2;
-        a.m1[0] += v0;
-        a.m1[1] += v1;
-        a.m1[2] += v2;
-        a.m2[0] += v0 * d0;
-        a.m2[1] += v0 * d1;
-        a.m2[2] += v0 * d2;
-        a.m2[3] += v1 * d1;
-        a.m2[4] += v1 * d2;
-        a.m2[5] += v2 * d2;
+        a.m1[0] = v0;
+        a.m1[1] = v1;
+        a.m1[2] = v2;
+        a.m2[0] = v0 * d0;
+        a.m2[1] = v0 * d1;
+        a.m2[2] = v0 * d2;
+        a.m2[3] = v1 * d1;
+        a.m2[4] = v1 * d2;
+        a.m2[5] = v2 * d2;
     }
     const BlockPartial r = bp_block_reduce(a, shp);
-    if (threadIdx.x == 0) st_wt_struct(&bp[blockIdx.x], r);
+    if (threadIdx.x == 0) {
+        st_wt_struct(&bp[blockIdx.x], r);
+        st_wt_d(&bsum[blockIdx.x], r.sw);                // approximate block total (exact-cumsum S1)
+    }
     if (!write_res) return;
     if (!arrive_last(counter)) return;
     // fixed-order combine: thread t merges blocks t, t+T, ... ; then the tree
@@ -487,60 +519,32 @@ __global__ __launch_bounds__(kNormThreads) void normalize_kernel(
     if (threadIdx.x == 0) {
         const int32_t st = io.ctr[0];
         write_result(tot, xs, ys, ts, gbase, refp, s, flags, ess_th, io.res + st, resampled_known);
+        want_scan = flags[kFlagResample];
         io.ctr[0] = st + 1;                              // advance the step context
         io.ctr[1] = io.ctr[1] + 1;
     }
+    __syncthreads();
+    // the next step resamples: prefix of the block totals for its exact cumsum
+    if (want_scan)
+        block_scan_array<double, kNormThreads>(bsum, boff, nb, boff + nb, (double*)shp);
 }
 
 // ====================================================================
 // exact sequential cumsum (np.cumsum, particle_filter.py:212)
 // ====================================================================
-// exclusive scan of a small per-block array (write-through words) by one block
-template <typename T, int NT>
-__device__ void block_scan_array(const T* in, T* out, const int nb, T* total, T* sh) {
-    const int per = (nb + NT - 1) / NT;
-    const int b0 = threadIdx.x * per;
-    auto ld = [](const T* p) -> T {
-        if constexpr (sizeof(T) == 8) {
-            const uint64_t u = ld_wt(p);
-            T v;
-            __builtin_memcpy(&v, &u, 8);
-            return v;
-        } else {
-            return (T)ld_wt_i((const int32_t*)p);
-        }
-    };
-    T loc = T(0);
-    for (int k = 0; k < per; ++k)
-        if (b0 + k < nb) loc = loc + ld(in + b0 + k);
-    T tot;
-    T ex = block_excl_scan<T, NT>(loc, sh, tot);
-    for (int k = 0; k < per; ++k)
-        if (b0 + k < nb) {
-            const T v = ld(in + b0 + k);
-            out[b0 + k] = ex;
-            ex = ex + v;
-        }
-    if (threadIdx.x == 0 && total) *total = tot;
-}
-
-// S1: approximate block totals; the last block scans them into boff
-__global__ __launch_bounds__(kScanThreads) void scan_bsum_kernel(
+// S1: approximate totals of 256-element blocks of w; the last block scans them
+// into boff (boff[nb] = total).  normalize_kernel produces the same arrays as
+// a by-product when the next step resamples.
+__global__ __launch_bounds__(kNormThreads) void scan_bsum_kernel(
     const double* __restrict__ w, const int64_t n, double* __restrict__ bsum,
-    double* __restrict__ boff, unsigned* __restrict__ counter,
-    const int32_t* __restrict__ flags, const int32_t force) {
-    if (!force && flags[kFlagResample] != 1) return;
-    __shared__ double sh[kScanThreads / 64 + 1];
-    const int64_t base = (int64_t)blockIdx.x * kScanBlock + threadIdx.x * kScanPer;
-    double s = 0.0;
-#pragma unroll
-    for (int k = 0; k < kScanPer; ++k)
-        if (base + k < n) s += w[base + k];
+    double* __restrict__ boff, unsigned* __restrict__ counter) {
+    __shared__ double sh[kNormThreads / 64 + 1];
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     double tot;
-    block_excl_scan<double, kScanThreads>(s, sh, tot);
+    block_excl_scan<double, kNormThreads>(i < n ? w[i] : 0.0, sh, tot);
     if (threadIdx.x == 0) st_wt_d(&bsum[blockIdx.x], tot);
     if (!arrive_last(counter)) return;
-    block_scan_array<double, kScanThreads>(bsum, boff, gridDim.x, boff + gridDim.x, sh);
+    block_scan_array<double, kNormThreads>(bsum, boff, gridDim.x, boff + gridDim.x, sh);
 }
 
 // S3: classify every element; k_i = increment on the run's ulp grid.  The last
@@ -567,7 +571,8 @@ __global__ __launch_bounds__(kScanThreads) void scan_classify_kernel(
         loc += v[k];
     }
     double dtot;
-    double run = block_excl_scan<double, kScanThreads>(loc, shd, dtot) + boff[blockIdx.x] +
+    double run = block_excl_scan<double, kScanThreads>(loc, shd, dtot) +
+                 boff[(int64_t)blockIdx.x * (kScanBlock / kNormThreads)] +
                  (base_off ? *base_off : 0.0);
     uint64_t kk[kScanPer];
     int32_t ff[kScanPer];

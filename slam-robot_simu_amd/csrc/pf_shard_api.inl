@@ -51,10 +51,9 @@ int slam_pf_shard_begin(slam_pf* h, const double* control, const double* z, cons
 int slam_pf_shard_scan_local(slam_pf* h, double* d_total) {
     SLAM_ARG_CHECK(h && d_total, "slam_pf_shard_scan_local: NULL argument");
     SLAM_HIP_TRY(hipSetDevice(h->device));
-    scan_bsum_kernel<<<h->nb_scan, kScanThreads, 0, h->stream>>>(h->w, h->n, h->bsum, h->boff,
-                                                                  h->counters + 2, h->flags, 1);
-    SLAM_HIP_TRY(hipGetLastError());
-    SLAM_HIP_TRY(hipMemcpyAsync(d_total, h->boff + h->nb_scan, 8, hipMemcpyDeviceToDevice, h->stream));
+    int rc = launch_bsum(h);
+    if (rc) return rc;
+    SLAM_HIP_TRY(hipMemcpyAsync(d_total, h->boff + h->nb_norm, 8, hipMemcpyDeviceToDevice, h->stream));
     return SLAM_OK;
 }
 
@@ -230,7 +229,8 @@ int slam_pf_shard_normalize(slam_pf* h, const double* d_all_partials, int64_t np
     shard_fold_sum_kernel<<<1, 256, 0, s>>>(d_all_partials, nparts, h->wsum);
     normalize_kernel<<<h->nb_norm, kNormThreads, 0, s>>>(
         h->n, h->w_un, h->w, h->wsum, h->pc.np_recip, h->x[c], h->y[c], h->th[c], h->refp, h->bp,
-        h->counters + 1, h->flags, h->cfg.ess_threshold, step_io(h), 0, 0, h->gbase);
+        h->bsum, h->boff, h->counters + 1, h->flags, h->cfg.ess_threshold, step_io(h), 0, 0,
+        h->gbase);
     shard_record_kernel<<<1, kNormThreads, 0, s>>>(h->bp, h->nb_norm, h->x[c], h->y[c], h->th[c],
                                                    h->gbase, (ShardRecord*)d_record);
     SLAM_HIP_TRY(hipGetLastError());
