@@ -118,9 +118,9 @@ int slam_pf_enable_timing(slam_pf* h, int32_t on);
 int slam_pf_timing(slam_pf* h, int32_t kernel, double* total_ms, int64_t* launches);
 /* slam_pf_run replays one captured hipGraph per step (default on). */
 int slam_pf_set_graphs(slam_pf* h, int32_t on);
-/* Run on the caller's HIP stream (e.g. torch.cuda.current_stream()); NULL
- * restores a private stream. */
-int slam_pf_set_stream(slam_pf* h, void* hip_stream);
+/* external != 0: run on the caller's HIP stream (e.g. torch.cuda.current_stream();
+ * NULL = the default stream).  external == 0: a private stream again. */
+int slam_pf_set_stream(slam_pf* h, void* hip_stream, int32_t external);
 
 /* ====================================================================
  * Sharded particle filter (BASELINE config 3): one handle per GPU holds

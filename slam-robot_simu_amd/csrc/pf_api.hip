@@ -73,6 +73,8 @@ struct slam_pf {
     int32_t n_tail_leaves = 0, n_tail_ops = 0;
     int32_t nb_norm = 0;
     BlockPartial* bp = nullptr;
+    BlockPartial* gp = nullptr;     // group partials of the two-level combine
+    unsigned* ncnt = nullptr;       // normalize tickets: [0] final, [1+g] groups
     double* wsum = nullptr;
     double* refp = nullptr;
     int32_t* flags = nullptr;
@@ -310,7 +312,7 @@ int launch_reduce(slam_pf* h, int32_t resampled_known) {
                                                  h->wsum);
     normalize_kernel<<<h->nb_norm, kNormThreads, 0, s>>>(
         n, h->w_un, h->w, h->wsum, h->pc.np_recip, h->x[c], h->y[c], h->th[c], h->refp, h->bp,
-        h->bsum, h->boff, h->counters + 1, h->flags, h->cfg.ess_threshold, step_io(h), 1,
+        h->gp, h->bsum, h->boff, h->ncnt, h->flags, h->cfg.ess_threshold, step_io(h), 1,
         resampled_known, 0);
     toc(h, 1);
     SLAM_HIP_TRY(hipGetLastError());
@@ -375,7 +377,7 @@ int create_impl(const slam_pf_config* cfg, int64_t n_local, int64_t n_global, in
     const int64_t n = n_local;
     h->nb_scan = (int32_t)((n + kScanBlock - 1) / kScanBlock);
     h->nchunks = (int32_t)((n + kSumChunk - 1) / kSumChunk);
-    h->nb_norm = (int32_t)((n + kNormThreads - 1) / kNormThreads);   // one particle per lane
+    h->nb_norm = (int32_t)((n + kNormPer - 1) / kNormPer);
     hipError_t e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking);
     if (e != hipSuccess) {
         delete h;
@@ -409,6 +411,8 @@ int create_impl(const slam_pf_config* cfg, int64_t n_local, int64_t n_global, in
     A(h->spec_out, n);
     A(h->part, h->nchunks);
     A(h->bp, h->nb_norm);
+    A(h->gp, h->nb_norm / 64 + 2);
+    A(h->ncnt, h->nb_norm / 64 + 4);
     A(h->wsum, 1);
     A(h->refp, 4);
     A(h->flags, kFlagWords);
@@ -443,6 +447,7 @@ int create_impl(const slam_pf_config* cfg, int64_t n_local, int64_t n_global, in
     SLAM_HIP_TRY(hipMemcpy(h->refp, cfg->x0, 3 * sizeof(double), hipMemcpyHostToDevice));
     SLAM_HIP_TRY(hipMemset(h->flags, 0, kFlagWords * sizeof(int32_t)));
     SLAM_HIP_TRY(hipMemset(h->counters, 0, 8 * sizeof(unsigned)));
+    SLAM_HIP_TRY(hipMemset(h->ncnt, 0, (h->nb_norm / 64 + 4) * sizeof(unsigned)));
     SLAM_HIP_TRY(hipMemset(h->ctr, 0, 4 * sizeof(int32_t)));
     if (n_landmarks > 0)
         SLAM_HIP_TRY(hipMemcpy(h->lm, landmarks, 2 * n_landmarks * sizeof(double), hipMemcpyHostToDevice));
@@ -503,13 +508,13 @@ int slam_pf_destroy(slam_pf* h) {
     return SLAM_OK;
 }
 
-int slam_pf_set_stream(slam_pf* h, void* stream) {
+int slam_pf_set_stream(slam_pf* h, void* stream, int32_t external) {
     SLAM_ARG_CHECK(h, "slam_pf_set_stream: NULL handle");
     SLAM_HIP_TRY(hipSetDevice(h->device));
     SLAM_HIP_TRY(hipStreamSynchronize(h->stream));
     drop_graphs(h);
     if (h->own_stream) (void)hipStreamDestroy(h->stream);
-    if (stream) {
+    if (external) {              // the caller's stream (NULL = the default stream)
         h->stream = (hipStream_t)stream;
         h->own_stream = false;
     } else {

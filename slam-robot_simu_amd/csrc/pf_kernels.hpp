@@ -10,6 +10,8 @@ constexpr int kScanBlock = 2048;    // elements per block of the exact-cumsum pa
 constexpr int kScanThreads = 256;
 constexpr int kScanPer = kScanBlock / kScanThreads;  // 8
 constexpr int kNormThreads = 256;
+constexpr int kNormEPT = 4;                          // particles per lane in normalize
+constexpr int kNormPer = kNormThreads * kNormEPT;    // particles per normalize block
 
 // particle_filter.py:179-181 + the mlab.bivariate_normal constants
 struct LikConst {

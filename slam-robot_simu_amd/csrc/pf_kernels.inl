@@ -424,17 +424,79 @@ __device__ __forceinline__ void bp_merge(BlockPartial& r, const BlockPartial& o)
     for (int q = 0; q < 6; ++q) r.m2[q] += o.m2[q];
 }
 
-// block-level fixed-order reduction of per-thread partials (result in thread 0)
-__device__ __forceinline__ BlockPartial bp_block_reduce(const BlockPartial& a, BlockPartial* shp) {
-    shp[threadIdx.x] = a;
-    __syncthreads();
-    for (int half = blockDim.x >> 1; half >= 1; half >>= 1) {
-        if ((int)threadIdx.x < half) bp_merge(shp[threadIdx.x], shp[threadIdx.x + half]);
-        __syncthreads();
+// xor-butterfly over the 64 lanes (lower lane always on the left: a fixed tree)
+__device__ __forceinline__ void bp_wave_reduce(BlockPartial& a) {
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        BlockPartial o;
+        o.maxv = __shfl_xor(a.maxv, d, 64);
+        o.maxi = __shfl_xor(a.maxi, d, 64);
+        o.sw = __shfl_xor(a.sw, d, 64);
+        o.sw2 = __shfl_xor(a.sw2, d, 64);
+#pragma unroll
+        for (int k = 0; k < 3; ++k) o.m1[k] = __shfl_xor(a.m1[k], d, 64);
+#pragma unroll
+        for (int k = 0; k < 6; ++k) o.m2[k] = __shfl_xor(a.m2[k], d, 64);
+        if (threadIdx.x & d) {
+            bp_merge(o, a);
+            a = o;
+        } else {
+            bp_merge(a, o);
+        }
     }
-    const BlockPartial r = shp[0];
+}
+
+// block-level fixed-order reduction of per-thread partials (result in thread 0)
+__device__ __forceinline__ BlockPartial bp_block_reduce(BlockPartial a, BlockPartial* shp) {
+    bp_wave_reduce(a);
+    if ((threadIdx.x & 63) == 0) shp[threadIdx.x >> 6] = a;
+    __syncthreads();
+    BlockPartial r = shp[0];
+    if (threadIdx.x == 0)
+        for (int k = 1; k < (int)(blockDim.x >> 6); ++k) bp_merge(r, shp[k]);
     __syncthreads();
     return r;
+}
+
+// ticket on `counter` among `expected` arrivers; true in the last one
+__device__ __forceinline__ bool arrive_last_n(unsigned* counter, const unsigned expected) {
+    __shared__ int last;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const unsigned t =
+            __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        last = (t == expected - 1) ? 1 : 0;
+        if (last) __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    return last != 0;
+}
+
+// Deterministic two-level combine of per-block partials: the last block of
+// every group of kGroup blocks merges the group (block order) into gp[g]; the
+// last group finisher merges the groups (group order).  Returns true in that
+// one block, with the total in thread 0's `out`.
+constexpr int kGroup = 64;
+__device__ bool hier_combine(const BlockPartial& mine, BlockPartial* bp, BlockPartial* gp,
+                             unsigned* cnt, BlockPartial* shp, BlockPartial& out) {
+    const int b = blockIdx.x, nb = gridDim.x;
+    if (threadIdx.x == 0) st_wt_struct(&bp[b], mine);
+    const int g = b / kGroup, g0 = g * kGroup;
+    const int gn = min(kGroup, nb - g0);
+    if (!arrive_last_n(&cnt[1 + g], (unsigned)gn)) return false;
+    BlockPartial c;
+    bp_zero(c);
+    if ((int)threadIdx.x < gn) c = ld_wt_struct(&bp[g0 + threadIdx.x]);
+    const BlockPartial gt = bp_block_reduce(c, shp);
+    if (threadIdx.x == 0) st_wt_struct(&gp[g], gt);
+    const int ng = (nb + kGroup - 1) / kGroup;
+    if (!arrive_last_n(&cnt[0], (unsigned)ng)) return false;
+    BlockPartial f;
+    bp_zero(f);
+    for (int k = threadIdx.x; k < ng; k += blockDim.x) bp_merge(f, ld_wt_struct(&gp[k]));
+    out = bp_block_reduce(f, shp);
+    return true;
 }
 
 // result record from the combined partial (x_est = particle at the argmax)
@@ -468,54 +530,79 @@ __device__ void write_result(const BlockPartial& r, const double* xs, const doub
     *res = o;
 }
 
+// One normalise block = kNormPer particles (kNormThreads lanes x kNormEPT,
+// coalesced per k); all loads of a lane are issued before any use.
 __global__ __launch_bounds__(kNormThreads) void normalize_kernel(
     const int64_t n, const double* __restrict__ w_un, double* __restrict__ w,
     const double* __restrict__ s_in, const double np_recip, const double* __restrict__ xs,
     const double* __restrict__ ys, const double* __restrict__ ts, double* __restrict__ refp,
-    BlockPartial* __restrict__ bp, double* __restrict__ bsum, double* __restrict__ boff,
-    unsigned* __restrict__ counter, int32_t* __restrict__ flags, const double ess_th, StepIO io,
-    const int32_t write_res, const int32_t resampled_known, const int64_t gbase) {
-    // one particle per lane: the loads of the whole grid are in flight at once
-    __shared__ BlockPartial shp[kNormThreads];
+    BlockPartial* __restrict__ bp, BlockPartial* __restrict__ gp, double* __restrict__ bsum,
+    double* __restrict__ boff, unsigned* __restrict__ cnt, int32_t* __restrict__ flags,
+    const double ess_th, StepIO io, const int32_t write_res, const int32_t resampled_known,
+    const int64_t gbase) {
+    __shared__ BlockPartial shp[kNormThreads / 64];
+    __shared__ double shd[kNormThreads / 64 + 1];
     __shared__ int32_t want_scan;
     const double s = *s_in;
     const double r0 = refp[0], r1 = refp[1], r2 = refp[2];
+    const int64_t base = (int64_t)blockIdx.x * kNormPer + threadIdx.x;
+    double wu[kNormEPT], xv[kNormEPT], yv[kNormEPT], tv[kNormEPT];
+    if (base + (kNormEPT - 1) * kNormThreads < n) {
+#pragma unroll
+        for (int k = 0; k < kNormEPT; ++k) {
+            const int64_t i = base + k * kNormThreads;
+            wu[k] = w_un[i];
+            xv[k] = xs[i];
+            yv[k] = ys[i];
+            tv[k] = ts[i];
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < kNormEPT; ++k) {
+            const int64_t i = base + k * kNormThreads;
+            const bool ok = i < n;
+            wu[k] = ok ? w_un[i] : 0.0;
+            xv[k] = ok ? xs[i] : r0;
+            yv[k] = ok ? ys[i] : r1;
+            tv[k] = ok ? ts[i] : r2;
+        }
+    }
     BlockPartial a;
     bp_zero(a);
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) {
-        double v = w_un[i] / s;                          // particle_filter.py:235
-        if (isnan(v)) v = np_recip;                      // :236
-        w[i] = v;
-        a.maxv = v;
-        a.maxi = gbase + i;
-        a.sw = v;
-        a.sw2 = v * v;
-        const double d0 = xs[i] - r0, d1 = ys[i] - r1, d2 = ts[i] - r2;
-        const double v0 = v * d0, v1 = v * d1, v2 = v * d2;
-        a.m1[0] = v0;
-        a.m1[1] = v1;
-        a.m1[2] = v2;
-        a.m2[0] = v0 * d0;
-        a.m2[1] = v0 * d1;
-        a.m2[2] = v0 * d2;
-        a.m2[3] = v1 * d1;
-        a.m2[4] = v1 * d2;
-        a.m2[5] = v2 * d2;
+#pragma unroll
+    for (int k = 0; k < kNormEPT; ++k) {
+        const int64_t i = base + k * kNormThreads;
+        if (i < n) {
+            double v = wu[k] / s;                        // particle_filter.py:235
+            if (isnan(v)) v = np_recip;                  // :236
+            w[i] = v;
+            if (v > a.maxv) {
+                a.maxv = v;
+                a.maxi = gbase + i;
+            }
+            a.sw += v;
+            a.sw2 += v * v;
+            const double d0 = xv[k] - r0, d1 = yv[k] - r1, d2 = tv[k] - r2;
+            const double v0 = v * d0, v1 = v * d1, v2 = v * d2;
+            a.m1[0] += v0;
+            a.m1[1] += v1;
+            a.m1[2] += v2;
+            a.m2[0] += v0 * d0;
+            a.m2[1] += v0 * d1;
+            a.m2[2] += v0 * d2;
+            a.m2[3] += v1 * d1;
+            a.m2[4] += v1 * d2;
+            a.m2[5] += v2 * d2;
+        }
     }
     const BlockPartial r = bp_block_reduce(a, shp);
-    if (threadIdx.x == 0) {
-        st_wt_struct(&bp[blockIdx.x], r);
-        st_wt_d(&bsum[blockIdx.x], r.sw);                // approximate block total (exact-cumsum S1)
+    if (threadIdx.x == 0) st_wt_d(&bsum[blockIdx.x], r.sw);   // approximate block total (S1)
+    if (!write_res) {
+        if (threadIdx.x == 0) st_wt_struct(&bp[blockIdx.x], r);
+        return;
     }
-    if (!write_res) return;
-    if (!arrive_last(counter)) return;
-    // fixed-order combine: thread t merges blocks t, t+T, ... ; then the tree
-    BlockPartial c;
-    bp_zero(c);
-    const int nb = gridDim.x;
-    for (int k = threadIdx.x; k < nb; k += blockDim.x) bp_merge(c, ld_wt_struct(&bp[k]));
-    const BlockPartial tot = bp_block_reduce(c, shp);
+    BlockPartial tot;
+    if (!hier_combine(r, bp, gp, cnt, shp, tot)) return;
     if (threadIdx.x == 0) {
         const int32_t st = io.ctr[0];
         write_result(tot, xs, ys, ts, gbase, refp, s, flags, ess_th, io.res + st, resampled_known);
@@ -526,22 +613,28 @@ __global__ __launch_bounds__(kNormThreads) void normalize_kernel(
     __syncthreads();
     // the next step resamples: prefix of the block totals for its exact cumsum
     if (want_scan)
-        block_scan_array<double, kNormThreads>(bsum, boff, nb, boff + nb, (double*)shp);
+        block_scan_array<double, kNormThreads>(bsum, boff, gridDim.x, boff + gridDim.x, shd);
 }
 
 // ====================================================================
 // exact sequential cumsum (np.cumsum, particle_filter.py:212)
 // ====================================================================
-// S1: approximate totals of 256-element blocks of w; the last block scans them
-// into boff (boff[nb] = total).  normalize_kernel produces the same arrays as
-// a by-product when the next step resamples.
+// S1: approximate totals of kNormPer-element blocks of w; the last block scans
+// them into boff (boff[nb] = total).  normalize_kernel produces the same
+// arrays as a by-product when the next step resamples.
 __global__ __launch_bounds__(kNormThreads) void scan_bsum_kernel(
     const double* __restrict__ w, const int64_t n, double* __restrict__ bsum,
     double* __restrict__ boff, unsigned* __restrict__ counter) {
     __shared__ double sh[kNormThreads / 64 + 1];
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t base = (int64_t)blockIdx.x * kNormPer + threadIdx.x;
+    double loc = 0.0;
+#pragma unroll
+    for (int k = 0; k < kNormEPT; ++k) {
+        const int64_t i = base + k * kNormThreads;
+        if (i < n) loc += w[i];
+    }
     double tot;
-    block_excl_scan<double, kNormThreads>(i < n ? w[i] : 0.0, sh, tot);
+    block_excl_scan<double, kNormThreads>(loc, sh, tot);
     if (threadIdx.x == 0) st_wt_d(&bsum[blockIdx.x], tot);
     if (!arrive_last(counter)) return;
     block_scan_array<double, kNormThreads>(bsum, boff, gridDim.x, boff + gridDim.x, sh);
@@ -572,7 +665,7 @@ __global__ __launch_bounds__(kScanThreads) void scan_classify_kernel(
     }
     double dtot;
     double run = block_excl_scan<double, kScanThreads>(loc, shd, dtot) +
-                 boff[(int64_t)blockIdx.x * (kScanBlock / kNormThreads)] +
+                 boff[(int64_t)blockIdx.x * (kScanBlock / kNormPer)] +
                  (base_off ? *base_off : 0.0);
     uint64_t kk[kScanPer];
     int32_t ff[kScanPer];

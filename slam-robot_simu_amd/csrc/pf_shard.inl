@@ -237,7 +237,7 @@ __global__ __launch_bounds__(kNormThreads) void shard_record_kernel(
     const BlockPartial* __restrict__ bp, const int32_t nb, const double* __restrict__ xs,
     const double* __restrict__ ys, const double* __restrict__ ts, const int64_t gbase,
     ShardRecord* __restrict__ out) {
-    __shared__ BlockPartial shp[kNormThreads];
+    __shared__ BlockPartial shp[kNormThreads / 64];
     BlockPartial c;
     bp_zero(c);
     for (int k = threadIdx.x; k < nb; k += blockDim.x) bp_merge(c, ld_wt_struct(&bp[k]));

@@ -123,7 +123,7 @@ class DeviceShard:
               "slam_pf_create_shard")
         self._h = h
         stream = torch.cuda.current_stream(self.device)
-        check(lib.slam_pf_set_stream(h, C.c_void_p(stream.cuda_stream)), "slam_pf_set_stream")
+        check(lib.slam_pf_set_stream(h, C.c_void_p(stream.cuda_stream), 1), "slam_pf_set_stream")
         sizes = np.zeros(4, dtype=np.int64)
         check(lib.slam_pf_shard_sizes(h, sizes.ctypes.data_as(_lib._I64)), "slam_pf_shard_sizes")
         self.nchunks, self.rec_bytes, self.spec_bytes, self.item_bytes = (int(v) for v in sizes)
