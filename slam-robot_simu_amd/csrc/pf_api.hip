@@ -73,12 +73,11 @@ struct slam_pf {
     int32_t n_tail_leaves = 0, n_tail_ops = 0;
     int32_t nb_norm = 0;
     BlockPartial* bp = nullptr;
-    BlockPartial* gp = nullptr;     // group partials of the two-level combine
-    unsigned* ncnt = nullptr;       // normalize tickets: [0] final, [1+g] groups
+    BlockPartial* gp = nullptr;     // residue-class partials of the two-level combine
     double* wsum = nullptr;
     double* refp = nullptr;
     int32_t* flags = nullptr;
-    unsigned* counters = nullptr;   // last-arriver tickets (re-zeroed by the last block)
+    unsigned* tk = nullptr;         // ticket blocks: +0 np.sum, +1 normalize, +2 scans (x kTicketWords)
     // inputs / step context
     double* lm = nullptr;
     double* noise = nullptr;
@@ -236,7 +235,7 @@ int set_flag(slam_pf* h, int word, int32_t v) {
 // leaves the same arrays behind whenever the next step resamples).
 int launch_bsum(slam_pf* h) {
     scan_bsum_kernel<<<h->nb_norm, kNormThreads, 0, h->stream>>>(h->w, h->n, h->bsum, h->boff,
-                                                                  h->counters + 2);
+                                                                  h->tk + 2 * kTicketWords);
     SLAM_HIP_TRY(hipGetLastError());
     return SLAM_OK;
 }
@@ -254,10 +253,10 @@ int launch_scans(slam_pf* h, int32_t force, bool with_s1) {
     }
     scan_classify_kernel<<<nb, kScanThreads, 0, s>>>(
         h->w, n, h->boff, nullptr, h->c, h->kincl, h->fexcl, h->bk, h->bf, h->boffk, h->bofff,
-        h->ktot, h->nspec, delta, 0, h->counters + 2, h->flags, force);
+        h->ktot, h->nspec, delta, 0, h->tk + 2 * kTicketWords, h->flags, force);
     scan_emit_kernel<<<nb, kScanThreads, 0, s>>>(h->w, n, h->c, h->kincl, h->fexcl, h->boffk,
                                                  h->bofff, h->spec_in, 0, h->spec_out, h->nspec,
-                                                 h->ktot, 1, h->c, h->counters + 2, h->flags,
+                                                 h->ktot, 1, h->c, h->tk + 2 * kTicketWords, h->flags,
                                                  force);
     scan_expand_kernel<<<nb, kScanThreads, 0, s>>>(n, h->kincl, h->fexcl, h->boffk, h->bofff,
                                                    h->spec_out, h->c, h->flags, nullptr,
@@ -308,11 +307,11 @@ int launch_reduce(slam_pf* h, int32_t resampled_known) {
     const int c = h->cur;
     tic(h, 1);
     chunk_sum_kernel<<<h->nchunks, 512, 0, s>>>(h->w_un, n, h->part, h->tail_leaves, h->tail_ops,
-                                                 h->n_tail_leaves, h->n_tail_ops, h->counters,
+                                                 h->n_tail_leaves, h->n_tail_ops, h->tk,
                                                  h->wsum);
     normalize_kernel<<<h->nb_norm, kNormThreads, 0, s>>>(
         n, h->w_un, h->w, h->wsum, h->pc.np_recip, h->x[c], h->y[c], h->th[c], h->refp, h->bp,
-        h->gp, h->bsum, h->boff, h->ncnt, h->flags, h->cfg.ess_threshold, step_io(h), 1,
+        h->gp, h->bsum, h->boff, h->tk + kTicketWords, h->flags, h->cfg.ess_threshold, step_io(h), 1,
         resampled_known, 0);
     toc(h, 1);
     SLAM_HIP_TRY(hipGetLastError());
@@ -411,12 +410,11 @@ int create_impl(const slam_pf_config* cfg, int64_t n_local, int64_t n_global, in
     A(h->spec_out, n);
     A(h->part, h->nchunks);
     A(h->bp, h->nb_norm);
-    A(h->gp, h->nb_norm / 64 + 2);
-    A(h->ncnt, h->nb_norm / 64 + 4);
+    A(h->gp, 8);
     A(h->wsum, 1);
     A(h->refp, 4);
     A(h->flags, kFlagWords);
-    A(h->counters, 8);
+    A(h->tk, 4 * kTicketWords);
     A(h->lm, 2 * std::max<int32_t>(n_landmarks, 1));
     A(h->noise, 3 * n);
     A(h->ctr, 4);
@@ -446,8 +444,7 @@ int create_impl(const slam_pf_config* cfg, int64_t n_local, int64_t n_global, in
     SLAM_HIP_TRY(hipMemcpy(h->w, tmp.data(), n * sizeof(double), hipMemcpyHostToDevice));
     SLAM_HIP_TRY(hipMemcpy(h->refp, cfg->x0, 3 * sizeof(double), hipMemcpyHostToDevice));
     SLAM_HIP_TRY(hipMemset(h->flags, 0, kFlagWords * sizeof(int32_t)));
-    SLAM_HIP_TRY(hipMemset(h->counters, 0, 8 * sizeof(unsigned)));
-    SLAM_HIP_TRY(hipMemset(h->ncnt, 0, (h->nb_norm / 64 + 4) * sizeof(unsigned)));
+    SLAM_HIP_TRY(hipMemset(h->tk, 0, 4 * kTicketWords * sizeof(unsigned)));
     SLAM_HIP_TRY(hipMemset(h->ctr, 0, 4 * sizeof(int32_t)));
     if (n_landmarks > 0)
         SLAM_HIP_TRY(hipMemcpy(h->lm, landmarks, 2 * n_landmarks * sizeof(double), hipMemcpyHostToDevice));
@@ -687,7 +684,7 @@ int slam_pf_weight_sum(slam_pf* h, double* sum_out) {
     SLAM_HIP_TRY(hipSetDevice(h->device));
     chunk_sum_kernel<<<h->nchunks, 512, 0, h->stream>>>(h->w, h->n, h->part, h->tail_leaves,
                                                          h->tail_ops, h->n_tail_leaves,
-                                                         h->n_tail_ops, h->counters, h->wsum);
+                                                         h->n_tail_ops, h->tk, h->wsum);
     SLAM_HIP_TRY(hipGetLastError());
     SLAM_HIP_TRY(hipMemcpyAsync(sum_out, h->wsum, 8, hipMemcpyDeviceToHost, h->stream));
     SLAM_HIP_TRY(hipStreamSynchronize(h->stream));

@@ -93,21 +93,42 @@ __device__ __forceinline__ S ld_wt_struct(const S* p) {
     return v;
 }
 
-// Last-arriver election: true in exactly one block, after every block has
-// published its write-through partials.  The ticket word is re-zeroed by the
-// winner (the next launch sees it after the kernel boundary).
-__device__ __forceinline__ bool arrive_last(unsigned* counter) {
+// ---- last-arriver election (Guideline 16 / microarch "fanin" + "dequeue"):
+// every block takes a ticket after publishing its write-through partials.
+// One counter word serialises its arrivals (~12 ns each), so the tickets are
+// two-level: blocks with equal blockIdx % 8 (one XCD under round-robin
+// dispatch) share a counter on a 128-B line of its own, and the last of each
+// residue class takes a ticket on the top word.  A ticket block is
+// kTicketWords unsigned words; every word is re-zeroed by its last arriver.
+constexpr int kTicketStride = 32;                       // 128 B
+constexpr int kTicketWords = 9 * kTicketStride;
+
+__device__ __forceinline__ bool arrive_last_n(unsigned* counter, const unsigned expected) {
     __shared__ int last;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");     // every storing wave drains
     __syncthreads();
     if (threadIdx.x == 0) {
         const unsigned t =
             __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        last = (t == gridDim.x - 1) ? 1 : 0;
+        last = (t == expected - 1) ? 1 : 0;
         if (last) __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     __syncthreads();
     return last != 0;
+}
+
+__device__ __forceinline__ int ticket_groups() { return gridDim.x < 8 ? (int)gridDim.x : 8; }
+
+// level 1 of the two-level ticket: true in the last block of this residue class
+__device__ __forceinline__ bool arrive_group(unsigned* tk) {
+    const int G = ticket_groups(), g = blockIdx.x % G;
+    const unsigned ng = (gridDim.x - g + G - 1) / G;
+    return arrive_last_n(tk + (1 + g) * kTicketStride, ng);
+}
+
+__device__ __forceinline__ bool arrive_last(unsigned* tk) {
+    if (!arrive_group(tk)) return false;
+    return arrive_last_n(tk, (unsigned)ticket_groups());
 }
 
 // ---- systematic resampling positions (particle_filter.py:213-215)
@@ -458,43 +479,26 @@ __device__ __forceinline__ BlockPartial bp_block_reduce(BlockPartial a, BlockPar
     return r;
 }
 
-// ticket on `counter` among `expected` arrivers; true in the last one
-__device__ __forceinline__ bool arrive_last_n(unsigned* counter, const unsigned expected) {
-    __shared__ int last;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        const unsigned t =
-            __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        last = (t == expected - 1) ? 1 : 0;
-        if (last) __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    __syncthreads();
-    return last != 0;
-}
-
 // Deterministic two-level combine of per-block partials: the last block of
-// every group of kGroup blocks merges the group (block order) into gp[g]; the
-// last group finisher merges the groups (group order).  Returns true in that
-// one block, with the total in thread 0's `out`.
-constexpr int kGroup = 64;
+// every residue class g (blocks g, g+G, g+2G, ...) merges its class in block
+// order into gp[g]; the last class finisher merges gp[0..G) in order.
+// Returns true in that one block, with the total in thread 0's `out`.
 __device__ bool hier_combine(const BlockPartial& mine, BlockPartial* bp, BlockPartial* gp,
-                             unsigned* cnt, BlockPartial* shp, BlockPartial& out) {
+                             unsigned* tk, BlockPartial* shp, BlockPartial& out) {
     const int b = blockIdx.x, nb = gridDim.x;
     if (threadIdx.x == 0) st_wt_struct(&bp[b], mine);
-    const int g = b / kGroup, g0 = g * kGroup;
-    const int gn = min(kGroup, nb - g0);
-    if (!arrive_last_n(&cnt[1 + g], (unsigned)gn)) return false;
+    if (!arrive_group(tk)) return false;
+    const int G = ticket_groups(), g = b % G;
     BlockPartial c;
     bp_zero(c);
-    if ((int)threadIdx.x < gn) c = ld_wt_struct(&bp[g0 + threadIdx.x]);
+    for (int k = g + (int)threadIdx.x * G; k < nb; k += (int)blockDim.x * G)
+        bp_merge(c, ld_wt_struct(&bp[k]));
     const BlockPartial gt = bp_block_reduce(c, shp);
     if (threadIdx.x == 0) st_wt_struct(&gp[g], gt);
-    const int ng = (nb + kGroup - 1) / kGroup;
-    if (!arrive_last_n(&cnt[0], (unsigned)ng)) return false;
+    if (!arrive_last_n(tk, (unsigned)G)) return false;
     BlockPartial f;
     bp_zero(f);
-    for (int k = threadIdx.x; k < ng; k += blockDim.x) bp_merge(f, ld_wt_struct(&gp[k]));
+    if ((int)threadIdx.x < G) f = ld_wt_struct(&gp[threadIdx.x]);
     out = bp_block_reduce(f, shp);
     return true;
 }

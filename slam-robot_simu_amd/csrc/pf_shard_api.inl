@@ -69,10 +69,10 @@ int slam_pf_shard_classify(slam_pf* h, const double* d_totals, int32_t rank, int
     shard_prefix_kernel<<<1, 64, 0, s>>>(d_totals, rank, h->sh.base_off);
     scan_classify_kernel<<<nb, kScanThreads, 0, s>>>(
         h->w, h->n, h->boff, h->sh.base_off, h->c, h->kincl, h->fexcl, h->bk, h->bf, h->boffk,
-        h->bofff, h->ktot, h->nspec, delta, h->gbase, h->counters + 2, h->flags, 1);
+        h->bofff, h->ktot, h->nspec, delta, h->gbase, h->tk + 2 * kTicketWords, h->flags, 1);
     scan_emit_kernel<<<nb, kScanThreads, 0, s>>>(h->w, h->n, h->c, h->kincl, h->fexcl, h->boffk,
                                                  h->bofff, h->spec_in, h->gbase, h->spec_out,
-                                                 h->nspec, h->ktot, 0, h->c, h->counters + 2,
+                                                 h->nspec, h->ktot, 0, h->c, h->tk + 2 * kTicketWords,
                                                  h->flags, 1);
     shard_meta_kernel<<<1, 64, 0, s>>>(h->nspec, h->ktot, d_meta);
     SLAM_HIP_TRY(hipGetLastError());
@@ -215,7 +215,7 @@ int slam_pf_shard_predict_update(slam_pf* h, double* d_partials) {
     if (rc) return rc;
     chunk_sum_kernel<<<h->nchunks, 512, 0, h->stream>>>(h->w_un, h->n, h->part, h->tail_leaves,
                                                          h->tail_ops, h->n_tail_leaves,
-                                                         h->n_tail_ops, h->counters, nullptr);
+                                                         h->n_tail_ops, h->tk, nullptr);
     SLAM_HIP_TRY(hipGetLastError());
     SLAM_HIP_TRY(hipMemcpyAsync(d_partials, h->part, h->nchunks * 8, hipMemcpyDeviceToDevice, h->stream));
     return SLAM_OK;
@@ -229,7 +229,7 @@ int slam_pf_shard_normalize(slam_pf* h, const double* d_all_partials, int64_t np
     shard_fold_sum_kernel<<<1, 256, 0, s>>>(d_all_partials, nparts, h->wsum);
     normalize_kernel<<<h->nb_norm, kNormThreads, 0, s>>>(
         h->n, h->w_un, h->w, h->wsum, h->pc.np_recip, h->x[c], h->y[c], h->th[c], h->refp, h->bp,
-        h->gp, h->bsum, h->boff, h->ncnt, h->flags, h->cfg.ess_threshold, step_io(h), 0, 0,
+        h->gp, h->bsum, h->boff, h->tk + kTicketWords, h->flags, h->cfg.ess_threshold, step_io(h), 0, 0,
         h->gbase);
     shard_record_kernel<<<1, kNormThreads, 0, s>>>(h->bp, h->nb_norm, h->x[c], h->y[c], h->th[c],
                                                    h->gbase, (ShardRecord*)d_record);
