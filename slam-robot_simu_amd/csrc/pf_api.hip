@@ -73,7 +73,6 @@ struct slam_pf {
     int32_t n_tail_leaves = 0, n_tail_ops = 0;
     int32_t nb_norm = 0;
     BlockPartial* bp = nullptr;
-    BlockPartial* gp = nullptr;     // residue-class partials of the two-level combine
     double* wsum = nullptr;
     double* refp = nullptr;
     int32_t* flags = nullptr;
@@ -309,10 +308,12 @@ int launch_reduce(slam_pf* h, int32_t resampled_known) {
     chunk_sum_kernel<<<h->nchunks, 512, 0, s>>>(h->w_un, n, h->part, h->tail_leaves, h->tail_ops,
                                                  h->n_tail_leaves, h->n_tail_ops, h->tk,
                                                  h->wsum);
-    normalize_kernel<<<h->nb_norm, kNormThreads, 0, s>>>(
-        n, h->w_un, h->w, h->wsum, h->pc.np_recip, h->x[c], h->y[c], h->th[c], h->refp, h->bp,
-        h->gp, h->bsum, h->boff, h->tk + kTicketWords, h->flags, h->cfg.ess_threshold, step_io(h), 1,
-        resampled_known, 0);
+    normalize_kernel<<<h->nb_norm, kNormThreads, 0, s>>>(n, h->w_un, h->w, h->wsum,
+                                                          h->pc.np_recip, h->x[c], h->y[c],
+                                                          h->th[c], h->refp, h->bp, h->bsum, 0);
+    finalize_kernel<<<1, 1024, 0, s>>>(h->bp, h->nb_norm, h->bsum, h->boff, h->x[c], h->y[c],
+                                        h->th[c], h->refp, h->wsum, h->flags,
+                                        h->cfg.ess_threshold, step_io(h), resampled_known, 0);
     toc(h, 1);
     SLAM_HIP_TRY(hipGetLastError());
     return SLAM_OK;
@@ -410,7 +411,6 @@ int create_impl(const slam_pf_config* cfg, int64_t n_local, int64_t n_global, in
     A(h->spec_out, n);
     A(h->part, h->nchunks);
     A(h->bp, h->nb_norm);
-    A(h->gp, 8);
     A(h->wsum, 1);
     A(h->refp, 4);
     A(h->flags, kFlagWords);

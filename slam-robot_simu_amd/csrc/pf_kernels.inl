@@ -479,30 +479,6 @@ __device__ __forceinline__ BlockPartial bp_block_reduce(BlockPartial a, BlockPar
     return r;
 }
 
-// Deterministic two-level combine of per-block partials: the last block of
-// every residue class g (blocks g, g+G, g+2G, ...) merges its class in block
-// order into gp[g]; the last class finisher merges gp[0..G) in order.
-// Returns true in that one block, with the total in thread 0's `out`.
-__device__ bool hier_combine(const BlockPartial& mine, BlockPartial* bp, BlockPartial* gp,
-                             unsigned* tk, BlockPartial* shp, BlockPartial& out) {
-    const int b = blockIdx.x, nb = gridDim.x;
-    if (threadIdx.x == 0) st_wt_struct(&bp[b], mine);
-    if (!arrive_group(tk)) return false;
-    const int G = ticket_groups(), g = b % G;
-    BlockPartial c;
-    bp_zero(c);
-    for (int k = g + (int)threadIdx.x * G; k < nb; k += (int)blockDim.x * G)
-        bp_merge(c, ld_wt_struct(&bp[k]));
-    const BlockPartial gt = bp_block_reduce(c, shp);
-    if (threadIdx.x == 0) st_wt_struct(&gp[g], gt);
-    if (!arrive_last_n(tk, (unsigned)G)) return false;
-    BlockPartial f;
-    bp_zero(f);
-    if ((int)threadIdx.x < G) f = ld_wt_struct(&gp[threadIdx.x]);
-    out = bp_block_reduce(f, shp);
-    return true;
-}
-
 // result record from the combined partial (x_est = particle at the argmax)
 __device__ void write_result(const BlockPartial& r, const double* xs, const double* ys,
                              const double* ts, const int64_t gbase, double* refp,
@@ -539,14 +515,9 @@ __device__ void write_result(const BlockPartial& r, const double* xs, const doub
 __global__ __launch_bounds__(kNormThreads) void normalize_kernel(
     const int64_t n, const double* __restrict__ w_un, double* __restrict__ w,
     const double* __restrict__ s_in, const double np_recip, const double* __restrict__ xs,
-    const double* __restrict__ ys, const double* __restrict__ ts, double* __restrict__ refp,
-    BlockPartial* __restrict__ bp, BlockPartial* __restrict__ gp, double* __restrict__ bsum,
-    double* __restrict__ boff, unsigned* __restrict__ cnt, int32_t* __restrict__ flags,
-    const double ess_th, StepIO io, const int32_t write_res, const int32_t resampled_known,
-    const int64_t gbase) {
+    const double* __restrict__ ys, const double* __restrict__ ts, const double* __restrict__ refp,
+    BlockPartial* __restrict__ bp, double* __restrict__ bsum, const int64_t gbase) {
     __shared__ BlockPartial shp[kNormThreads / 64];
-    __shared__ double shd[kNormThreads / 64 + 1];
-    __shared__ int32_t want_scan;
     const double s = *s_in;
     const double r0 = refp[0], r1 = refp[1], r2 = refp[2];
     const int64_t base = (int64_t)blockIdx.x * kNormPer + threadIdx.x;
@@ -600,24 +571,57 @@ __global__ __launch_bounds__(kNormThreads) void normalize_kernel(
         }
     }
     const BlockPartial r = bp_block_reduce(a, shp);
-    if (threadIdx.x == 0) st_wt_d(&bsum[blockIdx.x], r.sw);   // approximate block total (S1)
-    if (!write_res) {
-        if (threadIdx.x == 0) st_wt_struct(&bp[blockIdx.x], r);
-        return;
+    if (threadIdx.x == 0) {
+        bp[blockIdx.x] = r;
+        bsum[blockIdx.x] = r.sw;                         // approximate block total (S1)
     }
-    BlockPartial tot;
-    if (!hier_combine(r, bp, gp, cnt, shp, tot)) return;
+}
+
+// Combine the normalise blocks' partials in block order (one block of up to
+// 1024 lanes, one partial per lane, then a fixed tree), write the step's
+// result record, advance the step context, and -- when the next step
+// resamples -- scan the block totals for its exact cumsum.  A separate launch
+// instead of a last-arriver tail: the kernel boundary costs less than the
+// serial ticket/load chain of an in-kernel combine.
+__global__ __launch_bounds__(1024) void finalize_kernel(
+    const BlockPartial* __restrict__ bp, const int32_t nb, const double* __restrict__ bsum,
+    double* __restrict__ boff, const double* __restrict__ xs, const double* __restrict__ ys,
+    const double* __restrict__ ts, double* __restrict__ refp, const double* __restrict__ s_in,
+    int32_t* __restrict__ flags, const double ess_th, StepIO io, const int32_t resampled_known,
+    const int64_t gbase) {
+    __shared__ BlockPartial shp[1024 / 64];
+    __shared__ double shd[1024 / 64 + 1];
+    __shared__ int32_t want_scan;
+    BlockPartial c;
+    bp_zero(c);
+    for (int k = threadIdx.x; k < nb; k += blockDim.x) bp_merge(c, bp[k]);
+    const BlockPartial tot = bp_block_reduce(c, shp);
     if (threadIdx.x == 0) {
         const int32_t st = io.ctr[0];
-        write_result(tot, xs, ys, ts, gbase, refp, s, flags, ess_th, io.res + st, resampled_known);
+        write_result(tot, xs, ys, ts, gbase, refp, *s_in, flags, ess_th, io.res + st,
+                     resampled_known);
         want_scan = flags[kFlagResample];
         io.ctr[0] = st + 1;                              // advance the step context
         io.ctr[1] = io.ctr[1] + 1;
     }
     __syncthreads();
-    // the next step resamples: prefix of the block totals for its exact cumsum
-    if (want_scan)
-        block_scan_array<double, kNormThreads>(bsum, boff, gridDim.x, boff + gridDim.x, shd);
+    if (want_scan) {
+        // exclusive prefix of the block totals (plain loads: previous kernel's data)
+        const int per = (nb + 1023) / 1024;
+        const int b0 = threadIdx.x * per;
+        double loc = 0.0;
+        for (int k = 0; k < per; ++k)
+            if (b0 + k < nb) loc += bsum[b0 + k];
+        double total;
+        double ex = block_excl_scan<double, 1024>(loc, shd, total);
+        for (int k = 0; k < per; ++k)
+            if (b0 + k < nb) {
+                const double v = bsum[b0 + k];
+                boff[b0 + k] = ex;
+                ex = ex + v;
+            }
+        if (threadIdx.x == 0) boff[nb] = total;
+    }
 }
 
 // ====================================================================

@@ -240,7 +240,7 @@ __global__ __launch_bounds__(kNormThreads) void shard_record_kernel(
     __shared__ BlockPartial shp[kNormThreads / 64];
     BlockPartial c;
     bp_zero(c);
-    for (int k = threadIdx.x; k < nb; k += blockDim.x) bp_merge(c, ld_wt_struct(&bp[k]));
+    for (int k = threadIdx.x; k < nb; k += blockDim.x) bp_merge(c, bp[k]);
     const BlockPartial tot = bp_block_reduce(c, shp);
     if (threadIdx.x == 0) {
         ShardRecord r;

@@ -227,10 +227,10 @@ int slam_pf_shard_normalize(slam_pf* h, const double* d_all_partials, int64_t np
     hipStream_t s = h->stream;
     const int c = h->cur;
     shard_fold_sum_kernel<<<1, 256, 0, s>>>(d_all_partials, nparts, h->wsum);
-    normalize_kernel<<<h->nb_norm, kNormThreads, 0, s>>>(
-        h->n, h->w_un, h->w, h->wsum, h->pc.np_recip, h->x[c], h->y[c], h->th[c], h->refp, h->bp,
-        h->gp, h->bsum, h->boff, h->tk + kTicketWords, h->flags, h->cfg.ess_threshold, step_io(h), 0, 0,
-        h->gbase);
+    normalize_kernel<<<h->nb_norm, kNormThreads, 0, s>>>(h->n, h->w_un, h->w, h->wsum,
+                                                          h->pc.np_recip, h->x[c], h->y[c],
+                                                          h->th[c], h->refp, h->bp, h->bsum,
+                                                          h->gbase);
     shard_record_kernel<<<1, kNormThreads, 0, s>>>(h->bp, h->nb_norm, h->x[c], h->y[c], h->th[c],
                                                    h->gbase, (ShardRecord*)d_record);
     SLAM_HIP_TRY(hipGetLastError());

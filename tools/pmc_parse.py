@@ -1,0 +1,70 @@
+#!/usr/bin/env python
+"""Summarise the rocprofv3 --pmc passes of tools/pmc.sh per kernel.
+
+HBM bytes per launch follow MI355X_MICROARCH.md §HBM: FETCH_SIZE (KB) reads
+exactly half of a wide coalesced streaming read on gfx950, so it is doubled;
+WRITE_SIZE (KB) is taken as is.  Writes profiles/<tag>_pmc.json and, for the
+bench, profiles/pmc_traffic.json with the fused kernel's per-launch traffic.
+"""
+import collections
+import csv
+import glob
+import json
+import os
+import sys
+
+
+def load(dirpath):
+    per = collections.defaultdict(lambda: collections.defaultdict(list))
+    for f in glob.glob(os.path.join(dirpath, "p*", "pmc_counter_collection.csv")):
+        for r in csv.DictReader(open(f)):
+            name = r["Kernel_Name"]
+            per[name][r["Counter_Name"]].append(float(r["Counter_Value"]))
+            per[name]["_dur_ns"].append(float(r["End_Timestamp"]) - float(r["Start_Timestamp"]))
+    return per
+
+
+def short(name):
+    n = name.replace("slam::", "").replace("void ", "")
+    return n.split("(")[0]
+
+
+def main(src, tag):
+    per = load(src)
+    out = {}
+    for name, cs in per.items():
+        if "rocclr" in name:
+            continue
+        d = {k: sum(v) / len(v) for k, v in cs.items()}
+        rec = {"launch_records": len(cs.get("FETCH_SIZE", [])), "avg_dur_us_profiled": d["_dur_ns"] / 1e3}
+        if "FETCH_SIZE" in d:
+            rec["hbm_read_bytes"] = 2 * d["FETCH_SIZE"] * 1024
+        if "WRITE_SIZE" in d:
+            rec["hbm_write_bytes"] = d["WRITE_SIZE"] * 1024
+        for k in ("SQ_WAVES", "SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS", "SQ_WAVE_CYCLES",
+                  "SQ_BUSY_CYCLES", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY",
+                  "GRBM_GUI_ACTIVE", "SQ_INSTS_VMEM_RD", "SQ_INSTS_VMEM_WR"):
+            if k in d:
+                rec[k] = d[k]
+        if "SQ_INSTS_VALU" in d and "SQ_WAVES" in d and d["SQ_WAVES"]:
+            rec["valu_insts_per_wave"] = d["SQ_INSTS_VALU"] / d["SQ_WAVES"]
+        out[short(name) + ("" if "<" not in name else name[name.index("<"):name.index(">") + 1])] = rec
+    os.makedirs("profiles", exist_ok=True)
+    with open(f"profiles/{tag}_pmc.json", "w") as f:
+        json.dump(out, f, indent=1, sort_keys=True)
+    fused = {k: v for k, v in out.items() if k.startswith("pf_fused_kernel<1, 1")}
+    if fused:
+        v = next(iter(fused.values()))
+        traffic = v.get("hbm_read_bytes", 0) + v.get("hbm_write_bytes", 0)
+        with open("profiles/pmc_traffic.json", "w") as f:
+            json.dump({"source": f"profiles/{tag}_pmc.json", "kernel": "pf_fused_kernel<1, 1, false>",
+                       "fused_kernel_hbm_bytes_per_launch": traffic,
+                       "note": "FETCH_SIZE x2 (gfx950 half-count) + WRITE_SIZE, KB -> B, mean over launches"},
+                      f, indent=1)
+    for k, v in sorted(out.items()):
+        print(f"{k:45s} rd {v.get('hbm_read_bytes', 0)/1e6:8.2f} MB  wr {v.get('hbm_write_bytes', 0)/1e6:7.2f} MB"
+              f"  valu/wave {v.get('valu_insts_per_wave', 0):8.1f}  waves {v.get('SQ_WAVES', 0):8.0f}")
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], sys.argv[2] if len(sys.argv) > 2 else "r1")
