@@ -155,6 +155,86 @@ int slam_pf_shard_normalize(slam_pf* h, const double* d_all_partials, int64_t np
 int slam_pf_shard_finish(slam_pf* h, const void* d_all_records, int32_t world,
                          slam_pf_result* res);
 
+/* ====================================================================
+ * EKF localisation -- replaces ExtendedKalmanFilter
+ * (extended_kalman_filter.py:17-205) for a batch of independent filters
+ * (batch = 1 is the reference's single filter).  State on the device is
+ * structure-of-arrays: x[3][batch], P[9][batch] (row-major 3x3).
+ * ==================================================================== */
+typedef struct slam_ekf slam_ekf;
+
+typedef struct {
+    double dt;            /* extended_kalman_filter.py:29  DT_s */
+    double vel;           /* :46-48  V (control, also in jacobF :188) */
+    double omega;         /* :46     omega */
+    double q[9];          /* :62-66  Q (process noise, 3x3) */
+    double r[4];          /* :68-70  R (observation noise, 2x2) */
+    double x0[3];         /* :74-79  initial estimate */
+    double p0[9];         /* :81-84  initial covariance */
+} slam_ekf_config;
+
+/* ExtendedKalmanFilter.__init__: every filter starts at (x0, p0). */
+int slam_ekf_create(const slam_ekf_config* cfg, int64_t batch, int device, slam_ekf** out);
+int slam_ekf_destroy(slam_ekf* h);
+int slam_ekf_set_state(slam_ekf* h, const double* x /* batch x 3 */, const double* P /* batch x 9 */);
+int slam_ekf_get_state(slam_ekf* h, double* x /* batch x 3 */, double* P /* batch x 9 */);
+/* The filter half of main_ekf (extended_kalman_filter.py:108-128): prediction
+ * with jacobF, Kalman gain with inv(S), update, limit_angle on the yaw,
+ * P = (I - G C) P_m.  control = {v, omega} or NULL for the configured values;
+ * z: batch x 2 world positions (:141-146).  Outputs may be NULL. */
+int slam_ekf_step(slam_ekf* h, const double* control, const double* z, double* x_hat_m,
+                  double* x_hat, double* P);
+/* n_steps filter steps in one launch (state stays in registers):
+ * z_all: n_steps x batch x 2; x_hat_all: n_steps x batch x 3 or NULL;
+ * the final state is kept in the handle. */
+int slam_ekf_run(slam_ekf* h, int32_t n_steps, const double* control, const double* z_all,
+                 double* x_hat_all);
+/* Device-resident variant (bench path): z_dev / x_hat_dev are device pointers
+ * (x_hat_dev may be NULL); asynchronous on the handle's stream. */
+int slam_ekf_run_device(slam_ekf* h, int32_t n_steps, const double* control, const double* z_dev,
+                        double* x_hat_dev);
+int slam_ekf_synchronize(slam_ekf* h);
+
+/* ====================================================================
+ * EKF-SLAM (BASELINE config 4, an extension: the reference has no EKF-SLAM).
+ * State mu = (robot x, y, yaw, landmark_0 x, y, phi, ...), n = 3 + 3 * n_lm;
+ * P is n x n fp64 in HBM (7.2 GB at n = 30,003).  Robot motion is the
+ * reference EKF's model (extended_kalman_filter.py:160-194); the landmark
+ * measurement is graph_based_slam.py's ScanSensor (range, bearing,
+ * orientation; :150-153) with its covariance (:187-194).
+ * ==================================================================== */
+typedef struct slam_ekfslam slam_ekfslam;
+
+typedef struct {
+    double dt;            /* motion step (s) */
+    double q_robot[9];    /* robot process noise */
+    double r_dist;        /* ScanSensor range noise fraction  (graph_based_slam.py:187-192) */
+    double r_dir;         /* bearing noise (rad) */
+    double r_orient;      /* orientation noise (rad) */
+} slam_ekfslam_config;
+
+int slam_ekfslam_create(const slam_ekfslam_config* cfg, int64_t n_landmarks, int device,
+                        slam_ekfslam** out);
+int slam_ekfslam_destroy(slam_ekfslam* h);
+/* mu: n; P: n x n row-major (only the lower triangle is read). */
+int slam_ekfslam_set_state(slam_ekfslam* h, const double* mu, const double* P);
+/* mu: n; P <- diag(p_diag) (n values) without an n x n host buffer. */
+int slam_ekfslam_init_diag(slam_ekfslam* h, const double* mu, const double* p_diag);
+/* P may be NULL; when given it receives the full symmetric n x n matrix. */
+int slam_ekfslam_get_state(slam_ekfslam* h, double* mu, double* P);
+/* Prediction: robot pose through the motion model, P <- F P F^T + Q on the
+ * robot rows/columns (O(n)). control = {v, omega}. */
+int slam_ekfslam_predict(slam_ekfslam* h, const double* control);
+/* Batched update with k observed landmarks: ids[k], obs[k x 3] (range,
+ * bearing, orientation).  K = P H^T S^-1, mu += K e, P <- P - K (P H^T)^T
+ * (a rank-3k update of the lower triangle: the HBM-bound kernel). */
+int slam_ekfslam_update(slam_ekfslam* h, int32_t k, const int64_t* ids, const double* obs);
+int slam_ekfslam_step(slam_ekfslam* h, const double* control, int32_t k, const int64_t* ids,
+                      const double* obs);
+/* Device time of the last update (ms): out[5] = {H + P H^T gather, S^-1, K and mu,
+ * rank-3k covariance update, 0}. */
+int slam_ekfslam_timing(slam_ekfslam* h, double* out);
+
 #ifdef __cplusplus
 }
 #endif

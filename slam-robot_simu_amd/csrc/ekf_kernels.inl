@@ -1,0 +1,457 @@
+// ekf_kernels.inl -- EKF localisation (batched) and EKF-SLAM kernels (gfx950).
+//
+// Batched EKF: one lane owns one filter for a whole run; its state (3 + 9
+// doubles) stays in registers across steps, only the observations stream in
+// and the estimates stream out (16 B + 24 B per filter-step: HBM-bound).
+//
+// EKF-SLAM: the n x n covariance lives in HBM as a row-major matrix of which
+// only the lower triangle (i >= j) is kept current.  The update is
+//   PHt = P H^T   (n x m, m = 3k; H has 6 non-zeros per row)
+//   S   = H PHt + R,  Sinv = S^-1   (one workgroup, in LDS)
+//   K   = PHt Sinv,   mu += K e
+//   P  -= K PHt^T    (lower triangle only; fp64 MFMA 16x16x4 tiles)
+// The last line reads and writes the lower half of P once: 8 n^2 B per
+// update, the HBM bound of the whole step.
+#pragma once
+
+#include "common.hpp"
+
+namespace slam {
+
+struct EKFConst {
+    double dt, vel, omega;
+    double q[9];
+    double r[4];
+};
+
+// One step of extended_kalman_filter.py:108-128 on a register-resident filter.
+// Products with the structural 0/1 entries of A, B, C, jacobF are exact in the
+// reference's BLAS calls; the remaining two-term sums follow OpenBLAS dgemm's
+// accumulation (fma into a running sum, k ascending).
+__device__ __forceinline__ void ekf_filter_step(double& x, double& y, double& t, double* P,
+                                                const double zx, const double zy, const double v,
+                                                const double om, const EKFConst& c, double* xm_out) {
+    double sy, cy;
+    sincos(t, &sy, &cy);
+    // __f (:160-178): a = DT cos(yaw), b = DT sin(yaw); x' = A x + B u
+    const double a = c.dt * cy, b = c.dt * sy;
+    const double xm = x + v * a;
+    const double ym = y + v * b;
+    const double tm = wrap_angle(t + om * c.dt);
+    // jacobF (:180-194) at the previous estimate
+    const double f02 = (-c.dt) * v * sy;
+    const double f12 = c.dt * v * cy;
+    // P_m = F P F^T + Q  (:117-118)
+    double FP[9];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+        FP[j] = fma(f02, P[6 + j], P[j]);
+        FP[3 + j] = fma(f12, P[6 + j], P[3 + j]);
+        FP[6 + j] = P[6 + j];
+    }
+    double Pm[9];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        Pm[3 * i + 0] = fma(FP[3 * i + 2], f02, FP[3 * i + 0]) + c.q[3 * i + 0];
+        Pm[3 * i + 1] = fma(FP[3 * i + 2], f12, FP[3 * i + 1]) + c.q[3 * i + 1];
+        Pm[3 * i + 2] = FP[3 * i + 2] + c.q[3 * i + 2];
+    }
+    // S = C P_m C^T + R; G = P_m C^T S^-1  (:149-158)
+    const double s00 = Pm[0] + c.r[0], s01 = Pm[1] + c.r[1];
+    const double s10 = Pm[3] + c.r[2], s11 = Pm[4] + c.r[3];
+    const double det = s00 * s11 - s01 * s10;
+    const double i00 = s11 / det, i01 = -s01 / det, i10 = -s10 / det, i11 = s00 / det;
+    double G[6];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        G[2 * i + 0] = fma(Pm[3 * i + 1], i10, Pm[3 * i + 0] * i00);
+        G[2 * i + 1] = fma(Pm[3 * i + 1], i11, Pm[3 * i + 0] * i01);
+    }
+    // x_hat = x_m + G (z - C x_m), yaw wrapped  (:121-126)
+    const double e0 = zx - xm, e1 = zy - ym;
+    x = xm + fma(G[1], e1, G[0] * e0);
+    y = ym + fma(G[3], e1, G[2] * e0);
+    t = wrap_angle(tm + fma(G[5], e1, G[4] * e0));
+    // P = (I - G C) P_m  (:128-129)
+    const double M[9] = {1.0 - G[0], -G[1], 0.0, -G[2], 1.0 - G[3], 0.0, -G[4], -G[5], 1.0};
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            double acc = M[3 * i] * Pm[j];
+            acc = fma(M[3 * i + 1], Pm[3 + j], acc);
+            P[3 * i + j] = fma(M[3 * i + 2], Pm[6 + j], acc);
+        }
+    if (xm_out) {
+        xm_out[0] = xm;
+        xm_out[1] = ym;
+        xm_out[2] = tm;
+    }
+}
+
+// n_steps steps for every filter in one launch.  SoA state: xs[3][B], Ps[9][B];
+// z_all: [step][B][2]; xh_all: [step][B][3] (optional); xm_last: [B][3] x_hat_m
+// of the last step (optional).
+__global__ __launch_bounds__(256) void ekf_run_kernel(
+    const int64_t B, const int32_t n_steps, const EKFConst c, const double v, const double om,
+    double* __restrict__ xs, double* __restrict__ Ps, const double* __restrict__ z_all,
+    double* __restrict__ xh_all, double* __restrict__ xm_last) {
+    const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= B) return;
+    double x = xs[b], y = xs[B + b], t = xs[2 * B + b];
+    double P[9];
+#pragma unroll
+    for (int q = 0; q < 9; ++q) P[q] = Ps[q * B + b];
+    double xm[3];
+    for (int s = 0; s < n_steps; ++s) {
+        const double2 z = reinterpret_cast<const double2*>(z_all)[(int64_t)s * B + b];
+        ekf_filter_step(x, y, t, P, z.x, z.y, v, om, c, xm);
+        if (xh_all) {
+            double* o = xh_all + ((int64_t)s * B + b) * 3;
+            o[0] = x;
+            o[1] = y;
+            o[2] = t;
+        }
+    }
+    xs[b] = x;
+    xs[B + b] = y;
+    xs[2 * B + b] = t;
+#pragma unroll
+    for (int q = 0; q < 9; ++q) Ps[q * B + b] = P[q];
+    if (xm_last && n_steps > 0) {
+        xm_last[3 * b] = xm[0];
+        xm_last[3 * b + 1] = xm[1];
+        xm_last[3 * b + 2] = xm[2];
+    }
+}
+
+// ====================================================================
+// EKF-SLAM
+// ====================================================================
+constexpr int kEksTile = 128;        // rank-update tile (rows and columns)
+constexpr int kEksThreads = 512;     // 8 waves: 4 (rows of 32) x 2 (columns of 64)
+constexpr int kEksMaxM = 120;        // 3k <= 120 (S and S^-1 in LDS)
+constexpr int kEksKC = 32;           // k-chunk staged in LDS per pass
+constexpr int kEksKS = kEksKC + 1;   // odd LDS row stride: conflict-free fragment reads
+
+struct EksConst {
+    double dt;
+    double q[9];
+    double r_dist, r_dir, r_orient;
+};
+
+// symmetric read from the lower-triangle storage
+__device__ __forceinline__ double psym(const double* P, const int64_t ld, const int64_t i,
+                                       const int64_t j) {
+    return (i >= j) ? P[i * ld + j] : P[j * ld + i];
+}
+
+// Robot rows/columns of F P F^T (landmark part): P[i][0:3] <- P[i][0:3] F^T, i >= 3.
+__global__ __launch_bounds__(256) void eks_predict_rows_kernel(double* __restrict__ P,
+                                                               const int64_t n, const int64_t ld,
+                                                               const double* __restrict__ mu,
+                                                               const double dt, const double v) {
+    const int64_t i = 3 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    double sy, cy;
+    sincos(mu[2], &sy, &cy);
+    const double f02 = (-dt) * v * sy, f12 = dt * v * cy;
+    double* r = P + i * ld;
+    const double p2 = r[2];
+    r[0] = fma(p2, f02, r[0]);
+    r[1] = fma(p2, f12, r[1]);
+}
+
+// Robot block and pose (after eks_predict_rows_kernel has read the old yaw).
+__global__ void eks_predict_pose_kernel(double* __restrict__ P, const int64_t ld,
+                                        double* __restrict__ mu, const EksConst c, const double v,
+                                        const double om) {
+    if (threadIdx.x != 0) return;
+    const double x = mu[0], y = mu[1], t = mu[2];
+    double sy, cy;
+    sincos(t, &sy, &cy);
+    const double f02 = (-c.dt) * v * sy, f12 = c.dt * v * cy;
+    double p[9];
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) p[3 * i + j] = psym(P, ld, i, j);
+    double FP[9];
+    for (int j = 0; j < 3; ++j) {
+        FP[j] = fma(f02, p[6 + j], p[j]);
+        FP[3 + j] = fma(f12, p[6 + j], p[3 + j]);
+        FP[6 + j] = p[6 + j];
+    }
+    for (int i = 0; i < 3; ++i) {
+        P[i * ld + 0] = fma(FP[3 * i + 2], f02, FP[3 * i + 0]) + c.q[3 * i + 0];
+        P[i * ld + 1] = fma(FP[3 * i + 2], f12, FP[3 * i + 1]) + c.q[3 * i + 1];
+        P[i * ld + 2] = FP[3 * i + 2] + c.q[3 * i + 2];
+    }
+    const double a = c.dt * cy, b = c.dt * sy;
+    mu[0] = x + v * a;
+    mu[1] = y + v * b;
+    mu[2] = wrap_angle(t + om * c.dt);
+}
+
+// Per observation t (landmark j = ids[t]): predicted ScanSensor measurement,
+// its Jacobians (robot Hr, landmark Hl, 3x3 each), the wrapped innovation and
+// the measurement variance diag(scan_cov(range)).  hs: [k][18]; e, rd: [M].
+__global__ void eks_build_kernel(const double* __restrict__ mu, const int64_t* __restrict__ ids,
+                                 const double* __restrict__ obs, const int32_t k, const int32_t M,
+                                 const EksConst c, double* __restrict__ hs, double* __restrict__ e,
+                                 double* __restrict__ rd) {
+    const int t = threadIdx.x;
+    for (int u = 3 * k + t; u < M; u += blockDim.x) {
+        e[u] = 0.0;
+        rd[u] = 1.0;
+    }
+    if (t >= k) return;
+    const int64_t j = ids[t];
+    const double xr = mu[0], yr = mu[1], th = mu[2];
+    const double lx = mu[3 + 3 * j], ly = mu[4 + 3 * j], lp = mu[5 + 3 * j];
+    const double psi = kHalfPi - th;
+    double s, co;
+    sincos(psi, &s, &co);
+    const double dx = lx - xr, dy = ly - yr;
+    const double rx = co * dx - s * dy;
+    const double ry = s * dx + co * dy;
+    const double rng = hypot(rx, ry);
+    const double brg = atan2(ry, rx);
+    const double ori = wrap_angle(psi + lp);
+    const double q = dx * dx + dy * dy;
+    const double r = sqrt(q);
+    double* H = hs + 18 * t;
+    // Hr (d/d robot x, y, yaw)
+    H[0] = -dx / r; H[1] = -dy / r; H[2] = 0.0;
+    H[3] = dy / q;  H[4] = -dx / q; H[5] = -1.0;
+    H[6] = 0.0;     H[7] = 0.0;     H[8] = -1.0;
+    // Hl (d/d landmark x, y, phi)
+    H[9] = dx / r;  H[10] = dy / r; H[11] = 0.0;
+    H[12] = -dy / q; H[13] = dx / q; H[14] = 0.0;
+    H[15] = 0.0;    H[16] = 0.0;    H[17] = 1.0;
+    const double* o = obs + 3 * t;
+    e[3 * t] = o[0] - rng;
+    e[3 * t + 1] = wrap_angle(o[1] - brg);
+    e[3 * t + 2] = wrap_angle(o[2] - ori);
+    // graph_based_slam.py:187-192
+    const double d = o[0] * c.r_dist;
+    const double sd = o[0] * sin(c.r_dir);
+    rd[3 * t] = d * d;
+    rd[3 * t + 1] = sd * sd;
+    rd[3 * t + 2] = c.r_dir * c.r_dir + c.r_orient * c.r_orient;
+}
+
+// PHt[i][u] = sum over the six non-zero columns of H row u of P[i][col] H[u][col]
+// (one lane per row i; rows >= n and columns >= 3k are zero).
+__global__ __launch_bounds__(256) void eks_pht_kernel(const double* __restrict__ P,
+                                                      const int64_t n, const int64_t ld,
+                                                      const int64_t n_pad,
+                                                      const int64_t* __restrict__ ids,
+                                                      const double* __restrict__ hs,
+                                                      const int32_t k, const int32_t M,
+                                                      double* __restrict__ pht) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n_pad) return;
+    double* out = pht + i * M;
+    if (i >= n) {
+        for (int u = 0; u < M; ++u) out[u] = 0.0;
+        return;
+    }
+    const double p0 = psym(P, ld, i, 0), p1 = psym(P, ld, i, 1), p2 = psym(P, ld, i, 2);
+    for (int t = 0; t < k; ++t) {
+        const int64_t c0 = 3 + 3 * ids[t];
+        const double l0 = psym(P, ld, i, c0), l1 = psym(P, ld, i, c0 + 1),
+                     l2 = psym(P, ld, i, c0 + 2);
+        const double* H = hs + 18 * t;
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            double acc = p0 * H[3 * a];
+            acc = fma(p1, H[3 * a + 1], acc);
+            acc = fma(p2, H[3 * a + 2], acc);
+            acc = fma(l0, H[9 + 3 * a], acc);
+            acc = fma(l1, H[9 + 3 * a + 1], acc);
+            acc = fma(l2, H[9 + 3 * a + 2], acc);
+            out[3 * t + a] = acc;
+        }
+    }
+    for (int u = 3 * k; u < M; ++u) out[u] = 0.0;
+}
+
+// S = H PHt + R (padded to M with the identity), inverted in place in LDS by
+// Gauss-Jordan elimination (S is symmetric positive definite: no pivoting).
+__global__ __launch_bounds__(1024) void eks_gain_kernel(const double* __restrict__ pht,
+                                                        const int64_t* __restrict__ ids,
+                                                        const double* __restrict__ hs,
+                                                        const double* __restrict__ rd,
+                                                        const int32_t k, const int32_t M,
+                                                        double* __restrict__ sinv_out) {
+    extern __shared__ double S[];           // M * M
+    __shared__ double colp[kEksMaxM];
+    const int m = 3 * k;
+    for (int idx = threadIdx.x; idx < M * M; idx += blockDim.x) {
+        const int a = idx / M, u = idx % M;
+        double v;
+        if (a < m && u < m) {
+            const int t = a / 3, al = a % 3;
+            const double* H = hs + 18 * t;
+            const int64_t c0 = 3 + 3 * ids[t];
+            double acc = H[3 * al] * pht[0 * M + u];
+            acc = fma(H[3 * al + 1], pht[1 * M + u], acc);
+            acc = fma(H[3 * al + 2], pht[2 * M + u], acc);
+            acc = fma(H[9 + 3 * al], pht[c0 * M + u], acc);
+            acc = fma(H[9 + 3 * al + 1], pht[(c0 + 1) * M + u], acc);
+            acc = fma(H[9 + 3 * al + 2], pht[(c0 + 2) * M + u], acc);
+            v = acc + ((a == u) ? rd[a] : 0.0);
+        } else {
+            v = (a == u) ? 1.0 : 0.0;
+        }
+        S[idx] = v;
+    }
+    __syncthreads();
+    for (int p = 0; p < M; ++p) {
+        const double inv_p = 1.0 / S[p * M + p];
+        for (int i = threadIdx.x; i < M; i += blockDim.x) colp[i] = S[i * M + p];
+        __syncthreads();
+        for (int j = threadIdx.x; j < M; j += blockDim.x)
+            S[p * M + j] = (j == p) ? inv_p : S[p * M + j] * inv_p;
+        __syncthreads();
+        for (int idx = threadIdx.x; idx < M * M; idx += blockDim.x) {
+            const int i = idx / M, j = idx % M;
+            if (i == p) continue;
+            const double f = colp[i];
+            S[idx] = (j == p) ? -f * inv_p : S[idx] - f * S[p * M + j];
+        }
+        __syncthreads();
+    }
+    for (int idx = threadIdx.x; idx < M * M; idx += blockDim.x) sinv_out[idx] = S[idx];
+}
+
+// K = PHt S^-1 (rows of n_pad), mu += K e, yaw wrapped.
+__global__ __launch_bounds__(256) void eks_apply_kernel(const double* __restrict__ pht,
+                                                        const double* __restrict__ sinv,
+                                                        const double* __restrict__ e,
+                                                        const int64_t n, const int64_t n_pad,
+                                                        const int32_t M, double* __restrict__ kg,
+                                                        double* __restrict__ mu) {
+    extern __shared__ double Si[];          // M * M
+    for (int idx = threadIdx.x; idx < M * M; idx += blockDim.x) Si[idx] = sinv[idx];
+    __syncthreads();
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n_pad) return;
+    const double* prow = pht + i * M;
+    double* krow = kg + i * M;
+    double dmu = 0.0;
+    constexpr int U = 12;
+    for (int u0 = 0; u0 < M; u0 += U) {
+        double acc[U];
+#pragma unroll
+        for (int q = 0; q < U; ++q) acc[q] = 0.0;
+        for (int v = 0; v < M; ++v) {
+            const double pv = prow[v];
+#pragma unroll
+            for (int q = 0; q < U; ++q)
+                if (u0 + q < M) acc[q] = fma(pv, Si[v * M + u0 + q], acc[q]);
+        }
+#pragma unroll
+        for (int q = 0; q < U; ++q)
+            if (u0 + q < M) {
+                krow[u0 + q] = acc[q];
+                dmu = fma(acc[q], e[u0 + q], dmu);
+            }
+    }
+    if (i < n) {
+        double m = mu[i] + dmu;
+        if (i == 2) m = wrap_angle(m);
+        mu[i] = m;
+    }
+}
+
+// P[i][j] -= sum_u K[i][u] PHt[j][u] for i >= j, one 128 x 128 lower tile per
+// workgroup.  fp64 MFMA 16x16x4: A = K rows (lane l: row l&15, k l>>4),
+// B = PHt^T (lane l: k l>>4, column l&15), D: column l&15, row (l>>4) + 4 r.
+// Tiles are numbered so that each XCD (blockIdx % 8) takes a contiguous range
+// of tile rows and reuses its K rows through its own L2.
+__global__ __launch_bounds__(kEksThreads) void eks_rank_update_kernel(
+    double* __restrict__ P, const int64_t n, const int64_t ld, const double* __restrict__ kg,
+    const double* __restrict__ pht, const int32_t M, const int64_t n_tiles) {
+    __shared__ double Ks[kEksTile * kEksKS];    // K rows of the tile, one k-chunk
+    __shared__ double Hs[kEksTile * kEksKS];    // PHt rows of the tile's columns
+    const int64_t per_xcd = (n_tiles + 7) / 8;
+    const int64_t L = (int64_t)(blockIdx.x % 8) * per_xcd + blockIdx.x / 8;
+    if (L >= n_tiles) return;
+    int64_t ti = (int64_t)((sqrt(8.0 * (double)L + 1.0) - 1.0) * 0.5);
+    while (ti * (ti + 1) / 2 > L) --ti;
+    while ((ti + 1) * (ti + 2) / 2 <= L) ++ti;
+    const int64_t tj = L - ti * (ti + 1) / 2;
+    const int64_t r0 = ti * kEksTile, c0 = tj * kEksTile;
+    const int tid = threadIdx.x;
+    const int lane = tid & 63, wave = tid >> 6;
+    const int wr = (wave >> 1) * 32;        // wave's 32 rows
+    const int wc = (wave & 1) * 64;         // wave's 64 columns
+    const int lr = lane & 15, lk = lane >> 4;
+    typedef double double4v __attribute__((ext_vector_type(4)));
+    double4v acc[2][4];
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) acc[a][b] = double4v{0.0, 0.0, 0.0, 0.0};
+    const double* ksrc = kg + r0 * M;
+    const double* hsrc = pht + c0 * M;
+    for (int kc = 0; kc < M; kc += kEksKC) {
+        const int kw = min(kEksKC, M - kc);             // multiple of 4
+        __syncthreads();
+#pragma unroll
+        for (int s = 0; s < kEksTile * kEksKC / kEksThreads; ++s) {
+            const int idx = tid + s * kEksThreads;
+            const int r = idx / kEksKC, q = idx % kEksKC;
+            const bool ok = q < kw;
+            Ks[r * kEksKS + q] = ok ? ksrc[(int64_t)r * M + kc + q] : 0.0;
+            Hs[r * kEksKS + q] = ok ? hsrc[(int64_t)r * M + kc + q] : 0.0;
+        }
+        __syncthreads();
+        for (int k0 = 0; k0 < kw; k0 += 4) {
+            double fa[2], fb[4];
+#pragma unroll
+            for (int a = 0; a < 2; ++a) fa[a] = Ks[(wr + 16 * a + lr) * kEksKS + k0 + lk];
+#pragma unroll
+            for (int b = 0; b < 4; ++b) fb[b] = Hs[(wc + 16 * b + lr) * kEksKS + k0 + lk];
+#pragma unroll
+            for (int a = 0; a < 2; ++a)
+#pragma unroll
+                for (int b = 0; b < 4; ++b)
+                    acc[a][b] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[a], fb[b], acc[a][b], 0, 0, 0);
+        }
+    }
+    const bool diag = (ti == tj);
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int64_t gi = r0 + wr + 16 * a + lk + 4 * r;
+                const int64_t gj = c0 + wc + 16 * b + lr;
+                if (gi < n && gj < n && (!diag || gj <= gi)) {
+                    double* p = P + gi * ld + gj;
+                    *p = *p - acc[a][b][r];
+                }
+            }
+}
+
+// Full symmetric copy-out of rows [i0, i0 + gridDim.y): dst[i - i0][j] = P_sym[i][j].
+__global__ __launch_bounds__(256) void eks_symmetrize_kernel(const double* __restrict__ P,
+                                                             const int64_t n, const int64_t ld,
+                                                             const int64_t i0,
+                                                             double* __restrict__ dst) {
+    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t i = i0 + blockIdx.y;
+    if (j >= n || i >= n) return;
+    dst[(int64_t)blockIdx.y * n + j] = psym(P, ld, i, j);
+}
+
+__global__ __launch_bounds__(256) void eks_diag_kernel(double* __restrict__ P, const int64_t n,
+                                                       const int64_t ld,
+                                                       const double* __restrict__ dg) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) P[i * ld + i] = dg[i];
+}
+
+}  // namespace slam

@@ -36,6 +36,17 @@ class PFResult(C.Structure):
                 ("n_special", C.c_int32)]
 
 
+class EKFConfig(C.Structure):
+    _fields_ = [("dt", C.c_double), ("vel", C.c_double), ("omega", C.c_double),
+                ("q", C.c_double * 9), ("r", C.c_double * 4), ("x0", C.c_double * 3),
+                ("p0", C.c_double * 9)]
+
+
+class EKFSLAMConfig(C.Structure):
+    _fields_ = [("dt", C.c_double), ("q_robot", C.c_double * 9), ("r_dist", C.c_double),
+                ("r_dir", C.c_double), ("r_orient", C.c_double)]
+
+
 _P = C.c_void_p
 _D = C.POINTER(C.c_double)
 _I64 = C.POINTER(C.c_int64)
@@ -78,6 +89,24 @@ SIGNATURES = {
     "slam_pf_shard_predict_update": (C.c_int, [_P, _P]),
     "slam_pf_shard_normalize": (C.c_int, [_P, _P, C.c_int64, _P]),
     "slam_pf_shard_finish": (C.c_int, [_P, _P, C.c_int32, C.POINTER(PFResult)]),
+    "slam_ekf_create": (C.c_int, [C.POINTER(EKFConfig), C.c_int64, C.c_int, C.POINTER(_P)]),
+    "slam_ekf_destroy": (C.c_int, [_P]),
+    "slam_ekf_set_state": (C.c_int, [_P, _D, _D]),
+    "slam_ekf_get_state": (C.c_int, [_P, _D, _D]),
+    "slam_ekf_step": (C.c_int, [_P, _D, _D, _D, _D, _D]),
+    "slam_ekf_run": (C.c_int, [_P, C.c_int32, _D, _D, _D]),
+    "slam_ekf_run_device": (C.c_int, [_P, C.c_int32, _D, _P, _P]),
+    "slam_ekf_synchronize": (C.c_int, [_P]),
+    "slam_ekfslam_create": (C.c_int, [C.POINTER(EKFSLAMConfig), C.c_int64, C.c_int,
+                                      C.POINTER(_P)]),
+    "slam_ekfslam_destroy": (C.c_int, [_P]),
+    "slam_ekfslam_set_state": (C.c_int, [_P, _D, _D]),
+    "slam_ekfslam_init_diag": (C.c_int, [_P, _D, _D]),
+    "slam_ekfslam_get_state": (C.c_int, [_P, _D, _D]),
+    "slam_ekfslam_predict": (C.c_int, [_P, _D]),
+    "slam_ekfslam_update": (C.c_int, [_P, C.c_int32, _I64, _D]),
+    "slam_ekfslam_step": (C.c_int, [_P, _D, C.c_int32, _I64, _D]),
+    "slam_ekfslam_timing": (C.c_int, [_P, _D]),
 }
 
 _lib = None
