@@ -279,8 +279,96 @@ def gen_ekf(seed=3, steps=360):
                         **{k: np.array(v) for k, v in rows.items()})
 
 
+# -------------------------------------------------------------- graph SLAM
+def _pair_row(h1, h2):
+    o1, o2 = h1.getObs(), h2.getObs()
+    return [h1.getTime(), h1.getRobotPoseId(), o1.getLandMarkId(), o1.getDist(), o1.getDir(),
+            o1.getOrient(), h2.getTime(), h2.getRobotPoseId(), o2.getLandMarkId(), o2.getDist(),
+            o2.getDir(), o2.getOrient()]
+
+
+def gen_graph(seed=0, demo_frames=18, big_steps=300):
+    """graph_based_slam.py: the 18-frame demo (module-level robot, every
+    Gauss-Newton iteration) and a T=300 run paired once at the end.  The
+    reference's setPairObs / updateEstPose are wrapped to record their inputs
+    (half-edge pairs, pose estimates) and outputs (edge blocks, H, b, det,
+    cond, updated poses)."""
+    np.random.seed(seed)                         # the module draws at import
+    with _quiet():
+        import graph_based_slam as gs
+    TE = gs.TrajectoryEstimator
+    orig_pair, orig_upd = TE.setPairObs, TE.updateEstPose
+    log, cur = [], {"pairs": []}
+
+    def pair(self, h1, h2):
+        cur["pairs"].append(_pair_row(h1, h2))
+        return orig_pair(self, h1, h2)
+
+    def upd(self):
+        poses_b = np.array([p[:, 0] for p in self._TrajectoryEstimator__mPosesEst])
+        edges = [np.concatenate([e.mMatH_BfrBfr.ravel(), e.mMatH_BfrAft.ravel(),
+                                 e.mMatH_AftBfr.ravel(), e.mMatH_AftAft.ravel(),
+                                 e.mVecB_Bfr.ravel(), e.mVecB_Aft.ravel()])
+                 for e in self._TrajectoryEstimator__mEdge]
+        times = sorted(self._TrajectoryEstimator__KeepLandMarkTime)
+        r = orig_upd(self)
+        rec = dict(pairs=np.array(cur["pairs"], dtype=np.float64).reshape(-1, 12),
+                   poses_before=poses_b, edges=np.array(edges).reshape(-1, 42),
+                   times=np.array(times, dtype=np.int64),
+                   H=self._TrajectoryEstimator__mMatH.copy(),
+                   b=self._TrajectoryEstimator__mVecB[:, 0].copy(),
+                   stats=np.array([float(r[0]), r[1], r[2], r[3]]),
+                   poses_after=np.array([p[:, 0] for p in self._TrajectoryEstimator__mPosesEst]))
+        log.append(rec)
+        cur["pairs"] = []
+        return r
+
+    TE.setPairObs, TE.updateEstPose = pair, upd
+    try:
+        out = {"seed": np.array(seed)}
+        with _quiet():
+            for _ in range(demo_frames):
+                gs.gRbt.move(gs.VEL_mps, gs.OMEGA_rps)
+                gs.gRbt.estimateOpticalTrajectory()
+        demo = list(log)
+        out["demo_n"] = np.array(len(demo))
+        for i, r in enumerate(demo):
+            for k, v in r.items():
+                out[f"demo{i}_{k}"] = v
+        # T = 300: one robot, all moves first, then one trajectory estimate
+        log.clear()
+        x0 = np.array([[10.0], [0.0], [np.deg2rad(90.0)]])
+        with _quiet():
+            rbt = gs.Robot(x0, gs.PERIOD_ms / 1000, gs.SCN_SENS_RANGE_m, gs.SCN_SENS_ANGLE_rps,
+                           gs.LAND_MARKS)
+            for _ in range(big_steps):
+                rbt.move(gs.VEL_mps, gs.OMEGA_rps)
+            halves = [[h.getTime(), h.getRobotPoseId(), h.getObs().getLandMarkId(),
+                       h.getObs().getDist(), h.getObs().getDir(), h.getObs().getOrient()]
+                      for h in rbt._Robot__mHalfEdges]
+            rbt.estimateOpticalTrajectory()
+        out["big_halves"] = np.array(halves)
+        out["big_n"] = np.array(len(log))
+        for i, r in enumerate(log):
+            out[f"big{i}_poses_before"] = r["poses_before"]
+            out[f"big{i}_poses_after"] = r["poses_after"]
+            out[f"big{i}_times"] = r["times"]
+            out[f"big{i}_b"] = r["b"]
+            out[f"big{i}_stats"] = r["stats"]
+            out[f"big{i}_n_edges"] = np.array(len(r["edges"]))
+            out[f"big{i}_edges_head"] = r["edges"][:64]
+            out[f"big{i}_edges_colsum"] = r["edges"].sum(axis=0)
+            H = r["H"]
+            out[f"big{i}_H_diag3"] = np.array([H[j:j + 3, j:j + 3] for j in range(0, len(H), 3)])
+            out[f"big{i}_H_colsum"] = H.sum(axis=0)
+            out[f"big{i}_H_sample"] = H[::7, ::11]
+    finally:
+        TE.setPairObs, TE.updateEstPose = orig_pair, orig_upd
+    np.savez_compressed(os.path.join(OUT, "graph.npz"), **out)
+
+
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["units", "pf_c1", "pf_stages", "motion", "ekf"]
+    which = sys.argv[1:] or ["units", "pf_c1", "pf_stages", "motion", "ekf", "graph"]
     for w in which:
         print("generating", w, flush=True)
         globals()["gen_" + w]()

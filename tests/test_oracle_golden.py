@@ -142,3 +142,46 @@ def test_ekf_end_to_end():
     rows = eo.run_reference_order(int(g["seed"]), len(g["P"]))
     for key in ["x_true", "x_dr", "z", "x_hat_m", "P", "x_hat"]:
         _eq(np.array([r[key] for r in rows]), g[key])
+
+
+# ------------------------------------------------------------ graph SLAM
+def test_graph_demo_every_iteration_bit_exact():
+    import graph_oracle as go
+    g = golden("graph")
+    n = int(g["demo_n"])
+    assert n == 51
+    for i in range(n):
+        pairs = g[f"demo{i}_pairs"]
+        poses = g[f"demo{i}_poses_before"]
+        edges = go.edges_from_pairs(pairs)
+        blocks = go.linearize(edges, poses)
+        _eq(blocks, g[f"demo{i}_edges"])
+        times, H, b = go.assemble(edges, blocks)
+        _eq(np.array(times), g[f"demo{i}_times"])
+        _eq(H, g[f"demo{i}_H"])
+        _eq(b[:, 0], g[f"demo{i}_b"])
+        stats, after, _, _, _ = go.update_est_pose(edges, poses)
+        _eq(stats, g[f"demo{i}_stats"])
+        _eq(after, g[f"demo{i}_poses_after"])
+
+
+def test_graph_t300_pairing_and_gauss_newton_bit_exact():
+    import graph_oracle as go
+    g = golden("graph")
+    pairs = go.pairs_from_halves(g["big_halves"], 9)
+    edges = go.edges_from_pairs(pairs)
+    n = int(g["big_n"])
+    poses = g["big0_poses_before"]
+    for i in range(n):
+        assert len(edges) == int(g[f"big{i}_n_edges"])
+        _eq(poses, g[f"big{i}_poses_before"])
+        blocks = go.linearize(edges, poses)
+        _eq(blocks[:64], g[f"big{i}_edges_head"])
+        _eq(blocks.sum(axis=0), g[f"big{i}_edges_colsum"])
+        stats, poses, H, b, times = go.update_est_pose(edges, poses)
+        _eq(np.array(times), g[f"big{i}_times"])
+        _eq(b, g[f"big{i}_b"])
+        _eq(H.sum(axis=0), g[f"big{i}_H_colsum"])
+        _eq(H[::7, ::11], g[f"big{i}_H_sample"])
+        _eq(stats, g[f"big{i}_stats"])
+        _eq(poses, g[f"big{i}_poses_after"])
