@@ -235,6 +235,67 @@ int slam_ekfslam_step(slam_ekfslam* h, const double* control, int32_t k, const i
  * rank-3k covariance update, 0}. */
 int slam_ekfslam_timing(slam_ekfslam* h, double* out);
 
+/* ====================================================================
+ * Graph-based SLAM -- replaces TrajectoryEstimator's linearise-and-solve
+ * (graph_based_slam.py: setPairObs :362-439, updateEstPose :452-514) and
+ * the Gauss-Newton loop of Robot.estimateOpticalTrajectory (:685-715).
+ * ==================================================================== */
+typedef struct slam_graph slam_graph;
+
+/* One pair of half-edges of the same landmark (HalfEdge :259-300), already
+ * ordered as setPairObs orders them (:371-384: "bfr" is the earlier time).
+ * The estimate of pose_* is linearised; time_* selects the block of H
+ * (its rank among the edge set's times, :478-482) and the pose updated. */
+typedef struct {
+    int64_t time_bfr, pose_bfr, time_aft, pose_aft;
+    double obs_bfr[3];    /* Observation (:20-75): distance, direction, orientation */
+    double obs_aft[3];
+} slam_graph_edge;
+
+enum { SLAM_GRAPH_AUTO = 0,   /* dense up to 2048 unknowns, PCG above */
+       SLAM_GRAPH_DENSE = 1,  /* LU: det, cond and the reference's gate (:494-498) */
+       SLAM_GRAPH_PCG = 2 };  /* block-Jacobi PCG on the 3x3 block-sparse H (config 5) */
+
+typedef struct {
+    double r_dist;        /* ScanSensor range noise gain (setNoiseParam(5,2,2) :604 -> 0.05) */
+    double r_dir;         /* bearing sigma (rad) */
+    double r_orient;      /* orientation sigma (rad) */
+    double anchor;        /* :475  H[0:3,0:3] += anchor * I  (1e4) */
+    double det_min;       /* :496  0.1 < det */
+    double cond_max;      /* :496  cond < 1e15 */
+    double pcg_tol;       /* PCG: relative residual */
+    int32_t pcg_max_iter;
+    int32_t solver;       /* SLAM_GRAPH_* */
+} slam_graph_config;
+
+int slam_graph_create(const slam_graph_config* cfg, int device, slam_graph** out);
+int slam_graph_destroy(slam_graph* h);
+/* TrajectoryEstimator's pose list (mPosesEst): n_poses x 3. */
+int slam_graph_set_poses(slam_graph* h, int64_t n_poses, const double* poses);
+int slam_graph_get_poses(slam_graph* h, double* poses);
+/* The pairs setPairObs received (builds the block structure once). */
+int slam_graph_set_edges(slam_graph* h, int64_t n_edges, const slam_graph_edge* edges);
+/* updateEstPose: linearise every edge at the current poses, assemble H and
+ * b, gate, solve, update the poses.  stats[4] = {is_calc, sum delta^2, det,
+ * cond} (:514); det/cond are NaN on the PCG path. */
+int slam_graph_update(slam_graph* h, double* stats);
+/* estimateOpticalTrajectory's loop: update until sum delta^2 < delta_sum_th
+ * (:692-706) or max_iter; stats: max_iter x 4 (or NULL). */
+int slam_graph_optimize(slam_graph* h, double delta_sum_th, int32_t max_iter, double* stats,
+                        int32_t* n_iter);
+/* The last assembled system: times (n_times), H (3n_times squared, dense, or
+ * NULL), b (3 n_times or NULL), blocks (n_edges x 42: BB, BA, AB, AA, b_B, b_A
+ * or NULL).  n_times may be queried with everything else NULL. */
+int slam_graph_get_system(slam_graph* h, int64_t* n_times, int64_t* times, double* H, double* b,
+                          double* blocks);
+/* Device time of the last update (ms): out[5] = {linearise, assemble, solve,
+ * pose update, PCG iterations}. */
+int slam_graph_timing(slam_graph* h, double* out);
+/* One-shot form: poses in/out, stats[4] as slam_graph_update. */
+int slam_graph_linearize_solve(const slam_graph_config* cfg, const slam_graph_edge* edges,
+                               int64_t n_edges, double* poses, int64_t n_poses, double* stats,
+                               int device);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,491 @@
+// graph_api.hip -- C-ABI of graph-based SLAM (include/slam_hip.h).
+//
+// TrajectoryEstimator (graph_based_slam.py:330-581) -> slam_graph_*.  The
+// block structure of H and the per-block accumulation plan (which edge parts
+// land in which 3x3 block, in the reference's edge order) are built on the
+// host once per edge set; every Gauss-Newton iteration then runs entirely on
+// the device: linearise -> assemble -> solve -> pose update.
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <limits>
+#include <vector>
+
+#include "graph_kernels.inl"
+
+using namespace slam;
+
+struct slam_graph {
+    slam_graph_config cfg;
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::vector<void*> allocs;     // per edge-set / per pose-set buffers
+    // poses
+    int64_t T = 0;
+    double* poses = nullptr;
+    // edges and structure
+    int64_t E = 0, nt = 0, n_slots = 0;
+    std::vector<int64_t> times_h;
+    slam_graph_edge* edges = nullptr;
+    double* blocks = nullptr;      // [42][E]
+    int64_t *times = nullptr, *srow = nullptr, *scol = nullptr, *rptr = nullptr;
+    int64_t *cptr = nullptr, *clist = nullptr, *bptr = nullptr, *blist = nullptr;
+    int64_t* dslot = nullptr;
+    double *val = nullptr, *b = nullptr, *delta = nullptr, *dsum = nullptr;
+    // dense path
+    double *A = nullptr, *LU = nullptr, *S = nullptr, *V = nullptr, *lan = nullptr;
+    int32_t* piv = nullptr;
+    double* luout = nullptr;       // [0..2] LU, [3..4] Lanczos
+    // PCG
+    double *minv = nullptr, *r = nullptr, *z = nullptr, *p = nullptr, *q = nullptr;
+    double* part = nullptr;
+    PcgState* st = nullptr;
+    hipEvent_t ev[5] = {};
+    double last[5] = {0, 0, 0, 0, 0};
+};
+
+namespace {
+
+void free_list(std::vector<void*>& l) {
+    for (void* p : l) (void)hipFree(p);
+    l.clear();
+}
+
+template <typename T>
+int galloc(slam_graph* h, T** p, size_t count) {
+    void* q = nullptr;
+    SLAM_HIP_TRY(hipMalloc(&q, std::max<size_t>(count, 1) * sizeof(T)));
+    h->allocs.push_back(q);
+    *p = (T*)q;
+    return SLAM_OK;
+}
+
+#define GTRY(x)               \
+    do {                      \
+        int rc_ = (x);        \
+        if (rc_) return rc_;  \
+    } while (0)
+
+template <typename T>
+int upload(slam_graph* h, T* dst, const std::vector<T>& src) {
+    if (src.empty()) return SLAM_OK;
+    SLAM_HIP_TRY(hipMemcpyAsync(dst, src.data(), src.size() * sizeof(T), hipMemcpyHostToDevice,
+                                h->stream));
+    return SLAM_OK;
+}
+
+unsigned nblk(int64_t n, int t = 256) { return (unsigned)((n + t - 1) / t); }
+
+int build_structure(slam_graph* h, int64_t E, const slam_graph_edge* ed) {
+    std::vector<int64_t> tl;
+    tl.reserve(2 * E);
+    for (int64_t e = 0; e < E; ++e) {
+        tl.push_back(ed[e].time_bfr);
+        tl.push_back(ed[e].time_aft);
+    }
+    std::sort(tl.begin(), tl.end());
+    tl.erase(std::unique(tl.begin(), tl.end()), tl.end());
+    const int64_t nt = (int64_t)tl.size();
+    auto rank = [&](int64_t t) { return (int64_t)(std::lower_bound(tl.begin(), tl.end(), t) - tl.begin()); };
+    std::vector<int64_t> rb(E), ra(E);
+    std::vector<int64_t> keys;
+    keys.reserve(4 * E + nt);
+    for (int64_t i = 0; i < nt; ++i) keys.push_back(i * nt + i);
+    for (int64_t e = 0; e < E; ++e) {
+        rb[e] = rank(ed[e].time_bfr);
+        ra[e] = rank(ed[e].time_aft);
+        keys.push_back(rb[e] * nt + ra[e]);
+        keys.push_back(ra[e] * nt + rb[e]);
+    }
+    std::sort(keys.begin(), keys.end());
+    keys.erase(std::unique(keys.begin(), keys.end()), keys.end());
+    const int64_t ns = (int64_t)keys.size();
+    auto slot = [&](int64_t r, int64_t c) {
+        return (int64_t)(std::lower_bound(keys.begin(), keys.end(), r * nt + c) - keys.begin());
+    };
+    std::vector<int64_t> srow(ns), scol(ns), rptr(nt + 1, 0), dslot(nt);
+    for (int64_t s = 0; s < ns; ++s) {
+        srow[s] = keys[s] / nt;
+        scol[s] = keys[s] % nt;
+        rptr[srow[s] + 1]++;
+        if (srow[s] == scol[s]) dslot[srow[s]] = s;
+    }
+    for (int64_t i = 0; i < nt; ++i) rptr[i + 1] += rptr[i];
+    // accumulation plan, stable in edge order (updateEstPose :484-492)
+    std::vector<int64_t> cnt(ns + 1, 0), sl(4 * E);
+    for (int64_t e = 0; e < E; ++e) {
+        sl[4 * e + 0] = slot(rb[e], rb[e]);
+        sl[4 * e + 1] = slot(rb[e], ra[e]);
+        sl[4 * e + 2] = slot(ra[e], rb[e]);
+        sl[4 * e + 3] = slot(ra[e], ra[e]);
+        for (int k = 0; k < 4; ++k) cnt[sl[4 * e + k] + 1]++;
+    }
+    for (int64_t s = 0; s < ns; ++s) cnt[s + 1] += cnt[s];
+    std::vector<int64_t> cptr = cnt, clist(4 * E);
+    for (int64_t c = 0; c < 4 * E; ++c) clist[cnt[sl[c]]++] = c;     // c = 4 e + part
+    std::vector<int64_t> bc(nt + 1, 0), blist(2 * E);
+    for (int64_t e = 0; e < E; ++e) {
+        bc[rb[e] + 1]++;
+        bc[ra[e] + 1]++;
+    }
+    for (int64_t i = 0; i < nt; ++i) bc[i + 1] += bc[i];
+    std::vector<int64_t> bptr = bc;
+    for (int64_t e = 0; e < E; ++e) {
+        blist[bc[rb[e]]++] = 2 * e;
+        blist[bc[ra[e]]++] = 2 * e + 1;
+    }
+    // device buffers
+    free_list(h->allocs);
+    h->E = E;
+    h->nt = nt;
+    h->n_slots = ns;
+    h->times_h = tl;
+    const int64_t n = 3 * nt;
+    GTRY(galloc(h, &h->edges, E));
+    GTRY(galloc(h, &h->blocks, 42 * E));
+    GTRY(galloc(h, &h->times, nt));
+    GTRY(galloc(h, &h->srow, ns));
+    GTRY(galloc(h, &h->scol, ns));
+    GTRY(galloc(h, &h->rptr, nt + 1));
+    GTRY(galloc(h, &h->cptr, ns + 1));
+    GTRY(galloc(h, &h->clist, 4 * E));
+    GTRY(galloc(h, &h->bptr, nt + 1));
+    GTRY(galloc(h, &h->blist, 2 * E));
+    GTRY(galloc(h, &h->dslot, nt));
+    GTRY(galloc(h, &h->val, 9 * ns));
+    GTRY(galloc(h, &h->b, n));
+    GTRY(galloc(h, &h->delta, n));
+    GTRY(galloc(h, &h->dsum, 1));
+    GTRY(galloc(h, &h->minv, 9 * nt));
+    GTRY(galloc(h, &h->r, n));
+    GTRY(galloc(h, &h->z, n));
+    GTRY(galloc(h, &h->p, n));
+    GTRY(galloc(h, &h->q, n));
+    GTRY(galloc(h, &h->part, 2 * (int64_t)nblk(n) + 2));
+    GTRY(galloc(h, &h->st, 1));
+    GTRY(galloc(h, &h->luout, 8));
+    if (n <= kGraphDenseMax) {
+        GTRY(galloc(h, &h->A, n * n));
+        GTRY(galloc(h, &h->LU, n * n));
+        GTRY(galloc(h, &h->S, n * n));
+        GTRY(galloc(h, &h->V, n * (n + 1)));
+        GTRY(galloc(h, &h->lan, 3 * n + 8));
+        GTRY(galloc(h, &h->piv, n));
+    } else {
+        h->A = h->LU = h->S = h->V = h->lan = nullptr;
+        h->piv = nullptr;
+    }
+    SLAM_HIP_TRY(hipMemcpyAsync(h->edges, ed, E * sizeof(slam_graph_edge), hipMemcpyHostToDevice,
+                                h->stream));
+    GTRY(upload(h, h->times, tl));
+    GTRY(upload(h, h->srow, srow));
+    GTRY(upload(h, h->scol, scol));
+    GTRY(upload(h, h->rptr, rptr));
+    GTRY(upload(h, h->cptr, cptr));
+    GTRY(upload(h, h->clist, clist));
+    GTRY(upload(h, h->bptr, bptr));
+    GTRY(upload(h, h->blist, blist));
+    GTRY(upload(h, h->dslot, dslot));
+    SLAM_HIP_TRY(hipStreamSynchronize(h->stream));
+    return SLAM_OK;
+}
+
+GraphConst gconst(const slam_graph_config& c) { return GraphConst{c.r_dist, c.r_dir, c.r_orient}; }
+
+int linearize_assemble(slam_graph* h) {
+    SLAM_HIP_TRY(hipEventRecord(h->ev[0], h->stream));
+    hipLaunchKernelGGL(graph_linearize_kernel, dim3(nblk(h->E)), dim3(256), 0, h->stream, h->E,
+                       h->edges, h->poses, gconst(h->cfg), h->blocks);
+    SLAM_HIP_TRY(hipEventRecord(h->ev[1], h->stream));
+    hipLaunchKernelGGL(graph_assemble_h_kernel, dim3(nblk(9 * h->n_slots)), dim3(256), 0,
+                       h->stream, h->n_slots, h->E, h->cptr, h->clist, h->blocks, h->cfg.anchor,
+                       h->val);
+    hipLaunchKernelGGL(graph_assemble_b_kernel, dim3(nblk(3 * h->nt)), dim3(256), 0, h->stream,
+                       h->nt, h->E, h->bptr, h->blist, h->blocks, h->b);
+    SLAM_HIP_TRY(hipEventRecord(h->ev[2], h->stream));
+    SLAM_HIP_TRY(hipGetLastError());
+    return SLAM_OK;
+}
+
+int dense_matrix(slam_graph* h) {
+    const int64_t n = 3 * h->nt;
+    SLAM_HIP_TRY(hipMemsetAsync(h->A, 0, n * n * sizeof(double), h->stream));
+    hipLaunchKernelGGL(graph_dense_scatter_kernel, dim3(nblk(9 * h->n_slots)), dim3(256), 0,
+                       h->stream, h->n_slots, h->srow, h->scol, h->val, n, h->A);
+    SLAM_HIP_TRY(hipGetLastError());
+    return SLAM_OK;
+}
+
+// dense path: det, cond, gate, delta (updateEstPose :494-502)
+int solve_dense(slam_graph* h, double* stats, bool* solved) {
+    const int64_t n = 3 * h->nt;
+    GTRY(dense_matrix(h));
+    SLAM_HIP_TRY(hipMemcpyAsync(h->LU, h->A, n * n * sizeof(double), hipMemcpyDeviceToDevice,
+                                h->stream));
+    hipLaunchKernelGGL(graph_symmetrize_kernel, dim3(nblk(n * n)), dim3(256), 0, h->stream, h->A, n,
+                       h->S);
+    hipLaunchKernelGGL(graph_lu_kernel, dim3(1), dim3(kGraphThreads), 0, h->stream, h->LU, (int)n,
+                       h->piv, h->luout);
+    hipLaunchKernelGGL(graph_lanczos_kernel, dim3(1), dim3(kGraphThreads), 0, h->stream, h->S,
+                       (int)n, h->V, h->lan, h->lan + n, h->lan + 2 * n, h->luout + 3,
+                       (uint64_t)0x5EEDULL);
+    SLAM_HIP_TRY(hipGetLastError());
+    double lo[5];
+    SLAM_HIP_TRY(hipMemcpyAsync(lo, h->luout, 5 * sizeof(double), hipMemcpyDeviceToHost, h->stream));
+    SLAM_HIP_TRY(hipStreamSynchronize(h->stream));
+    // numpy det: sign * exp(logdet); a zero pivot gives 0 (getrf info > 0)
+    const double det = (lo[2] != 0.0) ? 0.0 : lo[0] * std::exp(lo[1]);
+    const double cond = (lo[4] > 0.0) ? lo[3] / lo[4] : std::numeric_limits<double>::infinity();
+    stats[2] = det;
+    stats[3] = cond;
+    *solved = (h->cfg.det_min < det) && (cond < h->cfg.cond_max);
+    if (*solved)
+        hipLaunchKernelGGL(graph_lu_solve_kernel, dim3(1), dim3(kGraphThreads), 0, h->stream,
+                           h->LU, (int)n, h->piv, h->b, h->delta);
+    SLAM_HIP_TRY(hipGetLastError());
+    return SLAM_OK;
+}
+
+__global__ void graph_negate_kernel(const int64_t n, const double* __restrict__ b,
+                                    double* __restrict__ r) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) r[i] = -b[i];
+}
+
+// PCG on H delta = -b with block-Jacobi (large trajectories)
+int solve_pcg(slam_graph* h, double* stats, bool* solved, int32_t* iters) {
+    const int64_t n = 3 * h->nt;
+    const unsigned nb = nblk(n);
+    hipLaunchKernelGGL(graph_block_inv_kernel, dim3(nblk(h->nt)), dim3(256), 0, h->stream, h->nt,
+                       h->dslot, h->val, h->minv);
+    SLAM_HIP_TRY(hipMemsetAsync(h->delta, 0, n * sizeof(double), h->stream));
+    hipLaunchKernelGGL(graph_negate_kernel, dim3(nb), dim3(256), 0, h->stream, n, h->b, h->r);
+    hipLaunchKernelGGL(graph_pcg_precond_kernel, dim3(nb), dim3(256), 0, h->stream, n, h->minv,
+                       h->r, h->z, h->part, h->st, 1);
+    hipLaunchKernelGGL(graph_pcg_scalar_kernel, dim3(1), dim3(1024), 0, h->stream, (int64_t)nb,
+                       h->part, h->st, 2, h->cfg.pcg_tol, h->cfg.pcg_max_iter);
+    hipLaunchKernelGGL(graph_pcg_dir_kernel, dim3(nb), dim3(256), 0, h->stream, n, h->p, h->z,
+                       h->st, 1);
+    SLAM_HIP_TRY(hipGetLastError());
+    PcgState s{};
+    const int chunk = 16;
+    for (int it = 0; it < h->cfg.pcg_max_iter; it += chunk) {
+        for (int k = 0; k < chunk; ++k) {
+            hipLaunchKernelGGL(graph_pcg_spmv_kernel, dim3(nb), dim3(256), 0, h->stream, n, h->rptr,
+                               h->scol, h->val, h->p, h->q, h->part, h->st);
+            hipLaunchKernelGGL(graph_pcg_scalar_kernel, dim3(1), dim3(1024), 0, h->stream,
+                               (int64_t)nb, h->part, h->st, 0, h->cfg.pcg_tol,
+                               h->cfg.pcg_max_iter);
+            hipLaunchKernelGGL(graph_pcg_axpy_kernel, dim3(nb), dim3(256), 0, h->stream, n,
+                               h->delta, h->r, h->p, h->q, h->st);
+            hipLaunchKernelGGL(graph_pcg_precond_kernel, dim3(nb), dim3(256), 0, h->stream, n,
+                               h->minv, h->r, h->z, h->part, h->st, 0);
+            hipLaunchKernelGGL(graph_pcg_scalar_kernel, dim3(1), dim3(1024), 0, h->stream,
+                               (int64_t)nb, h->part, h->st, 1, h->cfg.pcg_tol,
+                               h->cfg.pcg_max_iter);
+            hipLaunchKernelGGL(graph_pcg_dir_kernel, dim3(nb), dim3(256), 0, h->stream, n, h->p,
+                               h->z, h->st, 0);
+        }
+        SLAM_HIP_TRY(hipGetLastError());
+        SLAM_HIP_TRY(hipMemcpyAsync(&s, h->st, sizeof(PcgState), hipMemcpyDeviceToHost, h->stream));
+        SLAM_HIP_TRY(hipStreamSynchronize(h->stream));
+        if (s.done) break;
+    }
+    *iters = s.iter;
+    stats[2] = std::numeric_limits<double>::quiet_NaN();
+    stats[3] = std::numeric_limits<double>::quiet_NaN();
+    *solved = (s.status == 1);
+    return SLAM_OK;
+}
+
+int do_update(slam_graph* h, double* stats) {
+    stats[0] = stats[1] = stats[2] = stats[3] = 0.0;
+    for (double& x : h->last) x = 0.0;
+    if (h->E == 0 || 3 * h->nt <= 3) return SLAM_OK;        // :469 (leng > 3)
+    GTRY(linearize_assemble(h));
+    const int64_t n = 3 * h->nt;
+    const bool dense = (h->cfg.solver == SLAM_GRAPH_DENSE) ||
+                       (h->cfg.solver == SLAM_GRAPH_AUTO && n <= kGraphDenseMax);
+    if (dense && n > kGraphDenseMax)
+        return fail(SLAM_ERR_ARG, "slam_graph_update: dense solver limited to 2048 unknowns");
+    bool solved = false;
+    int32_t iters = 0;
+    if (dense) GTRY(solve_dense(h, stats, &solved));
+    else GTRY(solve_pcg(h, stats, &solved, &iters));
+    SLAM_HIP_TRY(hipEventRecord(h->ev[3], h->stream));
+    if (solved) {
+        hipLaunchKernelGGL(graph_pose_update_kernel, dim3(1), dim3(1024), 0, h->stream, h->nt,
+                           h->times, h->delta, h->poses, h->dsum);
+        SLAM_HIP_TRY(hipGetLastError());
+        SLAM_HIP_TRY(hipMemcpyAsync(&stats[1], h->dsum, sizeof(double), hipMemcpyDeviceToHost,
+                                    h->stream));
+        stats[0] = 1.0;
+    }
+    SLAM_HIP_TRY(hipEventRecord(h->ev[4], h->stream));
+    SLAM_HIP_TRY(hipStreamSynchronize(h->stream));
+    float ms;
+    for (int k = 0; k < 4; ++k) {
+        SLAM_HIP_TRY(hipEventElapsedTime(&ms, h->ev[k], h->ev[k + 1]));
+        h->last[k] = ms;
+    }
+    h->last[4] = iters;
+    return SLAM_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int slam_graph_create(const slam_graph_config* cfg, int device, slam_graph** out) {
+    SLAM_ARG_CHECK(cfg && out, "slam_graph_create: NULL argument");
+    *out = nullptr;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev)
+        return fail(SLAM_ERR_ARG, "slam_graph_create: no such HIP device");
+    SLAM_HIP_TRY(hipSetDevice(device));
+    slam_graph* h = new slam_graph();
+    h->cfg = *cfg;
+    if (h->cfg.pcg_max_iter <= 0) h->cfg.pcg_max_iter = 10000;
+    if (!(h->cfg.pcg_tol > 0.0)) h->cfg.pcg_tol = 1e-10;
+    h->device = device;
+    if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete h;
+        return fail(SLAM_ERR_HIP, "slam_graph_create: stream creation failed");
+    }
+    for (auto& e : h->ev)
+        if (hipEventCreate(&e) != hipSuccess) {
+            slam_graph_destroy(h);
+            return fail(SLAM_ERR_HIP, "slam_graph_create: event creation failed");
+        }
+    *out = h;
+    return SLAM_OK;
+}
+
+int slam_graph_destroy(slam_graph* h) {
+    if (!h) return SLAM_OK;
+    (void)hipSetDevice(h->device);
+    free_list(h->allocs);
+    if (h->poses) (void)hipFree(h->poses);
+    for (auto& e : h->ev)
+        if (e) (void)hipEventDestroy(e);
+    if (h->stream) (void)hipStreamDestroy(h->stream);
+    delete h;
+    return SLAM_OK;
+}
+
+int slam_graph_set_poses(slam_graph* h, int64_t n_poses, const double* poses) {
+    SLAM_ARG_CHECK(h && poses && n_poses >= 1, "slam_graph_set_poses: bad arguments");
+    SLAM_HIP_TRY(hipSetDevice(h->device));
+    if (n_poses != h->T) {
+        if (h->poses) SLAM_HIP_TRY(hipFree(h->poses));
+        h->poses = nullptr;
+        SLAM_HIP_TRY(hipMalloc(&h->poses, 3 * n_poses * sizeof(double)));
+        h->T = n_poses;
+    }
+    SLAM_HIP_TRY(hipMemcpyAsync(h->poses, poses, 3 * n_poses * sizeof(double),
+                                hipMemcpyHostToDevice, h->stream));
+    SLAM_HIP_TRY(hipStreamSynchronize(h->stream));
+    return SLAM_OK;
+}
+
+int slam_graph_get_poses(slam_graph* h, double* poses) {
+    SLAM_ARG_CHECK(h && poses && h->poses, "slam_graph_get_poses: no poses");
+    SLAM_HIP_TRY(hipSetDevice(h->device));
+    SLAM_HIP_TRY(hipMemcpyAsync(poses, h->poses, 3 * h->T * sizeof(double), hipMemcpyDeviceToHost,
+                                h->stream));
+    SLAM_HIP_TRY(hipStreamSynchronize(h->stream));
+    return SLAM_OK;
+}
+
+int slam_graph_set_edges(slam_graph* h, int64_t n_edges, const slam_graph_edge* edges) {
+    SLAM_ARG_CHECK(h && n_edges >= 0 && (edges || n_edges == 0), "slam_graph_set_edges: bad arguments");
+    SLAM_ARG_CHECK(h->poses, "slam_graph_set_edges: set the poses first");
+    for (int64_t e = 0; e < n_edges; ++e) {
+        const slam_graph_edge& d = edges[e];
+        SLAM_ARG_CHECK(d.pose_bfr >= 0 && d.pose_bfr < h->T && d.pose_aft >= 0 && d.pose_aft < h->T &&
+                           d.time_bfr >= 0 && d.time_bfr < h->T && d.time_aft >= 0 &&
+                           d.time_aft < h->T,
+                       "slam_graph_set_edges: pose / time index out of range");
+    }
+    SLAM_HIP_TRY(hipSetDevice(h->device));
+    if (n_edges == 0) {
+        free_list(h->allocs);
+        h->E = h->nt = h->n_slots = 0;
+        h->times_h.clear();
+        return SLAM_OK;
+    }
+    return build_structure(h, n_edges, edges);
+}
+
+int slam_graph_update(slam_graph* h, double* stats) {
+    SLAM_ARG_CHECK(h && stats && h->poses, "slam_graph_update: bad arguments");
+    SLAM_HIP_TRY(hipSetDevice(h->device));
+    return do_update(h, stats);
+}
+
+int slam_graph_optimize(slam_graph* h, double delta_sum_th, int32_t max_iter, double* stats,
+                        int32_t* n_iter) {
+    SLAM_ARG_CHECK(h && h->poses && max_iter >= 1, "slam_graph_optimize: bad arguments");
+    SLAM_HIP_TRY(hipSetDevice(h->device));
+    int32_t it = 0;
+    double s[4] = {0, 0, 0, 0};
+    double dsum = delta_sum_th;
+    while (delta_sum_th <= dsum && it < max_iter) {            // :692
+        GTRY(do_update(h, s));
+        if (stats) std::memcpy(stats + 4 * it, s, sizeof(s));
+        dsum = s[1];
+        ++it;
+    }
+    if (n_iter) *n_iter = it;
+    return SLAM_OK;
+}
+
+int slam_graph_get_system(slam_graph* h, int64_t* n_times, int64_t* times, double* H, double* b,
+                          double* blocks) {
+    SLAM_ARG_CHECK(h && n_times, "slam_graph_get_system: bad arguments");
+    SLAM_HIP_TRY(hipSetDevice(h->device));
+    *n_times = h->nt;
+    if (times) std::memcpy(times, h->times_h.data(), h->nt * sizeof(int64_t));
+    const int64_t n = 3 * h->nt;
+    if (H) {
+        SLAM_ARG_CHECK(h->A, "slam_graph_get_system: dense H only up to 2048 unknowns");
+        GTRY(dense_matrix(h));
+        SLAM_HIP_TRY(hipMemcpyAsync(H, h->A, n * n * sizeof(double), hipMemcpyDeviceToHost,
+                                    h->stream));
+    }
+    if (b)
+        SLAM_HIP_TRY(hipMemcpyAsync(b, h->b, n * sizeof(double), hipMemcpyDeviceToHost, h->stream));
+    if (blocks && h->E) {
+        std::vector<double> t(42 * h->E);
+        SLAM_HIP_TRY(hipMemcpyAsync(t.data(), h->blocks, t.size() * sizeof(double),
+                                    hipMemcpyDeviceToHost, h->stream));
+        SLAM_HIP_TRY(hipStreamSynchronize(h->stream));
+        for (int64_t e = 0; e < h->E; ++e)
+            for (int q = 0; q < 42; ++q) blocks[42 * e + q] = t[q * h->E + e];
+    }
+    SLAM_HIP_TRY(hipStreamSynchronize(h->stream));
+    return SLAM_OK;
+}
+
+int slam_graph_timing(slam_graph* h, double* out) {
+    SLAM_ARG_CHECK(h && out, "slam_graph_timing: NULL argument");
+    for (int k = 0; k < 5; ++k) out[k] = h->last[k];
+    return SLAM_OK;
+}
+
+int slam_graph_linearize_solve(const slam_graph_config* cfg, const slam_graph_edge* edges,
+                               int64_t n_edges, double* poses, int64_t n_poses, double* stats,
+                               int device) {
+    SLAM_ARG_CHECK(poses && stats, "slam_graph_linearize_solve: NULL argument");
+    slam_graph* h = nullptr;
+    int rc = slam_graph_create(cfg, device, &h);
+    if (rc) return rc;
+    rc = slam_graph_set_poses(h, n_poses, poses);
+    if (!rc) rc = slam_graph_set_edges(h, n_edges, edges);
+    if (!rc) rc = slam_graph_update(h, stats);
+    if (!rc) rc = slam_graph_get_poses(h, poses);
+    slam_graph_destroy(h);
+    return rc;
+}
+
+}  // extern "C"

@@ -47,6 +47,19 @@ class EKFSLAMConfig(C.Structure):
                 ("r_dir", C.c_double), ("r_orient", C.c_double)]
 
 
+class GraphEdge(C.Structure):
+    _fields_ = [("time_bfr", C.c_int64), ("pose_bfr", C.c_int64), ("time_aft", C.c_int64),
+                ("pose_aft", C.c_int64), ("obs_bfr", C.c_double * 3), ("obs_aft", C.c_double * 3)]
+
+
+class GraphConfig(C.Structure):
+    _fields_ = [("r_dist", C.c_double), ("r_dir", C.c_double), ("r_orient", C.c_double),
+                ("anchor", C.c_double), ("det_min", C.c_double), ("cond_max", C.c_double),
+                ("pcg_tol", C.c_double), ("pcg_max_iter", C.c_int32), ("solver", C.c_int32)]
+
+
+GRAPH_SOLVER = {"auto": 0, "dense": 1, "pcg": 2}
+
 _P = C.c_void_p
 _D = C.POINTER(C.c_double)
 _I64 = C.POINTER(C.c_int64)
@@ -107,6 +120,17 @@ SIGNATURES = {
     "slam_ekfslam_update": (C.c_int, [_P, C.c_int32, _I64, _D]),
     "slam_ekfslam_step": (C.c_int, [_P, _D, C.c_int32, _I64, _D]),
     "slam_ekfslam_timing": (C.c_int, [_P, _D]),
+    "slam_graph_create": (C.c_int, [C.POINTER(GraphConfig), C.c_int, C.POINTER(_P)]),
+    "slam_graph_destroy": (C.c_int, [_P]),
+    "slam_graph_set_poses": (C.c_int, [_P, C.c_int64, _D]),
+    "slam_graph_get_poses": (C.c_int, [_P, _D]),
+    "slam_graph_set_edges": (C.c_int, [_P, C.c_int64, _P]),
+    "slam_graph_update": (C.c_int, [_P, _D]),
+    "slam_graph_optimize": (C.c_int, [_P, C.c_double, C.c_int32, _D, _I32]),
+    "slam_graph_get_system": (C.c_int, [_P, _I64, _I64, _D, _D, _D]),
+    "slam_graph_timing": (C.c_int, [_P, _D]),
+    "slam_graph_linearize_solve": (C.c_int, [C.POINTER(GraphConfig), _P, C.c_int64, _D, C.c_int64,
+                                             _D, C.c_int]),
 }
 
 _lib = None

@@ -1,0 +1,165 @@
+"""Device graph-based SLAM: a handle on libslam_hip's slam_graph_* entry
+points (TrajectoryEstimator's linearise-and-solve, graph_based_slam.py
+:362-514, and the Gauss-Newton loop :685-715)."""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import _lib
+from ._lib import GRAPH_SOLVER, GraphConfig, check, dptr
+
+# slam_graph_edge, 80 bytes
+EDGE_DTYPE = np.dtype([("time_bfr", "<i8"), ("pose_bfr", "<i8"), ("time_aft", "<i8"),
+                       ("pose_aft", "<i8"), ("obs_bfr", "<f8", (3,)), ("obs_aft", "<f8", (3,))])
+
+
+def edge_array(rows):
+    """Edge rows [t_bfr, pose_bfr, d, dir, orient, t_aft, pose_aft, d, dir, orient, (lm)]
+    -> slam_graph_edge records."""
+    rows = np.asarray(rows, dtype=np.float64).reshape(len(rows), -1)
+    out = np.zeros(len(rows), dtype=EDGE_DTYPE)
+    out["time_bfr"] = rows[:, 0].astype(np.int64)
+    out["pose_bfr"] = rows[:, 1].astype(np.int64)
+    out["obs_bfr"] = rows[:, 2:5]
+    out["time_aft"] = rows[:, 5].astype(np.int64)
+    out["pose_aft"] = rows[:, 6].astype(np.int64)
+    out["obs_aft"] = rows[:, 7:10]
+    return out
+
+
+class DeviceGraph:
+    """Pose graph on one GPU.  Noise defaults = Robot's setNoiseParam(5, 2, 2)
+    (graph_based_slam.py:604); anchor and gate = updateEstPose :475, :496."""
+
+    def __init__(self, *, r_dist=0.05, r_dir=np.deg2rad(2.0), r_orient=np.deg2rad(2.0),
+                 anchor=1e4, det_min=0.1, cond_max=1e15, solver="auto", pcg_tol=1e-10,
+                 pcg_max_iter=20000, device=0):
+        cfg = GraphConfig()
+        cfg.r_dist, cfg.r_dir, cfg.r_orient = float(r_dist), float(r_dir), float(r_orient)
+        cfg.anchor, cfg.det_min, cfg.cond_max = float(anchor), float(det_min), float(cond_max)
+        cfg.pcg_tol, cfg.pcg_max_iter = float(pcg_tol), int(pcg_max_iter)
+        cfg.solver = GRAPH_SOLVER[solver]
+        self.cfg = cfg
+        self._lib = _lib.load()
+        h = C.c_void_p()
+        check(self._lib.slam_graph_create(C.byref(cfg), int(device), C.byref(h)), "slam_graph_create")
+        self._h = h
+        self.n_poses = 0
+        self.n_edges = 0
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._lib.slam_graph_destroy(self._h)
+            self._h = None
+
+    __del__ = close
+
+    def set_poses(self, poses):
+        poses = np.ascontiguousarray(poses, dtype=np.float64).reshape(-1, 3)
+        check(self._lib.slam_graph_set_poses(self._h, len(poses), dptr(poses)), "slam_graph_set_poses")
+        self.n_poses = len(poses)
+
+    def get_poses(self):
+        out = np.empty((self.n_poses, 3))
+        check(self._lib.slam_graph_get_poses(self._h, dptr(out)), "slam_graph_get_poses")
+        return out
+
+    def set_edges(self, edges):
+        rec = edges if (isinstance(edges, np.ndarray) and edges.dtype == EDGE_DTYPE) else edge_array(edges)
+        rec = np.ascontiguousarray(rec)
+        check(self._lib.slam_graph_set_edges(self._h, len(rec), rec.ctypes.data_as(C.c_void_p)),
+              "slam_graph_set_edges")
+        self.n_edges = len(rec)
+
+    def update(self):
+        """updateEstPose: returns (is_calc, delta_sum, det, cond)."""
+        st = np.zeros(4)
+        check(self._lib.slam_graph_update(self._h, dptr(st)), "slam_graph_update")
+        return bool(st[0]), float(st[1]), float(st[2]), float(st[3])
+
+    def optimize(self, delta_sum_th=0.01, max_iter=100):
+        st = np.zeros((max_iter, 4))
+        n = C.c_int32(0)
+        check(self._lib.slam_graph_optimize(self._h, float(delta_sum_th), int(max_iter), dptr(st),
+                                            C.byref(n)), "slam_graph_optimize")
+        return st[:n.value]
+
+    def get_system(self, dense=True, blocks=False):
+        nt = C.c_int64(0)
+        check(self._lib.slam_graph_get_system(self._h, C.byref(nt), None, None, None, None),
+              "slam_graph_get_system")
+        n = 3 * nt.value
+        times = np.empty(nt.value, dtype=np.int64)
+        H = np.empty((n, n)) if dense else None
+        b = np.empty(n)
+        blk = np.empty((self.n_edges, 42)) if blocks else None
+        check(self._lib.slam_graph_get_system(self._h, C.byref(nt),
+                                              times.ctypes.data_as(C.POINTER(C.c_int64)),
+                                              dptr(H), dptr(b), dptr(blk)), "slam_graph_get_system")
+        return times, H, b, blk
+
+    def timing(self):
+        out = np.zeros(5)
+        check(self._lib.slam_graph_timing(self._h, dptr(out)), "slam_graph_timing")
+        return dict(linearize_ms=out[0], assemble_ms=out[1], solve_ms=out[2], update_ms=out[3],
+                    pcg_iterations=int(out[4]))
+
+
+def circle_graph(n_poses, n_landmarks=64, loops_per_pose=3, seed=0, odom_noise=0.02):
+    """Synthetic pose graph of the graph_based_slam.py form (BASELINE config 5):
+    a robot circling at 10 m radius with a ScanSensor (15 m, +-80 deg,
+    :899-902) among ``n_landmarks`` landmarks on a 14 m ring; one edge per
+    consecutive pose pair sharing a landmark and ``loops_per_pose`` loop edges
+    per pose between observations of the same landmark at other times.
+    Returns (initial pose estimates (T,3), true poses (T,3), edge records)."""
+    rs = np.random.RandomState(seed)
+    step = np.deg2rad(10.0)
+    ang = np.arange(n_poses) * step
+    truth = np.column_stack([10 * np.cos(ang), 10 * np.sin(ang),
+                             np.mod(ang + np.pi / 2 + np.pi, 2 * np.pi) - np.pi])
+    la = np.linspace(0, 2 * np.pi, n_landmarks, endpoint=False)
+    lm = np.column_stack([14 * np.cos(la), 14 * np.sin(la)])
+    # visibility and noisy (distance, direction, orientation) per pose
+    d = lm[None, :, :] - truth[:, None, :2]
+    psi = np.pi / 2 - truth[:, 2]
+    rx = np.cos(psi)[:, None] * d[..., 0] - np.sin(psi)[:, None] * d[..., 1]
+    ry = np.sin(psi)[:, None] * d[..., 0] + np.cos(psi)[:, None] * d[..., 1]
+    dist = np.hypot(rx, ry)
+    vis = (dist <= 15.0) & (ry >= np.abs(rx) * np.tan(np.pi / 2 - np.deg2rad(80.0)))
+    bearing = np.arctan2(ry, rx)
+    orient = np.repeat((np.pi / 2 - truth[:, 2])[:, None], n_landmarks, 1)   # ScanSensor :153
+    obs = np.stack([dist * (1 + 0.05 * rs.standard_normal(dist.shape)),
+                    bearing + np.deg2rad(2.0) * rs.standard_normal(dist.shape),
+                    orient + np.deg2rad(2.0) * rs.standard_normal(dist.shape)], -1)
+    obs[..., 1:] = np.mod(obs[..., 1:] + np.pi, 2 * np.pi) - np.pi
+    seen_by = [np.flatnonzero(vis[:, j]) for j in range(n_landmarks)]
+    rows = []
+
+    def add(t1, t2, j):
+        a, b = (t1, t2) if t1 < t2 else (t2, t1)
+        rows.append((a, a, *obs[a, j], b, b, *obs[b, j]))
+
+    for t in range(1, n_poses):
+        common = np.flatnonzero(vis[t - 1] & vis[t])
+        if len(common):
+            add(t - 1, t, int(common[rs.randint(len(common))]))
+        vis_t = np.flatnonzero(vis[t])
+        for _ in range(loops_per_pose if len(vis_t) else 0):
+            j = int(vis_t[rs.randint(len(vis_t))])
+            others = seen_by[j]
+            o = int(others[rs.randint(len(others))])
+            if o != t:
+                add(o, t, j)
+    rec = np.zeros(len(rows), dtype=EDGE_DTYPE)
+    r = np.array(rows, dtype=np.float64)
+    rec["time_bfr"] = r[:, 0].astype(np.int64)
+    rec["pose_bfr"] = r[:, 1].astype(np.int64)
+    rec["obs_bfr"] = r[:, 2:5]
+    rec["time_aft"] = r[:, 5].astype(np.int64)
+    rec["pose_aft"] = r[:, 6].astype(np.int64)
+    rec["obs_aft"] = r[:, 7:10]
+    init = truth + np.cumsum(odom_noise * rs.standard_normal(truth.shape), axis=0)
+    init[:, 2] = np.mod(init[:, 2] + np.pi, 2 * np.pi) - np.pi
+    return init, truth, rec
