@@ -193,6 +193,11 @@ int slam_ekf_run(slam_ekf* h, int32_t n_steps, const double* control, const doub
  * (x_hat_dev may be NULL); asynchronous on the handle's stream. */
 int slam_ekf_run_device(slam_ekf* h, int32_t n_steps, const double* control, const double* z_dev,
                         double* x_hat_dev);
+/* Bench path without foreign device buffers: upload n_steps x batch x 2
+ * observations once, then run them from HBM (asynchronous; the estimates of
+ * every step are kept on the device when keep_history != 0). */
+int slam_ekf_load_observations(slam_ekf* h, int32_t n_steps, const double* z_all);
+int slam_ekf_run_loaded(slam_ekf* h, int32_t n_steps, const double* control, int32_t keep_history);
 int slam_ekf_synchronize(slam_ekf* h);
 
 /* ====================================================================
@@ -288,6 +293,11 @@ int slam_graph_optimize(slam_graph* h, double delta_sum_th, int32_t max_iter, do
  * or NULL).  n_times may be queried with everything else NULL. */
 int slam_graph_get_system(slam_graph* h, int64_t* n_times, int64_t* times, double* H, double* b,
                           double* blocks);
+/* The block-sparse H of the last update (block rows/columns are time ranks,
+ * vals: n_slots x 9 row-major 3x3) and its solution delta (3 n_times);
+ * n_slots may be queried with the arrays NULL. */
+int slam_graph_get_bsr(slam_graph* h, int64_t* n_slots, int64_t* rows, int64_t* cols, double* vals);
+int slam_graph_get_delta(slam_graph* h, double* delta);
 /* Device time of the last update (ms): out[5] = {linearise, assemble, solve,
  * pose update, PCG iterations}. */
 int slam_graph_timing(slam_graph* h, double* out);

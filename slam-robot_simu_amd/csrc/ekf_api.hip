@@ -289,6 +289,24 @@ int slam_ekf_run_device(slam_ekf* h, int32_t n_steps, const double* control, con
     return SLAM_OK;
 }
 
+int slam_ekf_load_observations(slam_ekf* h, int32_t n_steps, const double* z_all) {
+    SLAM_ARG_CHECK(h && z_all && n_steps >= 1, "slam_ekf_load_observations: bad arguments");
+    SLAM_HIP_TRY(hipSetDevice(h->device));
+    int rc = ekf_reserve(h, n_steps);
+    if (rc) return rc;
+    SLAM_HIP_TRY(hipMemcpyAsync(h->z, z_all, (size_t)n_steps * h->batch * 2 * sizeof(double),
+                                hipMemcpyHostToDevice, h->stream));
+    SLAM_HIP_TRY(hipStreamSynchronize(h->stream));
+    return SLAM_OK;
+}
+
+int slam_ekf_run_loaded(slam_ekf* h, int32_t n_steps, const double* control, int32_t keep_history) {
+    SLAM_ARG_CHECK(h && n_steps >= 1 && n_steps <= h->cap_steps,
+                   "slam_ekf_run_loaded: load at least n_steps observations first");
+    SLAM_HIP_TRY(hipSetDevice(h->device));
+    return ekf_launch(h, n_steps, control, h->xm, keep_history ? h->xh : nullptr);
+}
+
 int slam_ekf_synchronize(slam_ekf* h) {
     SLAM_ARG_CHECK(h, "slam_ekf_synchronize: NULL handle");
     SLAM_HIP_TRY(hipStreamSynchronize(h->stream));

@@ -467,6 +467,34 @@ int slam_graph_get_system(slam_graph* h, int64_t* n_times, int64_t* times, doubl
     return SLAM_OK;
 }
 
+int slam_graph_get_bsr(slam_graph* h, int64_t* n_slots, int64_t* rows, int64_t* cols,
+                       double* vals) {
+    SLAM_ARG_CHECK(h && n_slots, "slam_graph_get_bsr: bad arguments");
+    SLAM_HIP_TRY(hipSetDevice(h->device));
+    *n_slots = h->n_slots;
+    if (rows)
+        SLAM_HIP_TRY(hipMemcpyAsync(rows, h->srow, h->n_slots * sizeof(int64_t),
+                                    hipMemcpyDeviceToHost, h->stream));
+    if (cols)
+        SLAM_HIP_TRY(hipMemcpyAsync(cols, h->scol, h->n_slots * sizeof(int64_t),
+                                    hipMemcpyDeviceToHost, h->stream));
+    if (vals)
+        SLAM_HIP_TRY(hipMemcpyAsync(vals, h->val, 9 * h->n_slots * sizeof(double),
+                                    hipMemcpyDeviceToHost, h->stream));
+    SLAM_HIP_TRY(hipStreamSynchronize(h->stream));
+    return SLAM_OK;
+}
+
+int slam_graph_get_delta(slam_graph* h, double* delta) {
+    SLAM_ARG_CHECK(h && delta, "slam_graph_get_delta: bad arguments");
+    SLAM_HIP_TRY(hipSetDevice(h->device));
+    if (h->nt)
+        SLAM_HIP_TRY(hipMemcpyAsync(delta, h->delta, 3 * h->nt * sizeof(double),
+                                    hipMemcpyDeviceToHost, h->stream));
+    SLAM_HIP_TRY(hipStreamSynchronize(h->stream));
+    return SLAM_OK;
+}
+
 int slam_graph_timing(slam_graph* h, double* out) {
     SLAM_ARG_CHECK(h && out, "slam_graph_timing: NULL argument");
     for (int k = 0; k < 5; ++k) out[k] = h->last[k];

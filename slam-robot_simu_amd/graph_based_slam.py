@@ -1,0 +1,142 @@
+"""Drop-in TrajectoryEstimator backed by the MI355X kernels (libslam_hip.so).
+
+Same surface as the reference's estimator (graph_based_slam.py:330-514):
+``TrajectoryEstimator(aPose)`` with ``addPose``, ``setPairObs``,
+``updateEstPose`` and ``getEstTrajPose``, plus the Observation / HalfEdge
+records its callers build (:20-75, :259-300).  ``setPairObs`` only records the
+ordered pair; ``updateEstPose`` linearises every pair at the current pose
+estimates, assembles H and b, applies the reference's gate and solves on the
+GPU (csrc/graph_kernels.inl), then writes the updated poses back into the
+caller's (3,1) arrays in place -- the reference mutates them in place too
+(:499-502), and its Robot relies on that aliasing.
+
+``estimate_trajectory(halves, n_landmarks)`` is Robot.estimateOpticalTrajectory
+(:685-715): all 2-combinations of each landmark's half-edges, then
+Gauss-Newton until sum(delta^2) < 0.01, with the poses resident on the GPU
+between iterations.
+"""
+from __future__ import annotations
+
+import itertools
+
+import numpy as np
+
+from slamhip.graph import DeviceGraph
+
+DELTA_SUM_TH = 0.01          # graph_based_slam.py:662
+
+
+class Observation:
+    """graph_based_slam.py:20-75."""
+
+    def __init__(self, aLandMarkId, aDist_m, aDir_rad, aOrient_rad):
+        self._id, self._d, self._dir, self._or = aLandMarkId, aDist_m, aDir_rad, aOrient_rad
+
+    def getLandMarkId(self):
+        return self._id
+
+    def getDist(self):
+        return self._d
+
+    def getDir(self):
+        return self._dir
+
+    def getOrient(self):
+        return self._or
+
+
+class HalfEdge:
+    """graph_based_slam.py:259-300."""
+
+    def __init__(self, aTime, aObs, aRobotPoseId):
+        self._t, self._obs, self._pid = aTime, aObs, aRobotPoseId
+
+    def getTime(self):
+        return self._t
+
+    def getObs(self):
+        return self._obs
+
+    def getRobotPoseId(self):
+        return self._pid
+
+
+def _row(h_bfr, h_aft):
+    ob, oa = h_bfr.getObs(), h_aft.getObs()
+    return [h_bfr.getTime(), h_bfr.getRobotPoseId(), ob.getDist(), ob.getDir(), ob.getOrient(),
+            h_aft.getTime(), h_aft.getRobotPoseId(), oa.getDist(), oa.getDir(), oa.getOrient()]
+
+
+class TrajectoryEstimator(object):
+    """Pose-graph estimator (GPU linearise / assemble / solve)."""
+
+    def __init__(self, aPose, *, solver="auto", device=0):
+        self._poses = [aPose]
+        self._is_obs = [True]
+        self._rows = []
+        self._lm_ids = []
+        self._times = []
+        self._dev = DeviceGraph(solver=solver, device=device)
+
+    def addPose(self, aPose, aIsObs):
+        self._poses.append(aPose)
+        self._is_obs.append(aIsObs)
+
+    def setPairObs(self, aHalfEdge1, aHalfEdge2):
+        """:362-439 (the blocks are formed on the device at updateEstPose)."""
+        lm = aHalfEdge1.getObs().getLandMarkId()
+        if aHalfEdge1.getTime() > aHalfEdge2.getTime():
+            bfr, aft = aHalfEdge2, aHalfEdge1
+        else:
+            bfr, aft = aHalfEdge1, aHalfEdge2
+        if lm not in self._lm_ids:
+            self._lm_ids.append(lm)
+        for t in (bfr.getTime(), aft.getTime()):
+            if t not in self._times:
+                self._times.append(t)
+        self._rows.append(_row(bfr, aft))
+
+    def getEstTrajPose(self):
+        return [p for p, o in zip(self._poses, self._is_obs) if o]
+
+    def _upload_poses(self):
+        self._dev.set_poses(np.array([np.asarray(p, dtype=np.float64).reshape(3) for p in self._poses]))
+
+    def _write_back(self, times):
+        new = self._dev.get_poses()
+        for t in times:
+            self._poses[t][0, 0] = new[t, 0]
+            self._poses[t][1, 0] = new[t, 1]
+            self._poses[t][2, 0] = new[t, 2]
+
+    def updateEstPose(self):
+        """:452-514.  Returns (is_calc, delta_sum, det, cond)."""
+        is_calc, delta_sum, det, cond = False, 0.0, 0.0, 0.0
+        if len(self._times) * 3 > 3:
+            self._upload_poses()
+            self._dev.set_edges(self._rows)
+            is_calc, delta_sum, det, cond = self._dev.update()
+            if is_calc:
+                self._write_back(sorted(self._times))
+            else:
+                print("can Not calculate trajectory!")
+            self._rows, self._lm_ids, self._times = [], [], []
+        return is_calc, delta_sum, det, cond
+
+    def estimate_trajectory(self, halves, n_landmarks, max_iter=100):
+        """Robot.estimateOpticalTrajectory (:685-715) for the HalfEdge list
+        ``halves``: pairs every landmark's observations once, then iterates on
+        the device.  Returns the per-iteration (is_calc, delta_sum, det, cond)."""
+        for lm in range(n_landmarks):
+            mine = [h for h in halves if h.getObs().getLandMarkId() == lm]
+            for a, b in itertools.combinations(mine, 2):
+                self.setPairObs(a, b)
+        if len(self._times) * 3 <= 3:
+            return np.zeros((1, 4))
+        times = sorted(self._times)
+        self._upload_poses()
+        self._dev.set_edges(self._rows)
+        st = self._dev.optimize(DELTA_SUM_TH, max_iter)
+        self._write_back(times)
+        self._rows, self._lm_ids, self._times = [], [], []
+        return st

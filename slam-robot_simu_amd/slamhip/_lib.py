@@ -109,6 +109,8 @@ SIGNATURES = {
     "slam_ekf_step": (C.c_int, [_P, _D, _D, _D, _D, _D]),
     "slam_ekf_run": (C.c_int, [_P, C.c_int32, _D, _D, _D]),
     "slam_ekf_run_device": (C.c_int, [_P, C.c_int32, _D, _P, _P]),
+    "slam_ekf_load_observations": (C.c_int, [_P, C.c_int32, _D]),
+    "slam_ekf_run_loaded": (C.c_int, [_P, C.c_int32, _D, C.c_int32]),
     "slam_ekf_synchronize": (C.c_int, [_P]),
     "slam_ekfslam_create": (C.c_int, [C.POINTER(EKFSLAMConfig), C.c_int64, C.c_int,
                                       C.POINTER(_P)]),
@@ -128,6 +130,8 @@ SIGNATURES = {
     "slam_graph_update": (C.c_int, [_P, _D]),
     "slam_graph_optimize": (C.c_int, [_P, C.c_double, C.c_int32, _D, _I32]),
     "slam_graph_get_system": (C.c_int, [_P, _I64, _I64, _D, _D, _D]),
+    "slam_graph_get_bsr": (C.c_int, [_P, _I64, _I64, _I64, _D]),
+    "slam_graph_get_delta": (C.c_int, [_P, _D]),
     "slam_graph_timing": (C.c_int, [_P, _D]),
     "slam_graph_linearize_solve": (C.c_int, [C.POINTER(GraphConfig), _P, C.c_int64, _D, C.c_int64,
                                              _D, C.c_int]),

@@ -87,6 +87,30 @@ class DeviceEKF:
               "slam_ekf_run")
         return out
 
+    def run_device(self, n_steps, z_dev_ptr, xh_dev_ptr=None, control=None):
+        """n_steps steps with observations already in device memory (pointer to
+        n_steps x batch x 2 fp64); asynchronous (see synchronize)."""
+        ctl = None if control is None else _f64(control, (2,))
+        check(self._lib.slam_ekf_run_device(self._h, int(n_steps), dptr(ctl), C.c_void_p(z_dev_ptr),
+                                            C.c_void_p(xh_dev_ptr) if xh_dev_ptr else None),
+              "slam_ekf_run_device")
+
+    def load_observations(self, z_all):
+        z_all = _f64(z_all)
+        steps = z_all.shape[0]
+        check(self._lib.slam_ekf_load_observations(self._h, steps, dptr(z_all.reshape(steps, self.batch, 2))),
+              "slam_ekf_load_observations")
+        self.loaded_steps = steps
+
+    def run_loaded(self, n_steps, control=None, keep_history=True):
+        """Asynchronous: n_steps filter steps from the loaded observations."""
+        ctl = None if control is None else _f64(control, (2,))
+        check(self._lib.slam_ekf_run_loaded(self._h, int(n_steps), dptr(ctl), int(bool(keep_history))),
+              "slam_ekf_run_loaded")
+
+    def synchronize(self):
+        check(self._lib.slam_ekf_synchronize(self._h), "slam_ekf_synchronize")
+
 
 class DeviceEKFSLAM:
     """EKF-SLAM over ``n_landmarks`` landmarks (x, y, phi); covariance in HBM."""

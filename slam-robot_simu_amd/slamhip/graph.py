@@ -100,6 +100,26 @@ class DeviceGraph:
                                               dptr(H), dptr(b), dptr(blk)), "slam_graph_get_system")
         return times, H, b, blk
 
+    def get_bsr(self):
+        """(rows, cols, vals (n_slots, 3, 3)) of the last assembled H."""
+        ns = C.c_int64(0)
+        check(self._lib.slam_graph_get_bsr(self._h, C.byref(ns), None, None, None), "slam_graph_get_bsr")
+        rows = np.empty(ns.value, dtype=np.int64)
+        cols = np.empty(ns.value, dtype=np.int64)
+        vals = np.empty((ns.value, 3, 3))
+        P64 = C.POINTER(C.c_int64)
+        check(self._lib.slam_graph_get_bsr(self._h, C.byref(ns), rows.ctypes.data_as(P64),
+                                           cols.ctypes.data_as(P64), dptr(vals)), "slam_graph_get_bsr")
+        return rows, cols, vals
+
+    def get_delta(self):
+        nt = C.c_int64(0)
+        check(self._lib.slam_graph_get_system(self._h, C.byref(nt), None, None, None, None),
+              "slam_graph_get_system")
+        out = np.empty(3 * nt.value)
+        check(self._lib.slam_graph_get_delta(self._h, dptr(out)), "slam_graph_get_delta")
+        return out
+
     def timing(self):
         out = np.zeros(5)
         check(self._lib.slam_graph_timing(self._h, dptr(out)), "slam_graph_timing")
