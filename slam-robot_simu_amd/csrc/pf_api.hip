@@ -29,6 +29,8 @@ static void build_tail(int lo, int n, std::vector<int32_t>& leaves, std::vector<
     ops.push_back(-1);
 }
 
+constexpr int kGraphSteps = 8;     // steps per multi-step graph (even)
+
 struct Timer {
     std::vector<std::pair<hipEvent_t, hipEvent_t>> ev[4];
     size_t used[4] = {0, 0, 0, 0};
@@ -95,8 +97,14 @@ struct slam_pf {
     bool timing = false;
     bool use_graph = true;
     hipGraphExec_t graph[2] = {nullptr, nullptr};
+    hipGraphExec_t graph_multi[2] = {nullptr, nullptr};
     Timer tm;
     ShardScratch sh;
+    // deferred normalisation (single-GPU handles): current weights = w_un / s_cur
+    bool deferred = false;
+    double* s_cur = nullptr;
+    DeferParts dp{};
+    int32_t nb_part = 0;
 };
 
 namespace {
@@ -184,11 +192,12 @@ void toc(slam_pf* h, int k) {
 inline unsigned grid_for(int64_t n, int bs) { return (unsigned)((n + bs - 1) / bs); }
 
 void drop_graphs(slam_pf* h) {
-    for (auto& g : h->graph)
-        if (g) {
-            (void)hipGraphExecDestroy(g);
-            g = nullptr;
-        }
+    for (auto* gs : {h->graph, h->graph_multi})
+        for (int k = 0; k < 2; ++k)
+            if (gs[k]) {
+                (void)hipGraphExecDestroy(gs[k]);
+                gs[k] = nullptr;
+            }
 }
 
 void release(slam_pf* h, void* p) {
@@ -233,8 +242,12 @@ int set_flag(slam_pf* h, int word, int32_t v) {
 // S1 stand-alone: 256-block totals of w and their prefix (normalize_kernel
 // leaves the same arrays behind whenever the next step resamples).
 int launch_bsum(slam_pf* h) {
-    scan_bsum_kernel<<<h->nb_norm, kNormThreads, 0, h->stream>>>(h->w, h->n, h->bsum, h->boff,
-                                                                  h->tk + 2 * kTicketWords);
+    if (h->deferred)
+        scan_bsum256_kernel<<<h->nb_part, kPartPer, 0, h->stream>>>(
+            h->w_un, h->s_cur, h->pc.np_recip, h->n, h->bsum, h->boff, h->tk + 2 * kTicketWords);
+    else
+        scan_bsum_kernel<<<h->nb_norm, kNormThreads, 0, h->stream>>>(h->w, h->n, h->bsum, h->boff,
+                                                                      h->tk + 2 * kTicketWords);
     SLAM_HIP_TRY(hipGetLastError());
     return SLAM_OK;
 }
@@ -250,13 +263,17 @@ int launch_scans(slam_pf* h, int32_t force, bool with_s1) {
         const int rc = launch_bsum(h);
         if (rc) return rc;
     }
+    const double* w = h->deferred ? h->w_un : h->w;
+    const double* sd = h->deferred ? h->s_cur : nullptr;
+    const int32_t gran = h->deferred ? kPartPer : kNormPer;
     scan_classify_kernel<<<nb, kScanThreads, 0, s>>>(
-        h->w, n, h->boff, nullptr, h->c, h->kincl, h->fexcl, h->bk, h->bf, h->boffk, h->bofff,
-        h->ktot, h->nspec, delta, 0, h->tk + 2 * kTicketWords, h->flags, force);
-    scan_emit_kernel<<<nb, kScanThreads, 0, s>>>(h->w, n, h->c, h->kincl, h->fexcl, h->boffk,
+        w, n, h->boff, nullptr, h->c, h->kincl, h->fexcl, h->bk, h->bf, h->boffk, h->bofff,
+        h->ktot, h->nspec, delta, 0, h->tk + 2 * kTicketWords, h->flags, force, sd,
+        h->pc.np_recip, gran);
+    scan_emit_kernel<<<nb, kScanThreads, 0, s>>>(w, n, h->c, h->kincl, h->fexcl, h->boffk,
                                                  h->bofff, h->spec_in, 0, h->spec_out, h->nspec,
                                                  h->ktot, 1, h->c, h->tk + 2 * kTicketWords, h->flags,
-                                                 force);
+                                                 force, sd, h->pc.np_recip);
     scan_expand_kernel<<<nb, kScanThreads, 0, s>>>(n, h->kincl, h->fexcl, h->boffk, h->bofff,
                                                    h->spec_out, h->c, h->flags, nullptr,
                                                    nullptr, force);
@@ -268,15 +285,24 @@ int launch_fused(slam_pf* h, int motion, bool host_noise) {
     const int64_t n = h->n;
     const int src = h->cur, dst = 1 - h->cur;
     hipStream_t s = h->stream;
-    const unsigned g = grid_for(n, 256);
+    const unsigned g = h->deferred ? (unsigned)h->nb_part : grid_for(n, 256);
     const int lik = h->cfg.likelihood;
     const StepIO io = step_io(h);
     tic(h, 0);
-#define SLAM_FUSED(M, L, HN)                                                                     \
-    pf_fused_kernel<M, L, HN><<<g, 256, 0, s>>>(n, h->x[src], h->y[src], h->th[src], h->x[dst], \
-                                                h->y[dst], h->th[dst], h->w, h->w_un, h->c,      \
-                                                h->flags, h->noise, h->lm, io, h->pc, h->lc,     \
-                                                h->cfg.seed)
+    const double* w_in = h->deferred ? nullptr : h->w;     // deferred: read from w_un
+#define SLAM_FUSED_D(M, L, HN, D)                                                                \
+    pf_fused_kernel<M, L, HN, D><<<g, 256, 0, s>>>(n, h->x[src], h->y[src], h->th[src],         \
+                                                   h->x[dst], h->y[dst], h->th[dst], w_in,      \
+                                                   h->w_un, h->c, h->flags, h->noise, h->lm, io, \
+                                                   h->pc, h->lc, h->cfg.seed, h->s_cur, h->refp, \
+                                                   h->dp)
+#define SLAM_FUSED(M, L, HN)                 \
+    do {                                     \
+        if (h->deferred)                     \
+            SLAM_FUSED_D(M, L, HN, true);    \
+        else                                 \
+            SLAM_FUSED_D(M, L, HN, false);   \
+    } while (0)
     if (motion == kMotionNone) {
         if (lik == SLAM_LIK_PRODUCT) SLAM_FUSED(2, 0, false); else SLAM_FUSED(2, 1, false);
     } else if (motion == SLAM_MOTION_LINEAR) {
@@ -293,6 +319,7 @@ int launch_fused(slam_pf* h, int motion, bool host_noise) {
         }
     }
 #undef SLAM_FUSED
+#undef SLAM_FUSED_D
     toc(h, 0);
     h->cur = dst;
     SLAM_HIP_TRY(hipGetLastError());
@@ -305,6 +332,15 @@ int launch_reduce(slam_pf* h, int32_t resampled_known) {
     hipStream_t s = h->stream;
     const int c = h->cur;
     tic(h, 1);
+    if (h->deferred) {
+        finalize_deferred_kernel<<<1, 1024, 0, s>>>(
+            n, h->dp, h->w_un, h->s_cur, h->tail_leaves, h->tail_ops, h->n_tail_leaves,
+            h->n_tail_ops, h->x[c], h->y[c], h->th[c], h->refp, h->flags, h->cfg.ess_threshold,
+            step_io(h), resampled_known, h->pc.np_recip, h->boff);
+        toc(h, 1);
+        SLAM_HIP_TRY(hipGetLastError());
+        return SLAM_OK;
+    }
     chunk_sum_kernel<<<h->nchunks, 512, 0, s>>>(h->w_un, n, h->part, h->tail_leaves, h->tail_ops,
                                                  h->n_tail_leaves, h->n_tail_ops, h->tk,
                                                  h->wsum);
@@ -345,7 +381,8 @@ int sync_results(slam_pf* h, int32_t first, int32_t count, slam_pf_result* out) 
 }
 
 int create_impl(const slam_pf_config* cfg, int64_t n_local, int64_t n_global, int64_t gbase,
-                int32_t n_landmarks, const double* landmarks, int device, slam_pf** out) {
+                int32_t n_landmarks, const double* landmarks, int device, slam_pf** out,
+                bool deferred) {
     SLAM_ARG_CHECK(cfg && out, "slam_pf_create: NULL argument");
     SLAM_ARG_CHECK(n_local > 0 && n_global < (int64_t(1) << 31) && gbase >= 0 &&
                        gbase + n_local <= n_global,
@@ -378,6 +415,8 @@ int create_impl(const slam_pf_config* cfg, int64_t n_local, int64_t n_global, in
     h->nb_scan = (int32_t)((n + kScanBlock - 1) / kScanBlock);
     h->nchunks = (int32_t)((n + kSumChunk - 1) / kSumChunk);
     h->nb_norm = (int32_t)((n + kNormPer - 1) / kNormPer);
+    h->nb_part = (int32_t)((n + kPartPer - 1) / kPartPer);
+    h->deferred = deferred;
     hipError_t e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking);
     if (e != hipSuccess) {
         delete h;
@@ -399,8 +438,13 @@ int create_impl(const slam_pf_config* cfg, int64_t n_local, int64_t n_global, in
     A(h->kincl, n);
     A(h->fexcl, n);
     A(h->idx, n);
-    A(h->bsum, h->nb_norm);
-    A(h->boff, h->nb_norm + 1);
+    A(h->bsum, std::max(h->nb_norm, h->nb_part));
+    A(h->boff, std::max(h->nb_norm, h->nb_part) + 1);
+    A(h->s_cur, 1);
+    A(h->dp.pmax, h->nb_part);
+    A(h->dp.pidx, h->nb_part);
+    for (int q = 0; q < 11; ++q) A(h->dp.ps[q], h->nb_part);
+    A(h->dp.leaf, (size_t)(kPartPer / 128) * h->nb_part);
     A(h->bk, h->nb_scan);
     A(h->boffk, h->nb_scan);
     A(h->bf, h->nb_scan);
@@ -442,6 +486,9 @@ int create_impl(const slam_pf_config* cfg, int64_t n_local, int64_t n_global, in
     }
     std::fill(tmp.begin(), tmp.end(), 1.0 / (double)n_global);
     SLAM_HIP_TRY(hipMemcpy(h->w, tmp.data(), n * sizeof(double), hipMemcpyHostToDevice));
+    SLAM_HIP_TRY(hipMemcpy(h->w_un, tmp.data(), n * sizeof(double), hipMemcpyHostToDevice));
+    const double one = 1.0;
+    SLAM_HIP_TRY(hipMemcpy(h->s_cur, &one, sizeof(double), hipMemcpyHostToDevice));
     SLAM_HIP_TRY(hipMemcpy(h->refp, cfg->x0, 3 * sizeof(double), hipMemcpyHostToDevice));
     SLAM_HIP_TRY(hipMemset(h->flags, 0, kFlagWords * sizeof(int32_t)));
     SLAM_HIP_TRY(hipMemset(h->tk, 0, 4 * kTicketWords * sizeof(unsigned)));
@@ -449,6 +496,23 @@ int create_impl(const slam_pf_config* cfg, int64_t n_local, int64_t n_global, in
     if (n_landmarks > 0)
         SLAM_HIP_TRY(hipMemcpy(h->lm, landmarks, 2 * n_landmarks * sizeof(double), hipMemcpyHostToDevice));
     *out = h;
+    return SLAM_OK;
+}
+
+// deferred path: h->w <- w_un / s_cur (the current normalised weights)
+int materialize_w(slam_pf* h) {
+    if (!h->deferred) return SLAM_OK;
+    normalize_only_kernel<<<grid_for(h->n, 256), 256, 0, h->stream>>>(h->n, h->w_un, h->s_cur,
+                                                                       h->pc.np_recip, h->w);
+    SLAM_HIP_TRY(hipGetLastError());
+    return SLAM_OK;
+}
+
+int set_s_one(slam_pf* h) {
+    static const double one = 1.0;
+    if (h->deferred)
+        SLAM_HIP_TRY(hipMemcpyAsync(h->s_cur, &one, sizeof(double), hipMemcpyHostToDevice,
+                                    h->stream));
     return SLAM_OK;
 }
 
@@ -476,7 +540,7 @@ extern "C" {
 
 int slam_pf_create(const slam_pf_config* cfg, int64_t n_particles, int32_t n_landmarks,
                    const double* landmarks, int device, slam_pf** out) {
-    return create_impl(cfg, n_particles, n_particles, 0, n_landmarks, landmarks, device, out);
+    return create_impl(cfg, n_particles, n_particles, 0, n_landmarks, landmarks, device, out, true);
 }
 
 int slam_pf_create_shard(const slam_pf_config* cfg, int64_t n_local, int64_t n_global,
@@ -485,7 +549,7 @@ int slam_pf_create_shard(const slam_pf_config* cfg, int64_t n_local, int64_t n_g
     SLAM_ARG_CHECK(n_local % kSumChunk == 0 || gbase + n_local == n_global,
                    "slam_pf_create_shard: every shard but the last must hold a multiple of 8192 "
                    "particles (np.sum buffer alignment)");
-    return create_impl(cfg, n_local, n_global, gbase, n_landmarks, landmarks, device, out);
+    return create_impl(cfg, n_local, n_global, gbase, n_landmarks, landmarks, device, out, false);
 }
 
 int slam_pf_destroy(slam_pf* h) {
@@ -541,7 +605,14 @@ int slam_pf_set_state(slam_pf* h, const double* x, const double* y, const double
     if (y) SLAM_HIP_TRY(hipMemcpyAsync(h->y[c], y, b, hipMemcpyHostToDevice, h->stream));
     if (th) SLAM_HIP_TRY(hipMemcpyAsync(h->th[c], th, b, hipMemcpyHostToDevice, h->stream));
     if (w) {
-        SLAM_HIP_TRY(hipMemcpyAsync(h->w, w, b, hipMemcpyHostToDevice, h->stream));
+        if (h->deferred) {
+            static const double one = 1.0;
+            SLAM_HIP_TRY(hipMemcpyAsync(h->w_un, w, b, hipMemcpyHostToDevice, h->stream));
+            SLAM_HIP_TRY(hipMemcpyAsync(h->s_cur, &one, sizeof(double), hipMemcpyHostToDevice,
+                                        h->stream));
+        } else {
+            SLAM_HIP_TRY(hipMemcpyAsync(h->w, w, b, hipMemcpyHostToDevice, h->stream));
+        }
         // particle_filter.py:210-211: the resample decision from these weights
         // (single GPU; a shard's caller decides from the global ESS)
         if (h->n == h->n_global) {
@@ -564,7 +635,11 @@ int slam_pf_get_state(slam_pf* h, double* x, double* y, double* th, double* w) {
     if (x) SLAM_HIP_TRY(hipMemcpyAsync(x, h->x[c], b, hipMemcpyDeviceToHost, h->stream));
     if (y) SLAM_HIP_TRY(hipMemcpyAsync(y, h->y[c], b, hipMemcpyDeviceToHost, h->stream));
     if (th) SLAM_HIP_TRY(hipMemcpyAsync(th, h->th[c], b, hipMemcpyDeviceToHost, h->stream));
-    if (w) SLAM_HIP_TRY(hipMemcpyAsync(w, h->w, b, hipMemcpyDeviceToHost, h->stream));
+    if (w) {
+        int rc = materialize_w(h);
+        if (rc) return rc;
+        SLAM_HIP_TRY(hipMemcpyAsync(w, h->w, b, hipMemcpyDeviceToHost, h->stream));
+    }
     SLAM_HIP_TRY(hipStreamSynchronize(h->stream));
     return SLAM_OK;
 }
@@ -604,9 +679,10 @@ int slam_pf_resample(slam_pf* h, double u_resample, int32_t force, int32_t* resa
         h->n, h->c, h->idx, h->pc.rstep, ofs, h->pc.np_recip, h->cfg.seed, h->stepno, h->flags);
     const int src = h->cur, dst = 1 - h->cur;
     gather_kernel<<<grid_for(h->n, 256), 256, 0, h->stream>>>(
-        h->n, h->idx, h->x[src], h->y[src], h->th[src], h->x[dst], h->y[dst], h->th[dst], h->w,
-        h->pc.np_recip);
+        h->n, h->idx, h->x[src], h->y[src], h->th[src], h->x[dst], h->y[dst], h->th[dst],
+        h->deferred ? h->w_un : h->w, h->pc.np_recip);
     SLAM_HIP_TRY(hipGetLastError());
+    if ((rc = set_s_one(h))) return rc;
     h->cur = dst;
     int32_t st = 0;
     SLAM_HIP_TRY(hipMemcpyAsync(&st, h->flags + kFlagStatus, 4, hipMemcpyDeviceToHost, h->stream));
@@ -654,11 +730,18 @@ int slam_pf_predict(slam_pf* h, const double* control, const double* noise) {
     if ((rc = stage_inputs(h, control, nullptr, noise, std::nan("")))) return rc;
     if ((rc = set_flag(h, kFlagResample, 0))) return rc;
     const int32_t nl = h->lc.nl;
+    const double lnd = h->lc.neg_nl_ln_den;
     h->lc.nl = 0;
+    h->lc.neg_nl_ln_den = 0.0;          // zero landmarks: likelihood factor exactly 1
     rc = launch_fused(h, h->cfg.motion, noise != nullptr);
     h->lc.nl = nl;
+    h->lc.neg_nl_ln_den = lnd;
     if (rc) return rc;
-    SLAM_HIP_TRY(hipMemcpyAsync(h->w, h->w_un, h->n * 8, hipMemcpyDeviceToDevice, h->stream));
+    if (h->deferred) {
+        if ((rc = set_s_one(h))) return rc;   // w_un now holds the normalised weights
+    } else {
+        SLAM_HIP_TRY(hipMemcpyAsync(h->w, h->w_un, h->n * 8, hipMemcpyDeviceToDevice, h->stream));
+    }
     if ((rc = set_flag(h, kFlagResample, h->resample_next))) return rc;
     h->stepno++;
     SLAM_HIP_TRY(hipStreamSynchronize(h->stream));
@@ -682,6 +765,8 @@ int slam_pf_update(slam_pf* h, const double* z, slam_pf_result* res) {
 int slam_pf_weight_sum(slam_pf* h, double* sum_out) {
     SLAM_ARG_CHECK(h && sum_out, "slam_pf_weight_sum: NULL argument");
     SLAM_HIP_TRY(hipSetDevice(h->device));
+    int rc = materialize_w(h);
+    if (rc) return rc;
     chunk_sum_kernel<<<h->nchunks, 512, 0, h->stream>>>(h->w, h->n, h->part, h->tail_leaves,
                                                          h->tail_ops, h->n_tail_leaves,
                                                          h->n_tail_ops, h->tk, h->wsum);
@@ -720,30 +805,41 @@ int slam_pf_run(slam_pf* h, int32_t first_step, int32_t n_steps, const double* c
     if ((rc = set_ctr(h, first_step)) || (rc = set_flag(h, kFlagResample, h->resample_next))) return rc;
     if (h->resample_next && (rc = launch_bsum(h))) return rc;   // prefix for the first step's scan
     const bool graphs = h->use_graph && !h->timing;
-    for (int32_t k = 0; k < n_steps; ++k) {
+    // one captured hipGraph per ping-pong parity for kGraphSteps steps (even:
+    // the parity comes back) and for a single step; the step context lives in
+    // device memory, so a replay needs no host input.
+    auto capture = [&](hipGraphExec_t& ge, int steps) -> int {
+        const int cur0 = h->cur;
+        hipGraph_t g;
+        SLAM_HIP_TRY(hipStreamBeginCapture(h->stream, hipStreamCaptureModeThreadLocal));
+        int rc2 = SLAM_OK;
+        for (int k = 0; k < steps && rc2 == SLAM_OK; ++k) rc2 = launch_step(h, false);
+        hipError_t e = hipStreamEndCapture(h->stream, &g);
+        h->cur = cur0;
+        if (rc2) return rc2;
+        if (e != hipSuccess) return fail(SLAM_ERR_HIP, "hipStreamEndCapture failed");
+        SLAM_HIP_TRY(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
+        (void)hipGraphDestroy(g);
+        return SLAM_OK;
+    };
+    int32_t k = 0;
+    while (k < n_steps) {
         if (graphs) {
-            hipGraphExec_t& ge = h->graph[h->cur];
-            if (!ge) {
-                // capture one device-decided step for this ping-pong parity
-                const int cur0 = h->cur;
-                hipGraph_t g;
-                SLAM_HIP_TRY(hipStreamBeginCapture(h->stream, hipStreamCaptureModeThreadLocal));
-                rc = launch_step(h, false);
-                hipError_t e = hipStreamEndCapture(h->stream, &g);
-                h->cur = cur0;
-                if (rc) return rc;
-                if (e != hipSuccess) return fail(SLAM_ERR_HIP, "hipStreamEndCapture failed");
-                SLAM_HIP_TRY(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
-                (void)hipGraphDestroy(g);
-            }
+            const bool multi = n_steps - k >= kGraphSteps;
+            hipGraphExec_t& ge = multi ? h->graph_multi[h->cur] : h->graph[h->cur];
+            if (!ge && (rc = capture(ge, multi ? kGraphSteps : 1))) return rc;
             SLAM_HIP_TRY(hipGraphLaunch(ge, h->stream));
-            h->cur = 1 - h->cur;
+            const int done = multi ? kGraphSteps : 1;
+            if (done & 1) h->cur = 1 - h->cur;
+            k += done;
+            h->stepno += done;
         } else {
             tic(h, 3);
             if ((rc = launch_step(h, false))) return rc;
             toc(h, 3);
+            ++k;
+            h->stepno++;
         }
-        h->stepno++;
     }
     return sync_results(h, first_step, n_steps, results);
 }

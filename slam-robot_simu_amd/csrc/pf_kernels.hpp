@@ -12,6 +12,23 @@ constexpr int kScanPer = kScanBlock / kScanThreads;  // 8
 constexpr int kNormThreads = 256;
 constexpr int kNormEPT = 4;                          // particles per lane in normalize
 constexpr int kNormPer = kNormThreads * kNormEPT;    // particles per normalize block
+#ifndef SLAM_DEFER_PPT
+#define SLAM_DEFER_PPT 2
+#endif
+constexpr int kDeferPPT = SLAM_DEFER_PPT;            // particles per lane, deferred fused kernel
+constexpr int kPartPer = 256 * kDeferPPT;            // particles per fused block (deferred path)
+
+// Deferred normalisation (single-GPU handles): the fused kernel leaves, per
+// 512-particle block, its max unnormalised weight M_b with the first index,
+// sums scaled by 1/M_b (sum u, sum u^2, sum u d, sum u d d^T with u = w_un/M_b
+// and d = particle - refp; scaling keeps squares of tiny likelihoods out of
+// the subnormal range) and its four 128-element np.sum leaf sums.
+struct DeferParts {
+    double* pmax;
+    int64_t* pidx;
+    double* ps[11];         // sw, sw2, m1[3], m2[6]
+    double* leaf;           // [(kPartPer / 128) * blocks]
+};
 
 // particle_filter.py:179-181 + the mlab.bivariate_normal constants
 struct LikConst {

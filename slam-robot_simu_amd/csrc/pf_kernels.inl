@@ -157,19 +157,152 @@ __device__ __forceinline__ int64_t lower_bound_c(const double* __restrict__ c, c
 // fused [resample gather +] predict + likelihood
 //      (particle_filter.py:156-198, :216-222; motion_model.py:31-62)
 // ====================================================================
-template <int MOTION, int LIK, bool HOSTNOISE>
-__global__ __launch_bounds__(256) void pf_fused_kernel(
-    const int64_t n, const double* __restrict__ xs, const double* __restrict__ ys,
-    const double* __restrict__ ts, double* __restrict__ xo, double* __restrict__ yo,
-    double* __restrict__ to, const double* __restrict__ w_in, double* __restrict__ w_un,
-    const double* __restrict__ c, int32_t* __restrict__ flags, const double* __restrict__ noise,
-    const double* __restrict__ lm, StepIO io, PredictConst pc, LikConst lc, uint64_t seed) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const int32_t st = io.ctr[0];
-    const uint32_t rstep = (uint32_t)io.ctr[1];
-    const int32_t rflag = flags[kFlagResample];
+// weight of the current step from the deferred representation:
+// particle_filter.py:235-236  w = w_un / s, NaN -> 1/NP
+__device__ __forceinline__ double norm_w(const double wu, const double s, const double np_recip) {
+    const double v = wu / s;
+    return isnan(v) ? np_recip : v;
+}
 
+// (value, index) max with the first index on ties (np.argmax)
+__device__ __forceinline__ void max_first(double& v, int64_t& i, const double ov, const int64_t oi) {
+    if (ov > v || (ov == v && oi < i)) {
+        v = ov;
+        i = oi;
+    }
+}
+
+// Deferred-path epilogue of a 256-lane, kPartPer-particle fused block (see
+// DeferParts).  Lane t holds particles t + 256 k (k < kDeferPPT); invalid ones carry
+// w = 0.  Every sum has a fixed order: per lane over k, then 16 lane-strided
+// segments (conflict-free LDS reads) left to right, then the 16 segments.
+__device__ void defer_epilogue(const int64_t base, const int64_t n, const double* wv,
+                               const double* xv, const double* yv, const double* tv,
+                               const double* __restrict__ refp, const DeferParts& dp) {
+    __shared__ double s_w[kPartPer];
+    __shared__ double s_q[6 * 256];
+    __shared__ double s_seg[6 * 16];
+    __shared__ double s_acc[64];
+    __shared__ double s_mv[4];
+    __shared__ int64_t s_mi[4];
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    // lane max and its first particle, then the block max
+    double m = -1.0;
+    int64_t mi = INT64_MAX;
+#pragma unroll
+    for (int k = 0; k < kDeferPPT; ++k) {
+        const int64_t i = base + t + 256 * k;
+        const bool ok = i < n;
+        s_w[t + 256 * k] = ok ? wv[k] : 0.0;
+        if (ok && wv[k] > m) {
+            m = wv[k];
+            mi = i;
+        }
+    }
+    double mv = m;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) mv = fmax(mv, __shfl_xor(mv, d, 64));
+    if (lane == 0) s_mv[wave] = mv;
+    __syncthreads();
+    const double M = fmax(fmax(s_mv[0], s_mv[1]), fmax(s_mv[2], s_mv[3]));
+    // first index holding M: min over the lanes whose max equals M
+    int64_t cand = (m == M) ? mi : INT64_MAX;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const int64_t o = __shfl_xor(cand, d, 64);
+        cand = o < cand ? o : cand;
+    }
+    if (lane == 0) s_mi[wave] = cand;
+    const double rs = (M > 0.0) ? 1.0 / M : 0.0;
+    const double r0 = refp[0], r1 = refp[1], r2 = refp[2];
+    double q[11];
+#pragma unroll
+    for (int j = 0; j < 11; ++j) q[j] = 0.0;
+#pragma unroll
+    for (int k = 0; k < kDeferPPT; ++k) {
+        const bool ok = base + t + 256 * k < n;
+        const double u = ok ? wv[k] * rs : 0.0;
+        const double d0 = xv[k] - r0, d1 = yv[k] - r1, d2 = tv[k] - r2;
+        const double ud0 = u * d0, ud1 = u * d1, ud2 = u * d2;
+        q[0] += u;
+        q[1] += u * u;
+        q[2] += ud0;
+        q[3] += ud1;
+        q[4] += ud2;
+        q[5] += ud0 * d0;
+        q[6] += ud0 * d1;
+        q[7] += ud0 * d2;
+        q[8] += ud1 * d1;
+        q[9] += ud1 * d2;
+        q[10] += ud2 * d2;
+    }
+    const int blk = blockIdx.x;
+    constexpr int kLeaves = kPartPer / 128;
+    // round 1: sw, sw2, m1[3] (+ the np.sum leaves' accumulators on lanes 128 ..)
+#pragma unroll
+    for (int j = 0; j < 5; ++j) s_q[j * 256 + t] = q[j];
+    __syncthreads();
+    if (t < 5 * 16) {
+        const double* a = s_q + (t >> 4) * 256 + (t & 15);
+        double acc = a[0];
+#pragma unroll
+        for (int mm = 1; mm < 16; ++mm) acc = acc + a[16 * mm];
+        s_seg[t] = acc;
+    } else if (t >= 128 && t < 128 + 8 * kLeaves) {
+        // leaf (t-128)>>3, accumulator k = t & 7: elements k, k+8, ..., k+120
+        const double* a = s_w + ((t - 128) >> 3) * 128 + (t & 7);
+        double acc = a[0];
+#pragma unroll
+        for (int mm = 1; mm < 16; ++mm) acc = acc + a[8 * mm];
+        s_acc[t - 128] = acc;
+    }
+    __syncthreads();
+    if (t < 5) {
+        double acc = s_seg[16 * t];
+        for (int mm = 1; mm < 16; ++mm) acc = acc + s_seg[16 * t + mm];
+        dp.ps[t][blk] = acc;
+    } else if (t >= 64 && t < 64 + kLeaves) {
+        const double* r = s_acc + 8 * (t - 64);
+        dp.leaf[kLeaves * blk + (t - 64)] = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+    } else if (t == 128) {
+        int64_t bi = s_mi[0];
+        for (int w = 1; w < 4; ++w) bi = s_mi[w] < bi ? s_mi[w] : bi;
+        dp.pmax[blk] = M;
+        dp.pidx[blk] = bi;
+    }
+    __syncthreads();
+    // round 2: m2[6]
+#pragma unroll
+    for (int j = 0; j < 6; ++j) s_q[j * 256 + t] = q[5 + j];
+    __syncthreads();
+    if (t < 6 * 16) {
+        const double* a = s_q + (t >> 4) * 256 + (t & 15);
+        double acc = a[0];
+#pragma unroll
+        for (int mm = 1; mm < 16; ++mm) acc = acc + a[16 * mm];
+        s_seg[t] = acc;
+    }
+    __syncthreads();
+    if (t < 6) {
+        double acc = s_seg[16 * t];
+        for (int mm = 1; mm < 16; ++mm) acc = acc + s_seg[16 * t + mm];
+        dp.ps[5 + t][blk] = acc;
+    }
+}
+
+// One particle of the fused step: [resample gather +] predict + likelihood
+// (particle_filter.py:156-198, :216-222; motion_model.py:31-62).  Stores the
+// predicted particle and w_un = pw * likelihood when `store`.
+template <int MOTION, int LIK, bool HOSTNOISE>
+__device__ __forceinline__ void particle_update(
+    const int64_t i, const bool store, const int64_t n, const int32_t st, const uint32_t rstep,
+    const int32_t rflag, const double pw_prev, const double* __restrict__ xs,
+    const double* __restrict__ ys, const double* __restrict__ ts, double* __restrict__ xo,
+    double* __restrict__ yo, double* __restrict__ to, double* __restrict__ w_un,
+    const double* __restrict__ c, int32_t* __restrict__ flags, const double* __restrict__ noise,
+    const double* __restrict__ lm, const double* __restrict__ zs, const StepIO& io,
+    const PredictConst& pc, const LikConst& lc, const uint64_t seed, double& xn, double& yn,
+    double& tn, double& wv) {
     // ---- resample gather (1: search the exact cumsum here; 2: already gathered)
     int64_t src = i;
     if (rflag == 1) {
@@ -178,10 +311,10 @@ __global__ __launch_bounds__(256) void pf_fused_kernel(
         src = lower_bound_c(c, n, pos);
         if (src >= n) {
             src = n - 1;                                          // IndexError in the reference
-            atomicOr(&flags[kFlagStatus], 1);
+            if (store) atomicOr(&flags[kFlagStatus], 1);
         }
     }
-    const double pw = rflag ? pc.np_recip : w_in[i];              // particle_filter.py:222
+    const double pw = rflag ? pc.np_recip : pw_prev;             // particle_filter.py:222
     const double x = xs[src], y = ys[src], th = ts[src];
 
     // ---- control of this step (particle_filter.py:46-58 / motion_model.py:40-45)
@@ -215,7 +348,6 @@ __global__ __launch_bounds__(256) void pf_fused_kernel(
     }
 
     // ---- predict
-    double xn, yn, tn;
     if (MOTION == kMotionNone) {           // likelihood-only entry (particle_filter.py:170)
         xn = x;
         yn = y;
@@ -245,13 +377,15 @@ __global__ __launch_bounds__(256) void pf_fused_kernel(
         yn = (y + (a * c0)) - (a * c1);
         tn = wrap_angle(th + (wh + gh) * pc.dt);
     }
-    xo[i] = xn;
-    yo[i] = yn;
-    to[i] = tn;
+    if (store) {
+        xo[i] = xn;
+        yo[i] = yn;
+        to[i] = tn;
+    }
 
     // ---- likelihood: world2robot (mylib/transform.py:31-35) per landmark
     const int nl = lc.nl;
-    const double* __restrict__ z = io.z + (size_t)st * 2 * (size_t)(nl > 0 ? nl : 1);
+    const double* __restrict__ z = zs;
     double sp, cp;
     sincos(kHalfPi - tn, &sp, &cp);
     double bn;
@@ -304,7 +438,52 @@ __global__ __launch_bounds__(256) void pf_fused_kernel(
         }
         bn = exp(lc.has_rho ? fma(-S, lc.rd2, lc.neg_nl_ln_den) : fma(-0.5, S, lc.neg_nl_ln_den));
     }
-    w_un[i] = pw * bn;                                           // particle_filter.py:194
+    wv = pw * bn;                                               // particle_filter.py:194
+    if (store) w_un[i] = wv;
+}
+
+// The fused step kernel.  DEFER = false (shards): one particle per lane,
+// previous weights normalised in w_in.  DEFER = true (single GPU): four
+// particles per lane, previous weights = w_un / s (read and rewritten in
+// place), plus the block epilogue that replaces the normalise pass.
+template <int MOTION, int LIK, bool HOSTNOISE, bool DEFER>
+__global__ __launch_bounds__(256) void pf_fused_kernel(
+    const int64_t n, const double* __restrict__ xs, const double* __restrict__ ys,
+    const double* __restrict__ ts, double* __restrict__ xo, double* __restrict__ yo,
+    double* __restrict__ to, const double* __restrict__ w_in, double* __restrict__ w_un,
+    const double* __restrict__ c, int32_t* __restrict__ flags, const double* __restrict__ noise,
+    const double* __restrict__ lm, StepIO io, PredictConst pc, LikConst lc, uint64_t seed,
+    const double* __restrict__ s_in, const double* __restrict__ refp, DeferParts dp) {
+    // DEFER: the previous weights are read from w_un itself (w_in unused)
+    const int32_t st = io.ctr[0];
+    const uint32_t rstep = (uint32_t)io.ctr[1];
+    const int32_t rflag = flags[kFlagResample];
+    const double* __restrict__ zs = io.z + (size_t)st * 2 * (size_t)(lc.nl > 0 ? lc.nl : 1);
+    if constexpr (!DEFER) {
+        const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+        if (i >= n) return;
+        double xn, yn, tn, wv;
+        particle_update<MOTION, LIK, HOSTNOISE>(i, true, n, st, rstep, rflag, rflag ? 0.0 : w_in[i],
+                                                xs, ys, ts, xo, yo, to, w_un, c, flags, noise, lm,
+                                                zs, io, pc, lc, seed, xn, yn, tn, wv);
+    } else {
+        const int64_t base = (int64_t)blockIdx.x * kPartPer;
+        const double s_prev = *s_in;
+        double xv[kDeferPPT], yv[kDeferPPT], tv[kDeferPPT], wv[kDeferPPT];
+#pragma unroll
+        for (int k = 0; k < kDeferPPT; ++k) {
+            const int64_t i0 = base + threadIdx.x + 256 * k;
+            const bool valid = i0 < n;
+            const int64_t i = valid ? i0 : n - 1;
+            const double pw = rflag ? 0.0 : norm_w(w_un[i], s_prev, pc.np_recip);
+            particle_update<MOTION, LIK, HOSTNOISE>(i, valid, n, st, rstep, rflag, pw, xs, ys, ts,
+                                                    xo, yo, to, w_un, c, flags, noise, lm, zs, io,
+                                                    pc, lc, seed, xv[k], yv[k], tv[k], wv[k]);
+        }
+#ifndef SLAM_NO_EPILOGUE
+        defer_epilogue(base, n, wv, xv, yv, tv, refp, dp);
+#endif
+    }
 }
 
 // ====================================================================
@@ -446,9 +625,10 @@ __device__ __forceinline__ void bp_merge(BlockPartial& r, const BlockPartial& o)
 }
 
 // xor-butterfly over the 64 lanes (lower lane always on the left: a fixed tree)
+template <int W = 64>
 __device__ __forceinline__ void bp_wave_reduce(BlockPartial& a) {
 #pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
+    for (int d = 1; d < W; d <<= 1) {
         BlockPartial o;
         o.maxv = __shfl_xor(a.maxv, d, 64);
         o.maxi = __shfl_xor(a.maxi, d, 64);
@@ -467,14 +647,21 @@ __device__ __forceinline__ void bp_wave_reduce(BlockPartial& a) {
     }
 }
 
-// block-level fixed-order reduction of per-thread partials (result in thread 0)
+// block-level fixed-order reduction of per-thread partials (result in thread 0):
+// a butterfly inside every wave, then a butterfly over the wave partials in wave 0
 __device__ __forceinline__ BlockPartial bp_block_reduce(BlockPartial a, BlockPartial* shp) {
     bp_wave_reduce(a);
+    const int nw = (int)(blockDim.x >> 6);
     if ((threadIdx.x & 63) == 0) shp[threadIdx.x >> 6] = a;
     __syncthreads();
-    BlockPartial r = shp[0];
-    if (threadIdx.x == 0)
-        for (int k = 1; k < (int)(blockDim.x >> 6); ++k) bp_merge(r, shp[k]);
+    BlockPartial r;
+    if (threadIdx.x < 64) {
+        if ((int)threadIdx.x < nw) r = shp[threadIdx.x];
+        else bp_zero(r);
+        if (nw > 8) bp_wave_reduce<16>(r);
+        else if (nw > 4) bp_wave_reduce<8>(r);
+        else bp_wave_reduce<4>(r);
+    }
     __syncthreads();
     return r;
 }
@@ -624,6 +811,310 @@ __global__ __launch_bounds__(1024) void finalize_kernel(
     }
 }
 
+// np.sum of one full 8192-element buffer from its 64 leaf sums (perfect
+// pairwise tree, left + right at every node).
+__device__ __forceinline__ double chunk_tree64(const double* __restrict__ L) {
+    double stk[7];
+    for (int i = 0; i < 64; ++i) {
+        double v = L[i];
+        int b = 0;
+        for (; (i >> b) & 1; ++b) v = stk[b] + v;
+        stk[b] = v;
+    }
+    return stk[6];
+}
+
+// np.sum of a tail buffer (< 8192 elements) from raw weights: leaves by the
+// block's lanes, the post-order program by lane 0 (as chunk_sum_kernel).
+__device__ double tail_chunk_sum(const double* __restrict__ w, const int32_t* __restrict__ leaves,
+                                 const int32_t* __restrict__ ops, const int32_t n_leaves,
+                                 const int32_t n_ops, double* sh) {
+    for (int L = threadIdx.x; L < n_leaves; L += blockDim.x) {
+        const int lo = leaves[2 * L], cnt = leaves[2 * L + 1];
+        const double* a = w + lo;
+        double res;
+        if (cnt < 8) {
+            res = 0.0;
+            for (int i = 0; i < cnt; ++i) res = res + a[i];
+        } else {
+            double r[8];
+            for (int k = 0; k < 8; ++k) r[k] = a[k];
+            int i = 8;
+            const int stop = cnt - (cnt % 8);
+            for (; i < stop; i += 8)
+                for (int k = 0; k < 8; ++k) r[k] = r[k] + a[i + k];
+            res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+            for (; i < cnt; ++i) res = res + a[i];
+        }
+        sh[L] = res;
+    }
+    __syncthreads();
+    double out = 0.0;
+    if (threadIdx.x == 0) {
+        double stk[16];
+        int sp = 0;
+        for (int o = 0; o < n_ops; ++o) {
+            const int op = ops[o];
+            if (op >= 0) {
+                stk[sp++] = sh[op];
+            } else {
+                const double b = stk[--sp];
+                const double a = stk[--sp];
+                stk[sp++] = a + b;
+            }
+        }
+        out = stk[0];
+    }
+    __syncthreads();
+    return out;
+}
+
+#ifdef SLAM_FIN_PROBE
+__device__ long long g_fin_probe[16];
+#define FIN_STAMP(k) do { if (threadIdx.x == 0) g_fin_probe[k] = wall_clock64(); } while (0)
+#else
+#define FIN_STAMP(k) do { } while (0)
+#endif
+
+// Deferred-path step end (one workgroup, single-GPU handles): np.sum of the
+// unnormalised weights from the fused blocks' leaf sums (particle_filter.py:234),
+// the block partials rescaled to the global max and combined in block order,
+// the exact max / first argmax of w = w_un / s (the first block whose
+// fl(M_b / s) equals fl(M / s) is rescanned element by element), the result
+// record, the step context, s for the next step, and -- when the next step
+// resamples -- the prefix of the 256-block weight totals for its exact cumsum.
+// Loads are issued up front (the kernel is latency-bound).  A non-positive
+// or non-finite s (all weights NaN -> 1/NP, :236) takes a slow whole-array pass.
+__global__ __launch_bounds__(1024) void finalize_deferred_kernel(
+    const int64_t n, const DeferParts dp, const double* __restrict__ w_un,
+    double* __restrict__ s_cur, const int32_t* __restrict__ tail_leaves,
+    const int32_t* __restrict__ tail_ops, const int32_t n_tail_leaves, const int32_t n_tail_ops,
+    const double* __restrict__ xs, const double* __restrict__ ys, const double* __restrict__ ts,
+    double* __restrict__ refp, int32_t* __restrict__ flags, const double ess_th, StepIO io,
+    const int32_t resampled_known, const double np_recip, double* __restrict__ boff) {
+    __shared__ double sh[1024];
+    __shared__ BlockPartial shp[1024 / 64];
+    __shared__ double s_bc[2];
+    __shared__ double s_wmax[16];
+    __shared__ double s_q[11 * 1024];
+    __shared__ double s_tot[11];
+    __shared__ unsigned long long s_min;
+    __shared__ int32_t want_scan;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int64_t nb = (n + kPartPer - 1) / kPartPer;
+    FIN_STAMP(0);
+    // ---- the first partial of every lane: loads issued up front, unconditionally
+    const int64_t b0 = tid < nb ? tid : nb - 1;
+    const double pm0 = (tid < nb) ? dp.pmax[b0] : -1.0;
+    // ---- np.sum: 8192-element buffers left to right; 8 lanes per buffer
+    const int64_t nfull = n / kSumChunk;
+    const int64_t nch = (n + kSumChunk - 1) / kSumChunk;
+    double s = 0.0;
+    for (int64_t c0 = 0; c0 < nfull; c0 += 128) {
+        const int64_t cnt = (nfull - c0 < 128) ? nfull - c0 : 128;
+        const int64_t c = c0 + (tid >> 3);
+        const int part = tid & 7;
+        double v = 0.0;
+        if ((tid >> 3) < cnt) {
+            const double* L = dp.leaf + 64 * c + 8 * part;
+            const double l0 = L[0], l1 = L[1], l2 = L[2], l3 = L[3];
+            const double l4 = L[4], l5 = L[5], l6 = L[6], l7 = L[7];
+            v = ((l0 + l1) + (l2 + l3)) + ((l4 + l5) + (l6 + l7));
+        }
+#pragma unroll
+        for (int d = 1; d < 8; d <<= 1) {
+            const double o = __shfl_xor(v, d, 64);
+            v = (part & d) ? (o + v) : (v + o);          // left operand = lower lane
+        }
+        __syncthreads();
+        if (part == 0 && (tid >> 3) < cnt) sh[tid >> 3] = v;
+        __syncthreads();
+        if (tid == 0) {
+#pragma unroll 16
+            for (int k = 0; k < cnt; ++k) s = s + sh[k];
+        }
+    }
+    if (nch > nfull) {
+        __syncthreads();
+        const double tsum = tail_chunk_sum(w_un + nfull * kSumChunk, tail_leaves, tail_ops,
+                                           n_tail_leaves, n_tail_ops, sh);
+        if (tid == 0) s = s + tsum;
+    }
+    // ---- global max of the block maxima
+    FIN_STAMP(1);
+    double mx = pm0;
+    for (int64_t b = tid + 1024; b < nb; b += 1024) mx = fmax(mx, dp.pmax[b]);
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) mx = fmax(mx, __shfl_xor(mx, d, 64));
+    if (lane == 0) s_wmax[wave] = mx;
+    if (tid == 0) s_bc[0] = s;
+    __syncthreads();
+    double M = s_wmax[0];
+    for (int w = 1; w < 16; ++w) M = fmax(M, s_wmax[w]);
+    s = s_bc[0];
+    const bool ok = (s > 0.0) && !isinf(s) && (M > 0.0);
+    FIN_STAMP(2);
+    BlockPartial tot;
+    bp_zero(tot);
+    if (ok) {
+        // ---- block partials rescaled to the global max: per lane in block
+        // order, then a fixed LDS tree (16 lane-strided segments per wave
+        // position, a butterfly per quantity)
+        double acc[11];
+#pragma unroll
+        for (int j = 0; j < 11; ++j) acc[j] = 0.0;
+        for (int64_t b = tid; b < nb; b += 1024) {
+            const double r = (b == tid ? pm0 : dp.pmax[b]) / M;
+            double qb[11];
+#pragma unroll
+            for (int j = 0; j < 11; ++j) qb[j] = dp.ps[j][b];
+            acc[0] += r * qb[0];
+            acc[1] += (r * r) * qb[1];
+#pragma unroll
+            for (int j = 2; j < 11; ++j) acc[j] += r * qb[j];
+        }
+#pragma unroll
+        for (int j = 0; j < 11; ++j) s_q[j * 1024 + tid] = acc[j];
+        __syncthreads();
+        if (wave < 11) {
+            const double* a = s_q + wave * 1024 + lane;
+            double r = a[0];
+#pragma unroll
+            for (int mm = 1; mm < 16; ++mm) r = r + a[64 * mm];
+#pragma unroll
+            for (int d = 1; d < 64; d <<= 1) {
+                const double o = __shfl_xor(r, d, 64);
+                r = (lane & d) ? (o + r) : (r + o);
+            }
+            if (lane == 0) s_tot[wave] = r;
+        }
+        __syncthreads();
+        if (tid == 0) {
+            tot.sw = s_tot[0];
+            tot.sw2 = s_tot[1];
+            for (int j = 0; j < 3; ++j) tot.m1[j] = s_tot[2 + j];
+            for (int j = 0; j < 6; ++j) tot.m2[j] = s_tot[5 + j];
+        }
+    } else {
+        // ---- every weight through the reference's division (slow, degenerate case)
+        BlockPartial a;
+        bp_zero(a);
+        const double r0 = refp[0], r1 = refp[1], r2 = refp[2];
+        for (int64_t i = tid; i < n; i += 1024) {
+            const double v = norm_w(w_un[i], s, np_recip);
+            BlockPartial o;
+            o.maxv = v;
+            o.maxi = i;
+            o.sw = v;
+            o.sw2 = v * v;
+            const double d0 = xs[i] - r0, d1 = ys[i] - r1, d2 = ts[i] - r2;
+            const double v0 = v * d0, v1 = v * d1, v2 = v * d2;
+            o.m1[0] = v0; o.m1[1] = v1; o.m1[2] = v2;
+            o.m2[0] = v0 * d0; o.m2[1] = v0 * d1; o.m2[2] = v0 * d2;
+            o.m2[3] = v1 * d1; o.m2[4] = v1 * d2; o.m2[5] = v2 * d2;
+            bp_merge(a, o);
+        }
+        tot = bp_block_reduce(a, shp);
+    }
+    FIN_STAMP(3);
+    if (ok) {
+        // ---- exact argmax of fl(w_un / s): the first block whose rescaled max ties
+        const double mval = M / s;                      // max of fl(w_un/s) = fl(max w_un / s)
+        if (tid == 0) s_min = ~0ull;
+        __syncthreads();
+        unsigned long long cb = ~0ull;
+        if (tid < nb && pm0 / s == mval) cb = (unsigned long long)tid;
+        for (int64_t b = tid + 1024; b < nb; b += 1024)
+            if (dp.pmax[b] / s == mval) cb = min(cb, (unsigned long long)b);
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) cb = min(cb, (unsigned long long)__shfl_xor((long long)cb, d, 64));
+        if (lane == 0) atomicMin(&s_min, cb);
+        __syncthreads();
+        const int64_t bc = (int64_t)s_min;
+        __syncthreads();
+        if (tid == 0) s_min = ~0ull;
+        __syncthreads();
+        if (tid < kPartPer) {
+            const int64_t i = bc * kPartPer + tid;
+            unsigned long long hit = (i < n && norm_w(w_un[i], s, np_recip) == mval)
+                                         ? (unsigned long long)i : ~0ull;
+#pragma unroll
+            for (int d = 1; d < 64; d <<= 1)
+                hit = min(hit, (unsigned long long)__shfl_xor((long long)hit, d, 64));
+            if (lane == 0) atomicMin(&s_min, hit);
+        }
+        __syncthreads();
+        if (tid == 0) {
+            const double f = M / s;                      // back from max-relative to w_un / s
+            tot.maxv = mval;
+            tot.maxi = (int64_t)s_min;
+            tot.sw *= f;
+            tot.sw2 *= f * f;
+            for (int j = 0; j < 3; ++j) tot.m1[j] *= f;
+            for (int j = 0; j < 6; ++j) tot.m2[j] *= f;
+        }
+    }
+    if (tid == 0) {
+        const int32_t st = io.ctr[0];
+    FIN_STAMP(4);
+        write_result(tot, xs, ys, ts, 0, refp, s, flags, ess_th, io.res + st, resampled_known);
+        want_scan = flags[kFlagResample];
+        io.ctr[0] = st + 1;
+        io.ctr[1] = io.ctr[1] + 1;
+        *s_cur = s;
+    }
+    __syncthreads();
+    FIN_STAMP(5);
+    if (want_scan) {
+        // 256-block totals of w for the next step's exact cumsum (S1)
+        auto btot = [&](int64_t b) {
+            if (ok) return (dp.pmax[b] / s) * dp.ps[0][b];
+            double v = 0.0;
+            const int64_t e = (b + 1) * kPartPer < n ? (b + 1) * kPartPer : n;
+            for (int64_t i = b * kPartPer; i < e; ++i) v += norm_w(w_un[i], s, np_recip);
+            return v;
+        };
+        const int per = (int)((nb + 1023) / 1024);
+        const int64_t b0 = (int64_t)tid * per;
+        double loc = 0.0;
+        for (int k = 0; k < per; ++k)
+            if (b0 + k < nb) loc += btot(b0 + k);
+        double total;
+        double ex = block_excl_scan<double, 1024>(loc, sh, total);
+        for (int k = 0; k < per; ++k)
+            if (b0 + k < nb) {
+                boff[b0 + k] = ex;
+                ex = ex + btot(b0 + k);
+            }
+        if (tid == 0) boff[nb] = total;
+    }
+}
+
+// w = w_un / s (NaN -> 1/NP): materialise the current weights (get_state, np.sum)
+__global__ __launch_bounds__(256) void normalize_only_kernel(const int64_t n,
+                                                             const double* __restrict__ w_un,
+                                                             const double* __restrict__ s,
+                                                             const double np_recip,
+                                                             double* __restrict__ w) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) w[i] = norm_w(w_un[i], *s, np_recip);
+}
+
+// S1 of the deferred path: 256-block totals of w = w_un / s and their prefix.
+__global__ __launch_bounds__(kPartPer) void scan_bsum256_kernel(
+    const double* __restrict__ w_un, const double* __restrict__ s_in, const double np_recip,
+    const int64_t n, double* __restrict__ bsum, double* __restrict__ boff,
+    unsigned* __restrict__ counter) {
+    __shared__ double sh[kPartPer / 64 + 1];
+    const int64_t i = (int64_t)blockIdx.x * kPartPer + threadIdx.x;
+    const double v = (i < n) ? norm_w(w_un[i], *s_in, np_recip) : 0.0;
+    double tot;
+    block_excl_scan<double, kPartPer>(v, sh, tot);
+    if (threadIdx.x == 0) st_wt_d(&bsum[blockIdx.x], tot);
+    if (!arrive_last(counter)) return;
+    block_scan_array<double, kPartPer>(bsum, boff, gridDim.x, boff + gridDim.x, sh);
+}
+
 // ====================================================================
 // exact sequential cumsum (np.cumsum, particle_filter.py:212)
 // ====================================================================
@@ -648,6 +1139,12 @@ __global__ __launch_bounds__(kNormThreads) void scan_bsum_kernel(
     block_scan_array<double, kNormThreads>(bsum, boff, gridDim.x, boff + gridDim.x, sh);
 }
 
+// the weight an exact-cumsum pass reads: w itself, or w_un / s on the deferred path
+__device__ __forceinline__ double scan_w(const double* __restrict__ w, const int64_t i,
+                                         const double* __restrict__ s_div, const double np_recip) {
+    return s_div ? norm_w(w[i], *s_div, np_recip) : w[i];
+}
+
 // S3: classify every element; k_i = increment on the run's ulp grid.  The last
 // block scans the per-block special counts and increment sums.
 // base_off: approximate cumsum before local element 0 (other ranks' weight).
@@ -658,7 +1155,8 @@ __global__ __launch_bounds__(kScanThreads) void scan_classify_kernel(
     int32_t* __restrict__ bf, uint64_t* __restrict__ boffk, int32_t* __restrict__ bofff,
     uint64_t* __restrict__ ktot, int32_t* __restrict__ nspec, const double delta,
     const int64_t gbase, unsigned* __restrict__ counter, const int32_t* __restrict__ flags,
-    const int32_t force) {
+    const int32_t force, const double* __restrict__ s_div, const double np_recip,
+    const int32_t gran) {
     if (!force && flags[kFlagResample] != 1) return;
     __shared__ double shd[kScanThreads / 64 + 1];
     __shared__ uint64_t shk[kScanThreads / 64 + 1];
@@ -668,12 +1166,12 @@ __global__ __launch_bounds__(kScanThreads) void scan_classify_kernel(
     double loc = 0.0;
 #pragma unroll
     for (int k = 0; k < kScanPer; ++k) {
-        v[k] = (base + k < n) ? w[base + k] : 0.0;
+        v[k] = (base + k < n) ? scan_w(w, base + k, s_div, np_recip) : 0.0;
         loc += v[k];
     }
     double dtot;
     double run = block_excl_scan<double, kScanThreads>(loc, shd, dtot) +
-                 boff[(int64_t)blockIdx.x * (kScanBlock / kNormPer)] +
+                 boff[(int64_t)blockIdx.x * (kScanBlock / gran)] +
                  (base_off ? *base_off : 0.0);
     uint64_t kk[kScanPer];
     int32_t ff[kScanPer];
@@ -734,7 +1232,8 @@ __global__ __launch_bounds__(kScanThreads) void scan_classify_kernel(
 __device__ void serial_fold(const SpecialIn* __restrict__ spec, SpecialOut* __restrict__ out,
                             const int32_t M, const uint64_t ktot, const int64_t n_total,
                             int32_t* __restrict__ flags, const double* __restrict__ w,
-                            double* __restrict__ c, const int64_t n_local, const bool wt_loads) {
+                            double* __restrict__ c, const int64_t n_local, const bool wt_loads,
+                            const double* __restrict__ s_div, const double np_recip) {
     __shared__ SpecialIn tile[257];
     __shared__ int bad;
     double s = 0.0;
@@ -779,7 +1278,7 @@ __device__ void serial_fold(const SpecialIn* __restrict__ spec, SpecialOut* __re
         flags[kFlagFallback] = 1;
         double r = 0.0;
         for (int64_t i = 0; i < n_local; ++i) {
-            r = r + w[i];
+            r = r + scan_w(w, i, s_div, np_recip);
             c[i] = r;
         }
     } else if (threadIdx.x == 0) {
@@ -797,7 +1296,8 @@ __global__ __launch_bounds__(kScanThreads) void scan_emit_kernel(
     SpecialIn* __restrict__ spec, const int64_t gbase, SpecialOut* __restrict__ spec_out,
     const int32_t* __restrict__ nspec_p, const uint64_t* __restrict__ ktot_p,
     const int32_t do_fold, double* __restrict__ c, unsigned* __restrict__ counter,
-    int32_t* __restrict__ flags, const int32_t force) {
+    int32_t* __restrict__ flags, const int32_t force, const double* __restrict__ s_div,
+    const double np_recip) {
     if (!force && flags[kFlagResample] != 1) return;
     const int64_t base = (int64_t)blockIdx.x * kScanBlock + threadIdx.x * kScanPer;
     for (int k = 0; k < kScanPer; ++k) {
@@ -809,7 +1309,7 @@ __global__ __launch_bounds__(kScanThreads) void scan_emit_kernel(
             SpecialIn s;
             s.idx = gbase + i;
             s.P = boffk[blockIdx.x] + kincl[i];
-            s.w = w[i];
+            s.w = scan_w(w, i, s_div, np_recip);
             s.E = sum_binade(approx[i]);
             s.pad = 0;
             st_wt_struct(&spec[m], s);
@@ -817,7 +1317,7 @@ __global__ __launch_bounds__(kScanThreads) void scan_emit_kernel(
     }
     if (!do_fold) return;
     if (!arrive_last(counter)) return;
-    serial_fold(spec, spec_out, *nspec_p, *ktot_p, n, flags, w, c, n, true);
+    serial_fold(spec, spec_out, *nspec_p, *ktot_p, n, flags, w, c, n, true, s_div, np_recip);
 }
 
 // S6 stand-alone (multi-GPU: over the gathered global list)
@@ -825,7 +1325,7 @@ __global__ __launch_bounds__(256) void scan_fold_kernel(
     const SpecialIn* __restrict__ spec, SpecialOut* __restrict__ out, const int32_t* __restrict__ M,
     const uint64_t* __restrict__ ktot, const int64_t n_total, int32_t* __restrict__ flags,
     const double* __restrict__ w, double* __restrict__ c, const int64_t n_local) {
-    serial_fold(spec, out, *M, *ktot, n_total, flags, w, c, n_local, false);
+    serial_fold(spec, out, *M, *ktot, n_total, flags, w, c, n_local, false, nullptr, 0.0);
 }
 
 // S7: expand the exact cumsum from the specials.  spec_base / k_base: global

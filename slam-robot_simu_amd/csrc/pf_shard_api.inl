@@ -69,11 +69,12 @@ int slam_pf_shard_classify(slam_pf* h, const double* d_totals, int32_t rank, int
     shard_prefix_kernel<<<1, 64, 0, s>>>(d_totals, rank, h->sh.base_off);
     scan_classify_kernel<<<nb, kScanThreads, 0, s>>>(
         h->w, h->n, h->boff, h->sh.base_off, h->c, h->kincl, h->fexcl, h->bk, h->bf, h->boffk,
-        h->bofff, h->ktot, h->nspec, delta, h->gbase, h->tk + 2 * kTicketWords, h->flags, 1);
+        h->bofff, h->ktot, h->nspec, delta, h->gbase, h->tk + 2 * kTicketWords, h->flags, 1,
+        nullptr, h->pc.np_recip, kNormPer);
     scan_emit_kernel<<<nb, kScanThreads, 0, s>>>(h->w, h->n, h->c, h->kincl, h->fexcl, h->boffk,
                                                  h->bofff, h->spec_in, h->gbase, h->spec_out,
                                                  h->nspec, h->ktot, 0, h->c, h->tk + 2 * kTicketWords,
-                                                 h->flags, 1);
+                                                 h->flags, 1, nullptr, h->pc.np_recip);
     shard_meta_kernel<<<1, 64, 0, s>>>(h->nspec, h->ktot, d_meta);
     SLAM_HIP_TRY(hipGetLastError());
     return SLAM_OK;

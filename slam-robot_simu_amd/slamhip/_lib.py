@@ -10,7 +10,9 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libslam_hip.so")
+# SLAM_HIP_LIB: an alternative in-tree build (kernel variant experiments); the
+# product path is always this library, and a missing library raises.
+LIB_PATH = os.environ.get("SLAM_HIP_LIB", os.path.join(_HERE, "libslam_hip.so"))
 
 SLAM_OK = 0
 SLAM_ERR_ARG = -1
