@@ -84,6 +84,26 @@ __device__ __forceinline__ void normal2(u32x4 r, double& n0, double& n1) {
     n1 = rad * s;
 }
 
+// Four standard normals from ONE Philox block: two Box-Muller pairs on 32-bit
+// uniforms in (0, 1] (radius resolution 2^-32: |g| <= 6.66, a tail mass of
+// 3e-11 per draw).  Half the Philox work of 53-bit uniforms; the per-step
+// motion noise needs three normals per particle.
+__device__ __forceinline__ void normal4(u32x4 r, double& n0, double& n1, double& n2, double& n3) {
+    const double u1 = ((double)r.x + 1.0) * 0x1p-32;
+    const double u2 = ((double)r.y + 1.0) * 0x1p-32;
+    const double u3 = ((double)r.z + 1.0) * 0x1p-32;
+    const double u4 = ((double)r.w + 1.0) * 0x1p-32;
+    const double ra = sqrt(-2.0 * log(u1));
+    const double rb = sqrt(-2.0 * log(u3));
+    double s, c;
+    sincospi(2.0 * u2, &s, &c);
+    n0 = ra * c;
+    n1 = ra * s;
+    sincospi(2.0 * u4, &s, &c);
+    n2 = rb * c;
+    n3 = rb * s;
+}
+
 // RNG stream ids (counter word z)
 enum : uint32_t { kStreamPredict = 1, kStreamResample = 2 };
 

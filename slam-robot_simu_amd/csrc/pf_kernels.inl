@@ -328,14 +328,12 @@ __device__ __forceinline__ void particle_update(
         g1 = noise[3 * i + 1];
         g2 = noise[3 * i + 2];
     } else {
+        // one Philox block per particle and step: counter (global index, stream, RNG step)
         const uint64_t gi = (uint64_t)(pc.gbase + i);
         const u32x4 c0{(uint32_t)gi, (uint32_t)(gi >> 32), kStreamPredict, rstep};
         const u32x4 r0 = philox4x32(c0, (uint32_t)seed, (uint32_t)(seed >> 32));
-        const u32x4 c1{(uint32_t)gi, (uint32_t)(gi >> 32), kStreamPredict | 0x100u, rstep};
-        const u32x4 r1 = philox4x32(c1, (uint32_t)seed, (uint32_t)(seed >> 32));
         double h0, h1, h2, h3;
-        normal2(r0, h0, h1);
-        normal2(r1, h2, h3);
+        normal4(r0, h0, h1, h2, h3);
         if (MOTION == SLAM_MOTION_LINEAR) {   // noise_j = sum_k g_k q[k][j]
             g0 = h0 * pc.q[0] + h1 * pc.q[3] + h2 * pc.q[6];
             g1 = h0 * pc.q[1] + h1 * pc.q[4] + h2 * pc.q[7];
