@@ -66,6 +66,7 @@ struct slam_pf {
     uint64_t *bk = nullptr, *boffk = nullptr, *ktot = nullptr;
     int32_t *bf = nullptr, *bofff = nullptr, *nspec = nullptr;
     SpecialIn* spec_in = nullptr;
+    SpecialIn* stage = nullptr;     // lean exact cumsum: per-tile staged specials
     SpecialOut* spec_out = nullptr;
     // reductions
     int32_t nchunks = 0;
@@ -263,6 +264,20 @@ int launch_scans(slam_pf* h, int32_t force, bool with_s1) {
         const int rc = launch_bsum(h);
         if (rc) return rc;
     }
+    if (h->deferred) {
+        unsigned* tk = h->tk + 2 * kTicketWords;
+        scan_lean_classify_kernel<<<nb, kScanThreads, 0, s>>>(
+            h->w_un, h->s_cur, h->pc.np_recip, n, h->boff, delta, h->stage, h->bk, h->bf, h->boffk,
+            h->bofff, h->ktot, h->nspec, tk, h->flags, force);
+        scan_lean_place_kernel<<<nb, kScanThreads, 0, s>>>(
+            h->stage, h->bf, h->boffk, h->bofff, h->spec_in, h->spec_out, h->nspec, h->ktot, n,
+            h->flags, h->w_un, h->s_cur, h->pc.np_recip, h->c, tk, force);
+        scan_lean_expand_kernel<<<nb, kScanThreads, 0, s>>>(
+            h->w_un, h->s_cur, h->pc.np_recip, n, h->boff, delta, h->boffk, h->bofff, h->spec_out,
+            h->c, h->flags, force);
+        SLAM_HIP_TRY(hipGetLastError());
+        return SLAM_OK;
+    }
     const double* w = h->deferred ? h->w_un : h->w;
     const double* sd = h->deferred ? h->s_cur : nullptr;
     const int32_t gran = h->deferred ? kPartPer : kNormPer;
@@ -452,6 +467,7 @@ int create_impl(const slam_pf_config* cfg, int64_t n_local, int64_t n_global, in
     A(h->ktot, 1);
     A(h->nspec, 1);
     A(h->spec_in, n);
+    if (deferred) A(h->stage, n);
     A(h->spec_out, n);
     A(h->part, h->nchunks);
     A(h->bp, h->nb_norm);

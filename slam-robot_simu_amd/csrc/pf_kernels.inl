@@ -1355,6 +1355,193 @@ __global__ __launch_bounds__(kScanThreads) void scan_expand_kernel(
     }
 }
 
+// ====================================================================
+// Lean exact cumsum (single-GPU handles): no per-element scratch.  Pass A
+// classifies each 2048-element tile and stages its few special elements;
+// pass B places them in global order and folds them (last block); pass C
+// re-runs the identical classification and writes c.  Reads w twice,
+// writes c once: 24 B per element instead of ~60.
+// ====================================================================
+struct TileScan {
+    uint64_t kex;            // exclusive prefix of the tile-local increments (this lane)
+    int32_t fex;             // exclusive prefix of the tile-local special count (this lane)
+    uint64_t kk[kScanPer];   // increments of this lane's elements (0 for specials)
+    int32_t ff[kScanPer];    // special flags
+    double v[kScanPer];      // the weights
+    int E[kScanPer];         // binade of the approximate prefix after the element
+};
+
+// Tile b of the weights w = w_un / s: lane t owns elements 8t .. 8t+7 (read
+// through a padded LDS transpose so the global loads stay coalesced).
+__device__ __forceinline__ void tile_classify(const double* __restrict__ w_un,
+                                              const double s, const double np_recip,
+                                              const int64_t n, const int64_t b,
+                                              const double off, const double delta,
+                                              double* sv, double* shd, uint64_t* shk,
+                                              int32_t* shf, TileScan& ts, uint64_t& ktile,
+                                              int32_t& ftile) {
+    const int t = threadIdx.x;
+    const int64_t base = b * kScanBlock;
+#pragma unroll
+    for (int k = 0; k < kScanPer; ++k) {
+        const int e = t + kScanThreads * k;
+        const int64_t i = base + e;
+        sv[e + (e >> 3)] = (i < n) ? norm_w(w_un[i], s, np_recip) : 0.0;
+    }
+    __syncthreads();
+    double loc = 0.0;
+#pragma unroll
+    for (int k = 0; k < kScanPer; ++k) {
+        ts.v[k] = sv[9 * t + k];
+        loc += ts.v[k];
+    }
+    double dtot;
+    double run = block_excl_scan<double, kScanThreads>(loc, shd, dtot) + off;
+    uint64_t ksum = 0;
+    int32_t fsum = 0;
+#pragma unroll
+    for (int k = 0; k < kScanPer; ++k) {
+        const double prev = run;
+        run = run + ts.v[k];
+        const int64_t gi = base + 8 * t + k;
+        bool reg = (gi != 0) && (gi < n);
+        uint64_t inc = 0;
+        const int E = sum_binade(run);
+        if (reg) {
+            reg = (sum_binade(prev) == E);
+            if (reg && E != -1022) reg = prev >= ldexp(1.0, E) * (1.0 + delta);
+            if (reg) reg = run <= ldexp(1.0, E + 1) * (1.0 - delta);
+            if (reg) {
+                const double tt = ldexp(ts.v[k], 52 - E);
+                const double fl = floor(tt);
+                reg = (tt - fl) != 0.5;
+                inc = (uint64_t)rint(tt);
+            }
+        }
+        ts.kk[k] = reg ? inc : 0;
+        ts.ff[k] = (reg || gi >= n) ? 0 : 1;
+        ts.E[k] = E;
+        ksum += ts.kk[k];
+        fsum += ts.ff[k];
+    }
+    ts.kex = block_excl_scan<uint64_t, kScanThreads>(ksum, shk, ktile);
+    ts.fex = block_excl_scan<int32_t, kScanThreads>(fsum, shf, ftile);
+}
+
+// Pass A: classify, stage the tile's specials (local P), tile totals; the
+// last block scans the totals (boffk, bofff, ktot, nspec).
+__global__ __launch_bounds__(kScanThreads) void scan_lean_classify_kernel(
+    const double* __restrict__ w_un, const double* __restrict__ s_in, const double np_recip,
+    const int64_t n, const double* __restrict__ boff, const double delta,
+    SpecialIn* __restrict__ stage, uint64_t* __restrict__ bk, int32_t* __restrict__ bf,
+    uint64_t* __restrict__ boffk, int32_t* __restrict__ bofff, uint64_t* __restrict__ ktot,
+    int32_t* __restrict__ nspec, unsigned* __restrict__ counter,
+    const int32_t* __restrict__ flags, const int32_t force) {
+    if (!force && flags[kFlagResample] != 1) return;
+    __shared__ double sv[kScanBlock + kScanBlock / 8];
+    __shared__ double shd[kScanThreads / 64 + 1];
+    __shared__ uint64_t shk[kScanThreads / 64 + 1];
+    __shared__ int32_t shf[kScanThreads / 64 + 1];
+    const int64_t b = blockIdx.x;
+    TileScan ts;
+    uint64_t ktile;
+    int32_t ftile;
+    tile_classify(w_un, *s_in, np_recip, n, b, boff[b * (kScanBlock / kPartPer)], delta, sv, shd,
+                  shk, shf, ts, ktile, ftile);
+    uint64_t kex = ts.kex;
+    int32_t fex = ts.fex;
+#pragma unroll
+    for (int k = 0; k < kScanPer; ++k) {
+        kex += ts.kk[k];
+        if (ts.ff[k]) {
+            SpecialIn r;
+            r.idx = b * kScanBlock + 8 * threadIdx.x + k;
+            r.P = kex;                                  // tile-local inclusive prefix
+            r.w = ts.v[k];
+            r.E = ts.E[k];
+            r.pad = 0;
+            stage[b * kScanBlock + fex] = r;
+            ++fex;
+        }
+    }
+    if (threadIdx.x == 0) {
+        st_wt(&bk[b], ktile);
+        st_wt_i(&bf[b], ftile);
+    }
+    if (!arrive_last(counter)) return;
+    block_scan_array<uint64_t, kScanThreads>(bk, boffk, gridDim.x, ktot, shk);
+    __syncthreads();
+    block_scan_array<int32_t, kScanThreads>(bf, bofff, gridDim.x, nspec, shf);
+}
+
+// Pass B: staged specials to their global slots (P made global); the last
+// block folds them in order.
+__global__ __launch_bounds__(kScanThreads) void scan_lean_place_kernel(
+    const SpecialIn* __restrict__ stage, const int32_t* __restrict__ bf,
+    const uint64_t* __restrict__ boffk, const int32_t* __restrict__ bofff,
+    SpecialIn* __restrict__ spec, SpecialOut* __restrict__ spec_out,
+    const int32_t* __restrict__ nspec_p, const uint64_t* __restrict__ ktot_p, const int64_t n,
+    int32_t* __restrict__ flags, const double* __restrict__ w_un,
+    const double* __restrict__ s_in, const double np_recip, double* __restrict__ c,
+    unsigned* __restrict__ counter, const int32_t force) {
+    if (!force && flags[kFlagResample] != 1) return;
+    const int64_t b = blockIdx.x;
+    const int32_t cnt = bf[b];
+    for (int j = threadIdx.x; j < cnt; j += blockDim.x) {
+        SpecialIn r = stage[b * kScanBlock + j];
+        r.P += boffk[b];
+        st_wt_struct(&spec[bofff[b] + j], r);
+    }
+    if (!arrive_last(counter)) return;
+    serial_fold(spec, spec_out, *nspec_p, *ktot_p, n, flags, w_un, c, n, true, s_in, np_recip);
+}
+
+// Pass C: identical classification, then every c_i from the specials.
+__global__ __launch_bounds__(kScanThreads) void scan_lean_expand_kernel(
+    const double* __restrict__ w_un, const double* __restrict__ s_in, const double np_recip,
+    const int64_t n, const double* __restrict__ boff, const double delta,
+    const uint64_t* __restrict__ boffk, const int32_t* __restrict__ bofff,
+    const SpecialOut* __restrict__ so, double* __restrict__ c, const int32_t* __restrict__ flags,
+    const int32_t force) {
+    if (!force && flags[kFlagResample] != 1) return;
+    if (flags[kFlagFallback]) return;
+    __shared__ double sv[kScanBlock + kScanBlock / 8];
+    __shared__ double shd[kScanThreads / 64 + 1];
+    __shared__ uint64_t shk[kScanThreads / 64 + 1];
+    __shared__ int32_t shf[kScanThreads / 64 + 1];
+    const int64_t b = blockIdx.x;
+    TileScan ts;
+    uint64_t ktile;
+    int32_t ftile;
+    tile_classify(w_un, *s_in, np_recip, n, b, boff[b * (kScanBlock / kPartPer)], delta, sv, shd,
+                  shk, shf, ts, ktile, ftile);
+    uint64_t kin = boffk[b] + ts.kex;
+    int32_t m = bofff[b] + ts.fex;
+    double out[kScanPer];
+#pragma unroll
+    for (int k = 0; k < kScanPer; ++k) {
+        kin += ts.kk[k];
+        if (ts.ff[k]) {
+            out[k] = so[m].cs;
+            ++m;
+        } else {
+            const SpecialOut& p = so[m - 1];
+            out[k] = p.cs + (double)(kin - p.P) * ldexp(1.0, p.E - 52);
+        }
+    }
+    // back through the padded LDS tile so the global stores are coalesced
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kScanPer; ++k) sv[9 * threadIdx.x + k] = out[k];
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kScanPer; ++k) {
+        const int e = threadIdx.x + kScanThreads * k;
+        const int64_t i = b * kScanBlock + e;
+        if (i < n) c[i] = sv[e + (e >> 3)];
+    }
+}
+
 // gather for the stand-alone resampling stage (particle_filter.py:216-222)
 __global__ __launch_bounds__(256) void gather_kernel(
     const int64_t n, const int32_t* __restrict__ idx, const double* __restrict__ xs,
