@@ -11,6 +11,7 @@
 #include <string>
 
 #include "../../include/slam_hip.h"
+#include "fastmath.hpp"
 
 namespace slam {
 
@@ -84,24 +85,24 @@ __device__ __forceinline__ void normal2(u32x4 r, double& n0, double& n1) {
     n1 = rad * s;
 }
 
-// Four standard normals from ONE Philox block: two Box-Muller pairs on 32-bit
+// Three standard normals from ONE Philox block: two Box-Muller pairs on 32-bit
 // uniforms in (0, 1] (radius resolution 2^-32: |g| <= 6.66, a tail mass of
-// 3e-11 per draw).  Half the Philox work of 53-bit uniforms; the per-step
-// motion noise needs three normals per particle.
-__device__ __forceinline__ void normal4(u32x4 r, double& n0, double& n1, double& n2, double& n3) {
-    const double u1 = ((double)r.x + 1.0) * 0x1p-32;
+// 3e-11 per draw); the fourth normal of the block is not formed.  Half the
+// Philox work of 53-bit uniforms; the per-step motion noise needs three
+// normals per particle.  log and sin/cos from fastmath.hpp (< 2 ulp).
+__device__ __forceinline__ void normal3(u32x4 r, double& n0, double& n1, double& n2) {
+    const double d1 = (double)r.x + 1.0;                 // u = d 2^-32, exact
     const double u2 = ((double)r.y + 1.0) * 0x1p-32;
-    const double u3 = ((double)r.z + 1.0) * 0x1p-32;
+    const double d3 = (double)r.z + 1.0;
     const double u4 = ((double)r.w + 1.0) * 0x1p-32;
-    const double ra = sqrt(-2.0 * log(u1));
-    const double rb = sqrt(-2.0 * log(u3));
+    const double ra = sqrt(-2.0 * rng_log_scaled(d1, -32));
+    const double rb = sqrt(-2.0 * rng_log_scaled(d3, -32));
     double s, c;
-    sincospi(2.0 * u2, &s, &c);
+    rng_sincos2pi(u2, &s, &c);
     n0 = ra * c;
     n1 = ra * s;
-    sincospi(2.0 * u4, &s, &c);
+    rng_sincos2pi(u4, &s, &c);
     n2 = rb * c;
-    n3 = rb * s;
 }
 
 // RNG stream ids (counter word z)

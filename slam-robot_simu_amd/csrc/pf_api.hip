@@ -348,7 +348,7 @@ int launch_reduce(slam_pf* h, int32_t resampled_known) {
     const int c = h->cur;
     tic(h, 1);
     if (h->deferred) {
-        finalize_deferred_kernel<<<1, 1024, 0, s>>>(
+        finalize_deferred_kernel<<<1, kFinThreads, 0, s>>>(
             n, h->dp, h->w_un, h->s_cur, h->tail_leaves, h->tail_ops, h->n_tail_leaves,
             h->n_tail_ops, h->x[c], h->y[c], h->th[c], h->refp, h->flags, h->cfg.ess_threshold,
             step_io(h), resampled_known, h->pc.np_recip, h->boff);
@@ -458,6 +458,8 @@ int create_impl(const slam_pf_config* cfg, int64_t n_local, int64_t n_global, in
     A(h->s_cur, 1);
     A(h->dp.pmax, h->nb_part);
     A(h->dp.pidx, h->nb_part);
+    A(h->dp.ppre, h->nb_part);
+    for (int q = 0; q < 3; ++q) A(h->dp.pxe[q], h->nb_part);
     for (int q = 0; q < 11; ++q) A(h->dp.ps[q], h->nb_part);
     A(h->dp.leaf, (size_t)(kPartPer / 128) * h->nb_part);
     A(h->bk, h->nb_scan);

@@ -19,13 +19,18 @@ constexpr int kDeferPPT = SLAM_DEFER_PPT;            // particles per lane, defe
 constexpr int kPartPer = 256 * kDeferPPT;            // particles per fused block (deferred path)
 
 // Deferred normalisation (single-GPU handles): the fused kernel leaves, per
-// 512-particle block, its max unnormalised weight M_b with the first index,
+// kPartPer-particle block, its max unnormalised weight M_b with the first index,
 // sums scaled by 1/M_b (sum u, sum u^2, sum u d, sum u d d^T with u = w_un/M_b
 // and d = particle - refp; scaling keeps squares of tiny likelihoods out of
 // the subnormal range) and its four 128-element np.sum leaf sums.
+// Per block also: the largest w_un before the first max (-1 if none), so
+// the step end knows without a rescan whether a smaller weight can round to
+// the same normalised maximum, and the particle at the first max (x_est).
 struct DeferParts {
     double* pmax;
     int64_t* pidx;
+    double* ppre;           // max w_un at indices before pidx (-1: none)
+    double* pxe[3];         // particle (x, y, th) at pidx
     double* ps[11];         // sw, sw2, m1[3], m2[6]
     double* leaf;           // [(kPartPer / 128) * blocks]
 };

@@ -183,7 +183,7 @@ __device__ void defer_epilogue(const int64_t base, const int64_t n, const double
     __shared__ double s_q[6 * 256];
     __shared__ double s_seg[6 * 16];
     __shared__ double s_acc[64];
-    __shared__ double s_mv[4];
+    __shared__ double s_mv[4], s_pre[4];
     __shared__ int64_t s_mi[4];
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
     // lane max and its first particle, then the block max
@@ -242,6 +242,24 @@ __device__ void defer_epilogue(const int64_t base, const int64_t n, const double
 #pragma unroll
     for (int j = 0; j < 5; ++j) s_q[j * 256 + t] = q[j];
     __syncthreads();
+    // the block's first max index; the largest weight before it; x_est candidate
+    int64_t bi = s_mi[0];
+#pragma unroll
+    for (int w = 1; w < 4; ++w) bi = s_mi[w] < bi ? s_mi[w] : bi;
+    double pre = -1.0;
+#pragma unroll
+    for (int k = 0; k < kDeferPPT; ++k) {
+        const int64_t i = base + t + 256 * k;
+        if (i < bi) pre = fmax(pre, wv[k]);
+        if (i == bi) {
+            dp.pxe[0][blk] = xv[k];
+            dp.pxe[1][blk] = yv[k];
+            dp.pxe[2][blk] = tv[k];
+        }
+    }
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) pre = fmax(pre, __shfl_xor(pre, d, 64));
+    if (lane == 0) s_pre[wave] = pre;
     if (t < 5 * 16) {
         const double* a = s_q + (t >> 4) * 256 + (t & 15);
         double acc = a[0];
@@ -265,10 +283,9 @@ __device__ void defer_epilogue(const int64_t base, const int64_t n, const double
         const double* r = s_acc + 8 * (t - 64);
         dp.leaf[kLeaves * blk + (t - 64)] = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
     } else if (t == 128) {
-        int64_t bi = s_mi[0];
-        for (int w = 1; w < 4; ++w) bi = s_mi[w] < bi ? s_mi[w] : bi;
         dp.pmax[blk] = M;
         dp.pidx[blk] = bi;
+        dp.ppre[blk] = fmax(fmax(s_pre[0], s_pre[1]), fmax(s_pre[2], s_pre[3]));
     }
     __syncthreads();
     // round 2: m2[6]
@@ -290,19 +307,17 @@ __device__ void defer_epilogue(const int64_t base, const int64_t n, const double
     }
 }
 
-// One particle of the fused step: [resample gather +] predict + likelihood
-// (particle_filter.py:156-198, :216-222; motion_model.py:31-62).  Stores the
-// predicted particle and w_un = pw * likelihood when `store`.
-template <int MOTION, int LIK, bool HOSTNOISE>
-__device__ __forceinline__ void particle_update(
+// One particle of the fused step: [resample gather +] predict
+// (particle_filter.py:156-168, :216-222; motion_model.py:31-62).  Stores the
+// predicted particle when `store`.
+template <int MOTION, bool HOSTNOISE>
+__device__ __forceinline__ void particle_predict(
     const int64_t i, const bool store, const int64_t n, const int32_t st, const uint32_t rstep,
-    const int32_t rflag, const double pw_prev, const double* __restrict__ xs,
-    const double* __restrict__ ys, const double* __restrict__ ts, double* __restrict__ xo,
-    double* __restrict__ yo, double* __restrict__ to, double* __restrict__ w_un,
-    const double* __restrict__ c, int32_t* __restrict__ flags, const double* __restrict__ noise,
-    const double* __restrict__ lm, const double* __restrict__ zs, const StepIO& io,
-    const PredictConst& pc, const LikConst& lc, const uint64_t seed, double& xn, double& yn,
-    double& tn, double& wv) {
+    const int32_t rflag, const double* __restrict__ xs, const double* __restrict__ ys,
+    const double* __restrict__ ts, double* __restrict__ xo, double* __restrict__ yo,
+    double* __restrict__ to, const double* __restrict__ c, int32_t* __restrict__ flags,
+    const double* __restrict__ noise, const StepIO& io, const PredictConst& pc,
+    const uint64_t seed, double& xn, double& yn, double& tn) {
     // ---- resample gather (1: search the exact cumsum here; 2: already gathered)
     int64_t src = i;
     if (rflag == 1) {
@@ -314,7 +329,6 @@ __device__ __forceinline__ void particle_update(
             if (store) atomicOr(&flags[kFlagStatus], 1);
         }
     }
-    const double pw = rflag ? pc.np_recip : pw_prev;             // particle_filter.py:222
     const double x = xs[src], y = ys[src], th = ts[src];
 
     // ---- control of this step (particle_filter.py:46-58 / motion_model.py:40-45)
@@ -332,8 +346,8 @@ __device__ __forceinline__ void particle_update(
         const uint64_t gi = (uint64_t)(pc.gbase + i);
         const u32x4 c0{(uint32_t)gi, (uint32_t)(gi >> 32), kStreamPredict, rstep};
         const u32x4 r0 = philox4x32(c0, (uint32_t)seed, (uint32_t)(seed >> 32));
-        double h0, h1, h2, h3;
-        normal4(r0, h0, h1, h2, h3);
+        double h0, h1, h2;
+        normal3(r0, h0, h1, h2);
         if (MOTION == SLAM_MOTION_LINEAR) {   // noise_j = sum_k g_k q[k][j]
             g0 = h0 * pc.q[0] + h1 * pc.q[3] + h2 * pc.q[6];
             g1 = h0 * pc.q[1] + h1 * pc.q[4] + h2 * pc.q[7];
@@ -352,8 +366,10 @@ __device__ __forceinline__ void particle_update(
         tn = th;
     } else if (MOTION == SLAM_MOTION_LINEAR) {
         // particle_filter.py:129-140 then + v (:166); A = I, B = diag(V, V, w)
-        const double a = pc.dt * cos(th);
-        const double b = pc.dt * sin(th);
+        double sn, cs;
+        fast_sincos(th, &sn, &cs);
+        const double a = pc.dt * cs;
+        const double b = pc.dt * sn;
         xn = (x + v * a) + g0;
         yn = (y + v * b) + g1;
         tn = wrap_angle(th + om * pc.dt) + g2;
@@ -369,8 +385,8 @@ __device__ __forceinline__ void particle_update(
         const double a = vh / wh;
         const double b = wh * pc.dt;
         double s0, c0, s1, c1;
-        sincos(th, &s0, &c0);
-        sincos(th + b, &s1, &c1);
+        fast_sincos(th, &s0, &c0);
+        fast_sincos(th + b, &s1, &c1);
         xn = (x - (a * s0)) + (a * s1);
         yn = (y + (a * c0)) - (a * c1);
         tn = wrap_angle(th + (wh + gh) * pc.dt);
@@ -380,72 +396,101 @@ __device__ __forceinline__ void particle_update(
         yo[i] = yn;
         to[i] = tn;
     }
+}
 
-    // ---- likelihood: world2robot (mylib/transform.py:31-35) per landmark
+// Likelihood of P particles of one lane (particle_filter.py:170-192 with
+// mylib/transform.py:31-35 per landmark).  The landmark loop is shared: each
+// landmark and observation is loaded once (scalar loads, uniform across the
+// wave) and applied to the P particles, whose accumulators are independent
+// dependency chains.
+template <int LIK, int P>
+__device__ __forceinline__ void likelihood_lanes(const double* xn, const double* yn,
+                                                 const double* tn, const double* __restrict__ lm,
+                                                 const double* __restrict__ z, const LikConst& lc,
+                                                 double* bn) {
     const int nl = lc.nl;
-    const double* __restrict__ z = zs;
-    double sp, cp;
-    sincos(kHalfPi - tn, &sp, &cp);
-    double bn;
+    double sp[P], cp[P], acc[P];
+#pragma unroll
+    for (int k = 0; k < P; ++k) fast_sincos(kHalfPi - tn[k], &sp[k], &cp[k]);
     if (LIK == SLAM_LIK_PRODUCT) {
         // particle_filter.py:185-192 factor by factor, in NumPy's rounding order
-        double acc = 1.0;
+#pragma unroll
+        for (int k = 0; k < P; ++k) acc[k] = 1.0;
         for (int j = 0; j < nl; ++j) {
-            const double dxw = lm[2 * j] - xn;
-            const double dyw = lm[2 * j + 1] - yn;
-            // OpenBLAS dgemm order for (rot @ diff.T): fma(r01, d1, r00*d0)
-            const double rx = fma(-sp, dyw, cp * dxw);
-            const double ry = fma(cp, dyw, sp * dxw);
-            const double dx = rx - z[2 * j];
-            const double dy = ry - z[2 * j + 1];
-            double q = div_refined(dx * dx, lc.sx2, lc.rsx2) + div_refined(dy * dy, lc.sy2, lc.rsy2);
-            if (lc.has_rho) q = q - ((lc.rho2 * dx) * dy) / lc.sxsy;
-            const double e = lc.has_rho ? exp((-q) / lc.d2) : exp((-q) * 0.5);  // d2 == 2 exactly
-            const double f = div_refined(e, lc.den, lc.rden);
-            acc = (j == 0) ? f : acc * f;                 // ndarray.prod: left to right
-        }
-        bn = acc;
-    } else {
-        // one exp per particle: prod_j exp(-q_j/d2)/den = exp(-sum_j q_j/d2 - NL ln den)
-        double S;
-        if (lc.iso) {
-            double acc = 0.0;
-#pragma unroll 4
-            for (int j = 0; j < nl; ++j) {
-                const double dxw = lm[2 * j] - xn;
-                const double dyw = lm[2 * j + 1] - yn;
-                const double dx = fma(cp, dxw, fma(-sp, dyw, -z[2 * j]));
-                const double dy = fma(sp, dxw, fma(cp, dyw, -z[2 * j + 1]));
-                acc = fma(dx, dx, acc);
-                acc = fma(dy, dy, acc);
+            const double lx = lm[2 * j], ly = lm[2 * j + 1], zx = z[2 * j], zy = z[2 * j + 1];
+#pragma unroll
+            for (int k = 0; k < P; ++k) {
+                const double dxw = lx - xn[k];
+                const double dyw = ly - yn[k];
+                // OpenBLAS dgemm order for (rot @ diff.T): fma(r01, d1, r00*d0)
+                const double rx = fma(-sp[k], dyw, cp[k] * dxw);
+                const double ry = fma(cp[k], dyw, sp[k] * dxw);
+                const double dx = rx - zx;
+                const double dy = ry - zy;
+                double q = div_refined(dx * dx, lc.sx2, lc.rsx2) + div_refined(dy * dy, lc.sy2, lc.rsy2);
+                if (lc.has_rho) q = q - ((lc.rho2 * dx) * dy) / lc.sxsy;
+                const double e = lc.has_rho ? exp((-q) / lc.d2) : exp((-q) * 0.5);  // d2 == 2 exactly
+                const double f = div_refined(e, lc.den, lc.rden);
+                acc[k] = acc[k] * f;                        // ndarray.prod: left to right (1*f = f)
             }
-            S = acc * lc.rsx2;
-        } else {
-            double acc = 0.0;
-#pragma unroll 2
-            for (int j = 0; j < nl; ++j) {
-                const double dxw = lm[2 * j] - xn;
-                const double dyw = lm[2 * j + 1] - yn;
-                const double dx = fma(cp, dxw, fma(-sp, dyw, -z[2 * j]));
-                const double dy = fma(sp, dxw, fma(cp, dyw, -z[2 * j + 1]));
-                double q = fma(dx * lc.rsx2, dx, (dy * lc.rsy2) * dy);
-                if (lc.has_rho) q = q - ((lc.rho2 * dx) * dy) * lc.rsxsy;
-                acc = acc + q;
-            }
-            S = acc;
         }
-        bn = exp(lc.has_rho ? fma(-S, lc.rd2, lc.neg_nl_ln_den) : fma(-0.5, S, lc.neg_nl_ln_den));
+#pragma unroll
+        for (int k = 0; k < P; ++k) bn[k] = acc[k];
+        return;
     }
-    wv = pw * bn;                                               // particle_filter.py:194
-    if (store) w_un[i] = wv;
+    // one exp per particle: prod_j exp(-q_j/d2)/den = exp(-sum_j q_j/d2 - NL ln den)
+#pragma unroll
+    for (int k = 0; k < P; ++k) acc[k] = 0.0;
+    if (lc.iso) {
+#pragma unroll 4
+        for (int j = 0; j < nl; ++j) {
+            const double lx = lm[2 * j], ly = lm[2 * j + 1], zx = z[2 * j], zy = z[2 * j + 1];
+#pragma unroll
+            for (int k = 0; k < P; ++k) {
+                const double dxw = lx - xn[k];
+                const double dyw = ly - yn[k];
+                const double dx = fma(cp[k], dxw, fma(-sp[k], dyw, -zx));
+                const double dy = fma(sp[k], dxw, fma(cp[k], dyw, -zy));
+                acc[k] = fma(dx, dx, acc[k]);
+                acc[k] = fma(dy, dy, acc[k]);
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < P; ++k)
+            bn[k] = exp(fma(-0.5, acc[k] * lc.rsx2, lc.neg_nl_ln_den));
+        return;
+    }
+    for (int j = 0; j < nl; ++j) {
+        const double lx = lm[2 * j], ly = lm[2 * j + 1], zx = z[2 * j], zy = z[2 * j + 1];
+#pragma unroll
+        for (int k = 0; k < P; ++k) {
+            const double dxw = lx - xn[k];
+            const double dyw = ly - yn[k];
+            const double dx = fma(cp[k], dxw, fma(-sp[k], dyw, -zx));
+            const double dy = fma(sp[k], dxw, fma(cp[k], dyw, -zy));
+            double q = fma(dx * lc.rsx2, dx, (dy * lc.rsy2) * dy);
+            if (lc.has_rho) q = q - ((lc.rho2 * dx) * dy) * lc.rsxsy;
+            acc[k] = acc[k] + q;
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < P; ++k)
+        bn[k] = exp(lc.has_rho ? fma(-acc[k], lc.rd2, lc.neg_nl_ln_den)
+                               : fma(-0.5, acc[k], lc.neg_nl_ln_den));
 }
 
 // The fused step kernel.  DEFER = false (shards): one particle per lane,
-// previous weights normalised in w_in.  DEFER = true (single GPU): four
-// particles per lane, previous weights = w_un / s (read and rewritten in
-// place), plus the block epilogue that replaces the normalise pass.
+// previous weights normalised in w_in.  DEFER = true (single GPU):
+// kDeferPPT particles per lane, previous weights = w_un / s (read and
+// rewritten in place), plus the block epilogue that replaces the normalise
+// pass.
+#ifdef SLAM_FUSED_WPE
+#define SLAM_FUSED_ATTR __attribute__((amdgpu_waves_per_eu(SLAM_FUSED_WPE)))
+#else
+#define SLAM_FUSED_ATTR
+#endif
 template <int MOTION, int LIK, bool HOSTNOISE, bool DEFER>
-__global__ __launch_bounds__(256) void pf_fused_kernel(
+__global__ __launch_bounds__(256) SLAM_FUSED_ATTR void pf_fused_kernel(
     const int64_t n, const double* __restrict__ xs, const double* __restrict__ ys,
     const double* __restrict__ ts, double* __restrict__ xo, double* __restrict__ yo,
     double* __restrict__ to, const double* __restrict__ w_in, double* __restrict__ w_un,
@@ -457,27 +502,35 @@ __global__ __launch_bounds__(256) void pf_fused_kernel(
     const uint32_t rstep = (uint32_t)io.ctr[1];
     const int32_t rflag = flags[kFlagResample];
     const double* __restrict__ zs = io.z + (size_t)st * 2 * (size_t)(lc.nl > 0 ? lc.nl : 1);
-    if constexpr (!DEFER) {
-        const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-        if (i >= n) return;
-        double xn, yn, tn, wv;
-        particle_update<MOTION, LIK, HOSTNOISE>(i, true, n, st, rstep, rflag, rflag ? 0.0 : w_in[i],
-                                                xs, ys, ts, xo, yo, to, w_un, c, flags, noise, lm,
-                                                zs, io, pc, lc, seed, xn, yn, tn, wv);
-    } else {
-        const int64_t base = (int64_t)blockIdx.x * kPartPer;
-        const double s_prev = *s_in;
-        double xv[kDeferPPT], yv[kDeferPPT], tv[kDeferPPT], wv[kDeferPPT];
+    constexpr int P = DEFER ? kDeferPPT : 1;
+    const int64_t base = (int64_t)blockIdx.x * (256 * P);
+    double xv[P], yv[P], tv[P], pw[P], bn[P];
+    bool valid[P];
+    int64_t idx[P];
+    const double s_prev = DEFER ? *s_in : 0.0;
 #pragma unroll
-        for (int k = 0; k < kDeferPPT; ++k) {
-            const int64_t i0 = base + threadIdx.x + 256 * k;
-            const bool valid = i0 < n;
-            const int64_t i = valid ? i0 : n - 1;
-            const double pw = rflag ? 0.0 : norm_w(w_un[i], s_prev, pc.np_recip);
-            particle_update<MOTION, LIK, HOSTNOISE>(i, valid, n, st, rstep, rflag, pw, xs, ys, ts,
-                                                    xo, yo, to, w_un, c, flags, noise, lm, zs, io,
-                                                    pc, lc, seed, xv[k], yv[k], tv[k], wv[k]);
-        }
+    for (int k = 0; k < P; ++k) {
+        const int64_t i0 = base + threadIdx.x + 256 * k;
+        valid[k] = i0 < n;
+        idx[k] = valid[k] ? i0 : n - 1;
+        // particle_filter.py:222 (a resampled step starts from 1/NP) / :235-236
+        if (rflag) pw[k] = pc.np_recip;
+        else pw[k] = DEFER ? norm_w(w_un[idx[k]], s_prev, pc.np_recip) : w_in[idx[k]];
+    }
+    if (!DEFER && !valid[0]) return;
+#pragma unroll
+    for (int k = 0; k < P; ++k)
+        particle_predict<MOTION, HOSTNOISE>(idx[k], valid[k], n, st, rstep, rflag, xs, ys, ts, xo,
+                                            yo, to, c, flags, noise, io, pc, seed, xv[k], yv[k],
+                                            tv[k]);
+    likelihood_lanes<LIK, P>(xv, yv, tv, lm, zs, lc, bn);
+    double wv[P];
+#pragma unroll
+    for (int k = 0; k < P; ++k) {
+        wv[k] = pw[k] * bn[k];                                  // particle_filter.py:194
+        if (valid[k]) w_un[idx[k]] = wv[k];
+    }
+    if constexpr (DEFER) {
 #ifndef SLAM_NO_EPILOGUE
         defer_epilogue(base, n, wv, xv, yv, tv, refp, dp);
 #endif
@@ -695,6 +748,35 @@ __device__ void write_result(const BlockPartial& r, const double* xs, const doub
     *res = o;
 }
 
+// result record with x_est given (deferred path: taken from the block partials)
+__device__ void write_result_xe(const BlockPartial& r, const double* xe, double* refp,
+                                const double s, int32_t* flags, const double ess_th,
+                                slam_pf_result* res, const int32_t resampled_known) {
+    slam_pf_result o;
+    o.max_idx = r.maxi;
+    o.max_val = r.maxv;
+    o.x_est[0] = xe[0];
+    o.x_est[1] = xe[1];
+    o.x_est[2] = xe[2];
+    const double inv = 1.0 / r.sw;
+    const double mu[3] = {r.m1[0] * inv, r.m1[1] * inv, r.m1[2] * inv};
+    const double m2[9] = {r.m2[0], r.m2[1], r.m2[2], r.m2[1], r.m2[3], r.m2[4], r.m2[2], r.m2[4], r.m2[5]};
+    for (int a = 0; a < 3; ++a)
+        for (int b = 0; b < 3; ++b) o.cov[3 * a + b] = m2[3 * a + b] * inv - mu[a] * mu[b];
+    o.ess = 1.0 / r.sw2;
+    o.weight_sum = s;
+    o.resampled = resampled_known >= 0 ? resampled_known : (flags[kFlagResample] != 0);
+    o.resample_next = (o.ess < ess_th) ? 1 : 0;
+    o.status = flags[kFlagStatus];
+    o.n_special = flags[kFlagNSpecial];
+    flags[kFlagResample] = o.resample_next;
+    flags[kFlagStatus] = 0;
+    refp[0] = o.x_est[0];
+    refp[1] = o.x_est[1];
+    refp[2] = o.x_est[2];
+    *res = o;
+}
+
 // One normalise block = kNormPer particles (kNormThreads lanes x kNormEPT,
 // coalesced per k); all loads of a lane are issued before any use.
 __global__ __launch_bounds__(kNormThreads) void normalize_kernel(
@@ -867,226 +949,7 @@ __device__ double tail_chunk_sum(const double* __restrict__ w, const int32_t* __
     return out;
 }
 
-#ifdef SLAM_FIN_PROBE
-__device__ long long g_fin_probe[16];
-#define FIN_STAMP(k) do { if (threadIdx.x == 0) g_fin_probe[k] = wall_clock64(); } while (0)
-#else
-#define FIN_STAMP(k) do { } while (0)
-#endif
-
-// Deferred-path step end (one workgroup, single-GPU handles): np.sum of the
-// unnormalised weights from the fused blocks' leaf sums (particle_filter.py:234),
-// the block partials rescaled to the global max and combined in block order,
-// the exact max / first argmax of w = w_un / s (the first block whose
-// fl(M_b / s) equals fl(M / s) is rescanned element by element), the result
-// record, the step context, s for the next step, and -- when the next step
-// resamples -- the prefix of the 256-block weight totals for its exact cumsum.
-// Loads are issued up front (the kernel is latency-bound).  A non-positive
-// or non-finite s (all weights NaN -> 1/NP, :236) takes a slow whole-array pass.
-__global__ __launch_bounds__(1024) void finalize_deferred_kernel(
-    const int64_t n, const DeferParts dp, const double* __restrict__ w_un,
-    double* __restrict__ s_cur, const int32_t* __restrict__ tail_leaves,
-    const int32_t* __restrict__ tail_ops, const int32_t n_tail_leaves, const int32_t n_tail_ops,
-    const double* __restrict__ xs, const double* __restrict__ ys, const double* __restrict__ ts,
-    double* __restrict__ refp, int32_t* __restrict__ flags, const double ess_th, StepIO io,
-    const int32_t resampled_known, const double np_recip, double* __restrict__ boff) {
-    __shared__ double sh[1024];
-    __shared__ BlockPartial shp[1024 / 64];
-    __shared__ double s_bc[2];
-    __shared__ double s_wmax[16];
-    __shared__ double s_q[11 * 1024];
-    __shared__ double s_tot[11];
-    __shared__ unsigned long long s_min;
-    __shared__ int32_t want_scan;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int64_t nb = (n + kPartPer - 1) / kPartPer;
-    FIN_STAMP(0);
-    // ---- the first partial of every lane: loads issued up front, unconditionally
-    const int64_t b0 = tid < nb ? tid : nb - 1;
-    const double pm0 = (tid < nb) ? dp.pmax[b0] : -1.0;
-    // ---- np.sum: 8192-element buffers left to right; 8 lanes per buffer
-    const int64_t nfull = n / kSumChunk;
-    const int64_t nch = (n + kSumChunk - 1) / kSumChunk;
-    double s = 0.0;
-    for (int64_t c0 = 0; c0 < nfull; c0 += 128) {
-        const int64_t cnt = (nfull - c0 < 128) ? nfull - c0 : 128;
-        const int64_t c = c0 + (tid >> 3);
-        const int part = tid & 7;
-        double v = 0.0;
-        if ((tid >> 3) < cnt) {
-            const double* L = dp.leaf + 64 * c + 8 * part;
-            const double l0 = L[0], l1 = L[1], l2 = L[2], l3 = L[3];
-            const double l4 = L[4], l5 = L[5], l6 = L[6], l7 = L[7];
-            v = ((l0 + l1) + (l2 + l3)) + ((l4 + l5) + (l6 + l7));
-        }
-#pragma unroll
-        for (int d = 1; d < 8; d <<= 1) {
-            const double o = __shfl_xor(v, d, 64);
-            v = (part & d) ? (o + v) : (v + o);          // left operand = lower lane
-        }
-        __syncthreads();
-        if (part == 0 && (tid >> 3) < cnt) sh[tid >> 3] = v;
-        __syncthreads();
-        if (tid == 0) {
-#pragma unroll 16
-            for (int k = 0; k < cnt; ++k) s = s + sh[k];
-        }
-    }
-    if (nch > nfull) {
-        __syncthreads();
-        const double tsum = tail_chunk_sum(w_un + nfull * kSumChunk, tail_leaves, tail_ops,
-                                           n_tail_leaves, n_tail_ops, sh);
-        if (tid == 0) s = s + tsum;
-    }
-    // ---- global max of the block maxima
-    FIN_STAMP(1);
-    double mx = pm0;
-    for (int64_t b = tid + 1024; b < nb; b += 1024) mx = fmax(mx, dp.pmax[b]);
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) mx = fmax(mx, __shfl_xor(mx, d, 64));
-    if (lane == 0) s_wmax[wave] = mx;
-    if (tid == 0) s_bc[0] = s;
-    __syncthreads();
-    double M = s_wmax[0];
-    for (int w = 1; w < 16; ++w) M = fmax(M, s_wmax[w]);
-    s = s_bc[0];
-    const bool ok = (s > 0.0) && !isinf(s) && (M > 0.0);
-    FIN_STAMP(2);
-    BlockPartial tot;
-    bp_zero(tot);
-    if (ok) {
-        // ---- block partials rescaled to the global max: per lane in block
-        // order, then a fixed LDS tree (16 lane-strided segments per wave
-        // position, a butterfly per quantity)
-        double acc[11];
-#pragma unroll
-        for (int j = 0; j < 11; ++j) acc[j] = 0.0;
-        for (int64_t b = tid; b < nb; b += 1024) {
-            const double r = (b == tid ? pm0 : dp.pmax[b]) / M;
-            double qb[11];
-#pragma unroll
-            for (int j = 0; j < 11; ++j) qb[j] = dp.ps[j][b];
-            acc[0] += r * qb[0];
-            acc[1] += (r * r) * qb[1];
-#pragma unroll
-            for (int j = 2; j < 11; ++j) acc[j] += r * qb[j];
-        }
-#pragma unroll
-        for (int j = 0; j < 11; ++j) s_q[j * 1024 + tid] = acc[j];
-        __syncthreads();
-        if (wave < 11) {
-            const double* a = s_q + wave * 1024 + lane;
-            double r = a[0];
-#pragma unroll
-            for (int mm = 1; mm < 16; ++mm) r = r + a[64 * mm];
-#pragma unroll
-            for (int d = 1; d < 64; d <<= 1) {
-                const double o = __shfl_xor(r, d, 64);
-                r = (lane & d) ? (o + r) : (r + o);
-            }
-            if (lane == 0) s_tot[wave] = r;
-        }
-        __syncthreads();
-        if (tid == 0) {
-            tot.sw = s_tot[0];
-            tot.sw2 = s_tot[1];
-            for (int j = 0; j < 3; ++j) tot.m1[j] = s_tot[2 + j];
-            for (int j = 0; j < 6; ++j) tot.m2[j] = s_tot[5 + j];
-        }
-    } else {
-        // ---- every weight through the reference's division (slow, degenerate case)
-        BlockPartial a;
-        bp_zero(a);
-        const double r0 = refp[0], r1 = refp[1], r2 = refp[2];
-        for (int64_t i = tid; i < n; i += 1024) {
-            const double v = norm_w(w_un[i], s, np_recip);
-            BlockPartial o;
-            o.maxv = v;
-            o.maxi = i;
-            o.sw = v;
-            o.sw2 = v * v;
-            const double d0 = xs[i] - r0, d1 = ys[i] - r1, d2 = ts[i] - r2;
-            const double v0 = v * d0, v1 = v * d1, v2 = v * d2;
-            o.m1[0] = v0; o.m1[1] = v1; o.m1[2] = v2;
-            o.m2[0] = v0 * d0; o.m2[1] = v0 * d1; o.m2[2] = v0 * d2;
-            o.m2[3] = v1 * d1; o.m2[4] = v1 * d2; o.m2[5] = v2 * d2;
-            bp_merge(a, o);
-        }
-        tot = bp_block_reduce(a, shp);
-    }
-    FIN_STAMP(3);
-    if (ok) {
-        // ---- exact argmax of fl(w_un / s): the first block whose rescaled max ties
-        const double mval = M / s;                      // max of fl(w_un/s) = fl(max w_un / s)
-        if (tid == 0) s_min = ~0ull;
-        __syncthreads();
-        unsigned long long cb = ~0ull;
-        if (tid < nb && pm0 / s == mval) cb = (unsigned long long)tid;
-        for (int64_t b = tid + 1024; b < nb; b += 1024)
-            if (dp.pmax[b] / s == mval) cb = min(cb, (unsigned long long)b);
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) cb = min(cb, (unsigned long long)__shfl_xor((long long)cb, d, 64));
-        if (lane == 0) atomicMin(&s_min, cb);
-        __syncthreads();
-        const int64_t bc = (int64_t)s_min;
-        __syncthreads();
-        if (tid == 0) s_min = ~0ull;
-        __syncthreads();
-        if (tid < kPartPer) {
-            const int64_t i = bc * kPartPer + tid;
-            unsigned long long hit = (i < n && norm_w(w_un[i], s, np_recip) == mval)
-                                         ? (unsigned long long)i : ~0ull;
-#pragma unroll
-            for (int d = 1; d < 64; d <<= 1)
-                hit = min(hit, (unsigned long long)__shfl_xor((long long)hit, d, 64));
-            if (lane == 0) atomicMin(&s_min, hit);
-        }
-        __syncthreads();
-        if (tid == 0) {
-            const double f = M / s;                      // back from max-relative to w_un / s
-            tot.maxv = mval;
-            tot.maxi = (int64_t)s_min;
-            tot.sw *= f;
-            tot.sw2 *= f * f;
-            for (int j = 0; j < 3; ++j) tot.m1[j] *= f;
-            for (int j = 0; j < 6; ++j) tot.m2[j] *= f;
-        }
-    }
-    if (tid == 0) {
-        const int32_t st = io.ctr[0];
-    FIN_STAMP(4);
-        write_result(tot, xs, ys, ts, 0, refp, s, flags, ess_th, io.res + st, resampled_known);
-        want_scan = flags[kFlagResample];
-        io.ctr[0] = st + 1;
-        io.ctr[1] = io.ctr[1] + 1;
-        *s_cur = s;
-    }
-    __syncthreads();
-    FIN_STAMP(5);
-    if (want_scan) {
-        // 256-block totals of w for the next step's exact cumsum (S1)
-        auto btot = [&](int64_t b) {
-            if (ok) return (dp.pmax[b] / s) * dp.ps[0][b];
-            double v = 0.0;
-            const int64_t e = (b + 1) * kPartPer < n ? (b + 1) * kPartPer : n;
-            for (int64_t i = b * kPartPer; i < e; ++i) v += norm_w(w_un[i], s, np_recip);
-            return v;
-        };
-        const int per = (int)((nb + 1023) / 1024);
-        const int64_t b0 = (int64_t)tid * per;
-        double loc = 0.0;
-        for (int k = 0; k < per; ++k)
-            if (b0 + k < nb) loc += btot(b0 + k);
-        double total;
-        double ex = block_excl_scan<double, 1024>(loc, sh, total);
-        for (int k = 0; k < per; ++k)
-            if (b0 + k < nb) {
-                boff[b0 + k] = ex;
-                ex = ex + btot(b0 + k);
-            }
-        if (tid == 0) boff[nb] = total;
-    }
-}
+#include "pf_finalize.inl"
 
 // w = w_un / s (NaN -> 1/NP): materialise the current weights (get_state, np.sum)
 __global__ __launch_bounds__(256) void normalize_only_kernel(const int64_t n,

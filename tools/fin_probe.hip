@@ -15,11 +15,14 @@ int main() {
     std::uniform_real_distribution<double> U(0.0, 1.0);
     std::vector<double> w(n), pmax(nb), leaf((kPartPer / 128) * nb), ps(11 * nb);
     std::vector<int64_t> pidx(nb);
+    std::vector<double> ppre(nb);
     for (auto& v : w) { double u = U(g); v = u * u * u * u * 1e-20; }
     for (int64_t b = 0; b < nb; ++b) {
         double m = -1; int64_t mi = 0;
         for (int k = 0; k < kPartPer; ++k) if (w[b * kPartPer + k] > m) { m = w[b * kPartPer + k]; mi = b * kPartPer + k; }
         pmax[b] = m; pidx[b] = mi;
+        double pr = -1; for (int64_t i = b * kPartPer; i < mi; ++i) pr = w[i] > pr ? w[i] : pr;
+        ppre[b] = pr;
         for (int L = 0; L < kPartPer / 128; ++L) {
             double r[8];
             for (int k = 0; k < 8; ++k) { r[k] = w[b * kPartPer + L * 128 + k]; for (int j = 1; j < 16; ++j) r[k] += w[b * kPartPer + L * 128 + k + 8 * j]; }
@@ -32,6 +35,8 @@ int main() {
     for (int j = 0; j < 11; ++j) { dp.ps[j] = dev<double>(nb); CK(hipMemcpy(dp.ps[j], &ps[j * nb], nb * 8, hipMemcpyHostToDevice)); }
     CK(hipMemcpy(dp.pmax, pmax.data(), nb * 8, hipMemcpyHostToDevice));
     CK(hipMemcpy(dp.pidx, pidx.data(), nb * 8, hipMemcpyHostToDevice));
+    dp.ppre = dev<double>(nb); CK(hipMemcpy(dp.ppre, ppre.data(), nb * 8, hipMemcpyHostToDevice));
+    for (int j = 0; j < 3; ++j) dp.pxe[j] = dev<double>(nb);
     CK(hipMemcpy(dp.leaf, leaf.data(), leaf.size() * 8, hipMemcpyHostToDevice));
     double* w_un = dev<double>(n); CK(hipMemcpy(w_un, w.data(), n * 8, hipMemcpyHostToDevice));
     double *s_cur = dev<double>(1), *xs = dev<double>(n), *ys = dev<double>(n), *ts = dev<double>(n), *refp = dev<double>(4), *boff = dev<double>(nb + 1);
@@ -46,7 +51,7 @@ int main() {
         int32_t fl = rep & 1;     // odd reps: next step resamples (prefix pass)
         CK(hipMemcpy(flags, &fl, 4, hipMemcpyHostToDevice));
         CK(hipEventRecord(a));
-        finalize_deferred_kernel<<<1, 1024>>>(n, dp, w_un, s_cur, tl, to, 0, 0, xs, ys, ts, refp, flags, (rep & 1) ? 1e30 : -1.0, io, -1, 1.0 / n, boff);
+        finalize_deferred_kernel<<<1, kFinThreads>>>(n, dp, w_un, s_cur, tl, to, 0, 0, xs, ys, ts, refp, flags, (rep & 1) ? 1e30 : -1.0, io, -1, 1.0 / n, boff);
         CK(hipEventRecord(b));
         CK(hipEventSynchronize(b));
         float ms; CK(hipEventElapsedTime(&ms, a, b));
@@ -54,6 +59,7 @@ int main() {
         slam_pf_result r; CK(hipMemcpy(&r, io.res, sizeof(r), hipMemcpyDeviceToHost));
         printf("rep %d total %.1f us | phases(us):", rep, ms * 1e3);
         for (int k = 1; k <= 5; ++k) printf(" %.2f", (st[k] - st[k - 1]) * 1e3 / rate);
+
         printf(" | max_idx %lld ess %.4g\n", (long long)r.max_idx, r.ess);
     }
     return 0;
