@@ -74,39 +74,48 @@ __device__ __forceinline__ double u01_open0(uint32_t a, uint32_t b) {
     return ((double)m + 1.0) * 0x1p-53;
 }
 
-// Two standard normals (Box-Muller) from one Philox block.
-__device__ __forceinline__ void normal2(u32x4 r, double& n0, double& n1) {
-    const double u1 = u01_open0(r.x, r.y);
-    const double u2 = u01_open0(r.z, r.w);
-    const double rad = sqrt(-2.0 * log(u1));
-    double s, c;
-    sincospi(2.0 * u2, &s, &c);
-    n0 = rad * c;
-    n1 = rad * s;
+// Philox-2x32-10 (Random123): one 64-bit counter, one 32-bit key.
+__device__ __forceinline__ void philox2x32(uint32_t& c0, uint32_t& c1, uint32_t k) {
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        const uint32_t lo = 0xD256D193u * c0, hi = __umulhi(0xD256D193u, c0);
+        c0 = hi ^ k ^ c1;
+        c1 = lo;
+        k += 0x9E3779B9u;
+    }
 }
 
-// Three standard normals from ONE Philox block: two Box-Muller pairs on 32-bit
-// uniforms in (0, 1] (radius resolution 2^-32: |g| <= 6.66, a tail mass of
-// 3e-11 per draw); the fourth normal of the block is not formed.  Half the
-// Philox work of 53-bit uniforms; the per-step motion noise needs three
-// normals per particle.  log and sin/cos from fastmath.hpp (< 2 ulp).
-__device__ __forceinline__ void normal3(u32x4 r, double& n0, double& n1, double& n2) {
-    const double d1 = (double)r.x + 1.0;                 // u = d 2^-32, exact
-    const double u2 = ((double)r.y + 1.0) * 0x1p-32;
-    const double d3 = (double)r.z + 1.0;
-    const double u4 = ((double)r.w + 1.0) * 0x1p-32;
-    const double ra = sqrt(-2.0 * rng_log_scaled(d1, -32));
-    const double rb = sqrt(-2.0 * rng_log_scaled(d3, -32));
+// One Box-Muller pair from two 32-bit words: uniforms (a + 1) 2^-32 and
+// (b + 1) 2^-32 in (0, 1] (radius resolution 2^-32: |g| <= 6.66, a tail mass of
+// 3e-11 per draw); log, sqrt and sin/cos from fastmath.hpp (< 2 ulp).
+__device__ __forceinline__ void bm_pair(uint32_t a, uint32_t b, double& gc, double& gs) {
+    const double rad = sqrt_pos(-2.0 * rng_log_scaled((double)a + 1.0, -32));
     double s, c;
-    rng_sincos2pi(u2, &s, &c);
-    n0 = ra * c;
-    n1 = ra * s;
-    rng_sincos2pi(u4, &s, &c);
-    n2 = rb * c;
+    rng_sincos2pi(((double)b + 1.0) * 0x1p-32, &s, &c);
+    gc = rad * c;
+    gs = rad * s;
 }
 
-// RNG stream ids (counter word z)
-enum : uint32_t { kStreamPredict = 1, kStreamResample = 2 };
+// RNG stream ids (counter word z / Philox-2x32 key salt)
+enum : uint32_t { kStreamPredict = 1, kStreamResample = 2, kStreamPredict2 = 3 };
+
+// The six standard normals of particle pair p (particles 2p and 2p+1) at RNG
+// step `rstep`: a Philox-4x32-10 block (counter p, kStreamPredict, rstep) feeds
+// Box-Muller pairs A and B, a Philox-2x32-10 block (counter (p, rstep), key
+// seed ^ kStreamPredict2 salt) pair C.  Particle 2p draws (A.c, A.s, B.c),
+// particle 2p+1 (B.s, C.c, C.s): three pairs per two particles, no normal
+// formed and dropped.
+__device__ __forceinline__ void pair_normals(const uint64_t p, const uint32_t rstep,
+                                             const uint64_t seed, double g[6]) {
+    const u32x4 r = philox4x32(u32x4{(uint32_t)p, (uint32_t)(p >> 32), kStreamPredict, rstep},
+                               (uint32_t)seed, (uint32_t)(seed >> 32));
+    uint32_t c0 = (uint32_t)p, c1 = rstep;
+    philox2x32(c0, c1, ((uint32_t)seed ^ (uint32_t)(seed >> 32) * 0x85EBCA6Bu) ^ (kStreamPredict2 * 0x27D4EB2Fu));
+    bm_pair(r.x, r.y, g[0], g[1]);
+    bm_pair(r.z, r.w, g[2], g[3]);
+    bm_pair(c0, c1, g[4], g[5]);
+}
+
 
 // --------------------------------------------------- exact-cumsum binades
 // Binade of a non-negative running sum: E such that s in [2^E, 2^(E+1));

@@ -268,13 +268,11 @@ int launch_scans(slam_pf* h, int32_t force, bool with_s1) {
         unsigned* tk = h->tk + 2 * kTicketWords;
         scan_lean_classify_kernel<<<nb, kScanThreads, 0, s>>>(
             h->w_un, h->s_cur, h->pc.np_recip, n, h->boff, delta, h->stage, h->bk, h->bf, h->boffk,
-            h->bofff, h->ktot, h->nspec, tk, h->flags, force);
-        scan_lean_place_kernel<<<nb, kScanThreads, 0, s>>>(
-            h->stage, h->bf, h->boffk, h->bofff, h->spec_in, h->spec_out, h->nspec, h->ktot, n,
-            h->flags, h->w_un, h->s_cur, h->pc.np_recip, h->c, tk, force);
+            h->bofff, h->ktot, h->nspec, tk, h->flags, force, h->spec_in, h->spec_out, h->c);
         scan_lean_expand_kernel<<<nb, kScanThreads, 0, s>>>(
             h->w_un, h->s_cur, h->pc.np_recip, n, h->boff, delta, h->boffk, h->bofff, h->spec_out,
-            h->c, h->flags, force);
+            h->c, h->flags, force, step_io(h), h->pc, h->cfg.seed, h->dp.mark,
+            h->dp.carry);
         SLAM_HIP_TRY(hipGetLastError());
         return SLAM_OK;
     }
@@ -442,13 +440,24 @@ int create_impl(const slam_pf_config* cfg, int64_t n_local, int64_t n_global, in
         slam_pf_destroy(h);                               \
         return rc;                                        \
     }
+    // deferred handles: particle and weight arrays padded to whole fused blocks
+    // (the fused kernel moves particle pairs with 16-byte loads and stores)
+    const int64_t npad = deferred ? (int64_t)h->nb_part * kPartPer : n;
     for (int k = 0; k < 2; ++k) {
-        A(h->x[k], n);
-        A(h->y[k], n);
-        A(h->th[k], n);
+        A(h->x[k], npad);
+        A(h->y[k], npad);
+        A(h->th[k], npad);
     }
     A(h->w, n);
-    A(h->w_un, n);
+    A(h->w_un, npad);
+    if (npad > n) {
+        for (int k = 0; k < 2; ++k) {
+            SLAM_HIP_TRY(hipMemsetAsync(h->x[k], 0, sizeof(double) * npad, h->stream));
+            SLAM_HIP_TRY(hipMemsetAsync(h->y[k], 0, sizeof(double) * npad, h->stream));
+            SLAM_HIP_TRY(hipMemsetAsync(h->th[k], 0, sizeof(double) * npad, h->stream));
+        }
+        SLAM_HIP_TRY(hipMemsetAsync(h->w_un, 0, sizeof(double) * npad, h->stream));
+    }
     A(h->c, n);
     A(h->kincl, n);
     A(h->fexcl, n);
@@ -462,6 +471,10 @@ int create_impl(const slam_pf_config* cfg, int64_t n_local, int64_t n_global, in
     for (int q = 0; q < 3; ++q) A(h->dp.pxe[q], h->nb_part);
     for (int q = 0; q < 11; ++q) A(h->dp.ps[q], h->nb_part);
     A(h->dp.leaf, (size_t)(kPartPer / 128) * h->nb_part);
+    A(h->dp.mark, npad);
+    A(h->dp.carry, h->nb_part + 1);
+    SLAM_HIP_TRY(hipMemsetAsync(h->dp.mark, 0xff, sizeof(int64_t) * npad, h->stream));
+    SLAM_HIP_TRY(hipMemsetAsync(h->dp.carry, 0, sizeof(int32_t) * (h->nb_part + 1), h->stream));
     A(h->bk, h->nb_scan);
     A(h->boffk, h->nb_scan);
     A(h->bf, h->nb_scan);
@@ -553,6 +566,14 @@ int stage_inputs(slam_pf* h, const double* control, const double* z, const doubl
 }  // namespace
 
 #include "pf_shard_api.inl"
+
+#ifdef SLAM_PROBE
+extern "C" int slam_probe_read(unsigned long long* out, int count) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_probe), sizeof(unsigned long long) * count) != hipSuccess) return -1;
+    unsigned long long z[32] = {0};
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_probe), z, sizeof(z)) == hipSuccess ? 0 : -1;
+}
+#endif
 
 extern "C" {
 

@@ -33,6 +33,8 @@ struct DeferParts {
     double* pxe[3];         // particle (x, y, th) at pidx
     double* ps[11];         // sw, sw2, m1[3], m2[6]
     double* leaf;           // [(kPartPer / 128) * blocks]
+    int64_t* mark;          // [npad] resample-run starts: (RNG step << 32) | source (expand pass)
+    int32_t* carry;         // [blocks] source of each fused block's first position
 };
 
 // particle_filter.py:179-181 + the mlab.bivariate_normal constants
@@ -101,6 +103,7 @@ enum : int {
     kFlagStatus = 1,        // bit0 clamp (reference IndexError), bit1 scan fallback
     kFlagNSpecial = 2,
     kFlagFallback = 3,
+    kFlagMarkGen = 4,       // tag of the resample-run marks, advanced by every step end
     kFlagWords = 8,
 };
 

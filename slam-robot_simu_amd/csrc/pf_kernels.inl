@@ -8,6 +8,17 @@
 // Particles are SoA fp64 (x[], y[], th[]) in HBM, one particle per lane.
 #include "pf_kernels.hpp"
 
+// Phase stamps of the resample passes (probe builds only: -DSLAM_PROBE,
+// read back with slam_probe_read; never in the product library).
+#ifdef SLAM_PROBE
+__device__ unsigned long long g_probe[32];
+#define PROBE_AT(k) do { if (threadIdx.x == 0) g_probe[k] = wall_clock64(); } while (0)
+#define PROBE_MAX(k) do { if (threadIdx.x == 0) atomicMax(&g_probe[k], (unsigned long long)wall_clock64()); } while (0)
+#else
+#define PROBE_AT(k) do { } while (0)
+#define PROBE_MAX(k) do { } while (0)
+#endif
+
 namespace slam {
 
 // ====================================================================
@@ -173,7 +184,7 @@ __device__ __forceinline__ void max_first(double& v, int64_t& i, const double ov
 }
 
 // Deferred-path epilogue of a 256-lane, kPartPer-particle fused block (see
-// DeferParts).  Lane t holds particles t + 256 k (k < kDeferPPT); invalid ones carry
+// DeferParts).  Lane t holds particles kDeferPPT t + k (k < kDeferPPT); invalid ones carry
 // w = 0.  Every sum has a fixed order: per lane over k, then 16 lane-strided
 // segments (conflict-free LDS reads) left to right, then the 16 segments.
 __device__ void defer_epilogue(const int64_t base, const int64_t n, const double* wv,
@@ -191,9 +202,9 @@ __device__ void defer_epilogue(const int64_t base, const int64_t n, const double
     int64_t mi = INT64_MAX;
 #pragma unroll
     for (int k = 0; k < kDeferPPT; ++k) {
-        const int64_t i = base + t + 256 * k;
+        const int64_t i = base + kDeferPPT * t + k;
         const bool ok = i < n;
-        s_w[t + 256 * k] = ok ? wv[k] : 0.0;
+        s_w[kDeferPPT * t + k] = ok ? wv[k] : 0.0;
         if (ok && wv[k] > m) {
             m = wv[k];
             mi = i;
@@ -220,7 +231,7 @@ __device__ void defer_epilogue(const int64_t base, const int64_t n, const double
     for (int j = 0; j < 11; ++j) q[j] = 0.0;
 #pragma unroll
     for (int k = 0; k < kDeferPPT; ++k) {
-        const bool ok = base + t + 256 * k < n;
+        const bool ok = base + kDeferPPT * t + k < n;
         const double u = ok ? wv[k] * rs : 0.0;
         const double d0 = xv[k] - r0, d1 = yv[k] - r1, d2 = tv[k] - r2;
         const double ud0 = u * d0, ud1 = u * d1, ud2 = u * d2;
@@ -249,7 +260,7 @@ __device__ void defer_epilogue(const int64_t base, const int64_t n, const double
     double pre = -1.0;
 #pragma unroll
     for (int k = 0; k < kDeferPPT; ++k) {
-        const int64_t i = base + t + 256 * k;
+        const int64_t i = base + kDeferPPT * t + k;
         if (i < bi) pre = fmax(pre, wv[k]);
         if (i == bi) {
             dp.pxe[0][blk] = xv[k];
@@ -307,63 +318,40 @@ __device__ void defer_epilogue(const int64_t base, const int64_t n, const double
     }
 }
 
-// One particle of the fused step: [resample gather +] predict
-// (particle_filter.py:156-168, :216-222; motion_model.py:31-62).  Stores the
-// predicted particle when `store`.
-template <int MOTION, bool HOSTNOISE>
-__device__ __forceinline__ void particle_predict(
-    const int64_t i, const bool store, const int64_t n, const int32_t st, const uint32_t rstep,
-    const int32_t rflag, const double* __restrict__ xs, const double* __restrict__ ys,
-    const double* __restrict__ ts, double* __restrict__ xo, double* __restrict__ yo,
-    double* __restrict__ to, const double* __restrict__ c, int32_t* __restrict__ flags,
-    const double* __restrict__ noise, const StepIO& io, const PredictConst& pc,
-    const uint64_t seed, double& xn, double& yn, double& tn) {
-    // ---- resample gather (1: search the exact cumsum here; 2: already gathered)
-    int64_t src = i;
-    if (rflag == 1) {
-        const double ofs = resample_offset(io.ofs[st], pc.np_recip, seed, rstep);
-        const double pos = (double)i * pc.rstep + ofs;           // arange value + ofs
-        src = lower_bound_c(c, n, pos);
-        if (src >= n) {
-            src = n - 1;                                          // IndexError in the reference
-            if (store) atomicOr(&flags[kFlagStatus], 1);
-        }
+// first j in [lo, hi) with c[j] >= pos, hi if none: the while loop of
+// particle_filter.py:218-220 over the exact cumsum, restricted to a bracket
+// known to hold the answer
+__device__ __forceinline__ int64_t search_c(const double* __restrict__ c, int64_t lo, int64_t hi,
+                                            const double pos) {
+    while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        if (c[mid] < pos) lo = mid + 1;
+        else hi = mid;
     }
-    const double x = xs[src], y = ys[src], th = ts[src];
+    return lo;
+}
 
-    // ---- control of this step (particle_filter.py:46-58 / motion_model.py:40-45)
-    const double v = io.ctl[2 * st], om = io.ctl[2 * st + 1];
-
-    // ---- noise
-    double g0 = 0.0, g1 = 0.0, g2 = 0.0;
-    if (MOTION == kMotionNone) {
-    } else if (HOSTNOISE) {
-        g0 = noise[3 * i + 0];
-        g1 = noise[3 * i + 1];
-        g2 = noise[3 * i + 2];
-    } else {
-        // one Philox block per particle and step: counter (global index, stream, RNG step)
-        const uint64_t gi = (uint64_t)(pc.gbase + i);
-        const u32x4 c0{(uint32_t)gi, (uint32_t)(gi >> 32), kStreamPredict, rstep};
-        const u32x4 r0 = philox4x32(c0, (uint32_t)seed, (uint32_t)(seed >> 32));
-        double h0, h1, h2;
-        normal3(r0, h0, h1, h2);
-        if (MOTION == SLAM_MOTION_LINEAR) {   // noise_j = sum_k g_k q[k][j]
-            g0 = h0 * pc.q[0] + h1 * pc.q[3] + h2 * pc.q[6];
-            g1 = h0 * pc.q[1] + h1 * pc.q[4] + h2 * pc.q[7];
-            g2 = h0 * pc.q[2] + h1 * pc.q[5] + h2 * pc.q[8];
-        } else {
-            g0 = h0;
-            g1 = h1;
-            g2 = h2;
-        }
-    }
-
-    // ---- predict
+// Predict one particle (particle_filter.py:129-140, :165-166; motion_model.py:
+// 40-56) from its state and standard normals g, and give the likelihood the
+// rotation of mylib/transform.py:31-33 for the predicted heading:
+// ls = sin(pi/2 - th'), lc = cos(pi/2 - th').
+//  * linear model: ls, lc from fast_sincos(pi/2 - th') exactly as the
+//    reference forms them (the C1 parity path);
+//  * velocity model: sin/cos(th + w dt) and sin/cos(th') by angle addition
+//    from sin/cos(th) and the small turn increments w dt and gamma dt (two
+//    kernel-only sin/cos instead of two range-reduced ones; within 2 ulp of
+//    the direct evaluation).
+template <int MOTION>
+__device__ __forceinline__ void predict_particle(const double x, const double y, const double th,
+                                                 const double v, const double om, const double g0,
+                                                 const double g1, const double g2,
+                                                 const PredictConst& pc, double& xn, double& yn,
+                                                 double& tn, double& ls, double& lc) {
     if (MOTION == kMotionNone) {           // likelihood-only entry (particle_filter.py:170)
         xn = x;
         yn = y;
         tn = th;
+        fast_sincos(kHalfPi - tn, &ls, &lc);
     } else if (MOTION == SLAM_MOTION_LINEAR) {
         // particle_filter.py:129-140 then + v (:166); A = I, B = diag(V, V, w)
         double sn, cs;
@@ -373,6 +361,7 @@ __device__ __forceinline__ void particle_predict(
         xn = (x + v * a) + g0;
         yn = (y + v * b) + g1;
         tn = wrap_angle(th + om * pc.dt) + g2;
+        fast_sincos(kHalfPi - tn, &ls, &lc);
     } else {
         // motion_model.py:40-56 (the std handed to normal() is sigma**2)
         const double v2 = v * v, w2 = om * om;
@@ -384,17 +373,15 @@ __device__ __forceinline__ void particle_predict(
         const double gh = 0.0 + (sg * sg) * g2;
         const double a = vh / wh;
         const double b = wh * pc.dt;
-        double s0, c0, s1, c1;
+        double s0, c0, sb, cb, s1, c1, se, ce;
         fast_sincos(th, &s0, &c0);
-        fast_sincos(th + b, &s1, &c1);
+        small_sincos(b, &sb, &cb);
+        rotate_sc(s0, c0, sb, cb, &s1, &c1);                 // (th + w dt)
         xn = (x - (a * s0)) + (a * s1);
         yn = (y + (a * c0)) - (a * c1);
         tn = wrap_angle(th + (wh + gh) * pc.dt);
-    }
-    if (store) {
-        xo[i] = xn;
-        yo[i] = yn;
-        to[i] = tn;
+        small_sincos(gh * pc.dt, &se, &ce);
+        rotate_sc(s1, c1, se, ce, &lc, &ls);                 // th' = th + w dt + gamma dt
     }
 }
 
@@ -402,16 +389,15 @@ __device__ __forceinline__ void particle_predict(
 // mylib/transform.py:31-35 per landmark).  The landmark loop is shared: each
 // landmark and observation is loaded once (scalar loads, uniform across the
 // wave) and applied to the P particles, whose accumulators are independent
-// dependency chains.
+// dependency chains.  sp/cp: sin/cos(pi/2 - th) of each particle.
 template <int LIK, int P>
 __device__ __forceinline__ void likelihood_lanes(const double* xn, const double* yn,
-                                                 const double* tn, const double* __restrict__ lm,
+                                                 const double* sp, const double* cp,
+                                                 const double* __restrict__ lm,
                                                  const double* __restrict__ z, const LikConst& lc,
                                                  double* bn) {
     const int nl = lc.nl;
-    double sp[P], cp[P], acc[P];
-#pragma unroll
-    for (int k = 0; k < P; ++k) fast_sincos(kHalfPi - tn[k], &sp[k], &cp[k]);
+    double acc[P];
     if (LIK == SLAM_LIK_PRODUCT) {
         // particle_filter.py:185-192 factor by factor, in NumPy's rounding order
 #pragma unroll
@@ -457,7 +443,7 @@ __device__ __forceinline__ void likelihood_lanes(const double* xn, const double*
         }
 #pragma unroll
         for (int k = 0; k < P; ++k)
-            bn[k] = exp(fma(-0.5, acc[k] * lc.rsx2, lc.neg_nl_ln_den));
+            bn[k] = exp_lean(fma(-0.5, acc[k] * lc.rsx2, lc.neg_nl_ln_den));
         return;
     }
     for (int j = 0; j < nl; ++j) {
@@ -475,15 +461,17 @@ __device__ __forceinline__ void likelihood_lanes(const double* xn, const double*
     }
 #pragma unroll
     for (int k = 0; k < P; ++k)
-        bn[k] = exp(lc.has_rho ? fma(-acc[k], lc.rd2, lc.neg_nl_ln_den)
-                               : fma(-0.5, acc[k], lc.neg_nl_ln_den));
+        bn[k] = exp_lean(lc.has_rho ? fma(-acc[k], lc.rd2, lc.neg_nl_ln_den)
+                                    : fma(-0.5, acc[k], lc.neg_nl_ln_den));
 }
 
-// The fused step kernel.  DEFER = false (shards): one particle per lane,
-// previous weights normalised in w_in.  DEFER = true (single GPU):
-// kDeferPPT particles per lane, previous weights = w_un / s (read and
-// rewritten in place), plus the block epilogue that replaces the normalise
-// pass.
+// The fused step kernel: [resample gather +] predict + likelihood + weight.
+// DEFER = false (shards): one particle per lane, previous weights normalised
+// in w_in.  DEFER = true (single GPU, gbase = 0, particle arrays padded to
+// whole blocks): lane t of block b holds the consecutive particles
+// b kPartPer + kDeferPPT t + k -- 16-byte loads and stores, one device-RNG
+// pair per lane -- and the previous weights are w_un / s (read and rewritten
+// in place), followed by the block epilogue that replaces the normalise pass.
 #ifdef SLAM_FUSED_WPE
 #define SLAM_FUSED_ATTR __attribute__((amdgpu_waves_per_eu(SLAM_FUSED_WPE)))
 #else
@@ -497,43 +485,187 @@ __global__ __launch_bounds__(256) SLAM_FUSED_ATTR void pf_fused_kernel(
     const double* __restrict__ c, int32_t* __restrict__ flags, const double* __restrict__ noise,
     const double* __restrict__ lm, StepIO io, PredictConst pc, LikConst lc, uint64_t seed,
     const double* __restrict__ s_in, const double* __restrict__ refp, DeferParts dp) {
-    // DEFER: the previous weights are read from w_un itself (w_in unused)
+    static_assert(!DEFER || kDeferPPT == 2, "the deferred path pairs particles");
     const int32_t st = io.ctr[0];
     const uint32_t rstep = (uint32_t)io.ctr[1];
     const int32_t rflag = flags[kFlagResample];
     const double* __restrict__ zs = io.z + (size_t)st * 2 * (size_t)(lc.nl > 0 ? lc.nl : 1);
     constexpr int P = DEFER ? kDeferPPT : 1;
     const int64_t base = (int64_t)blockIdx.x * (256 * P);
-    double xv[P], yv[P], tv[P], pw[P], bn[P];
+    const int64_t i0 = base + P * (int64_t)threadIdx.x;
     bool valid[P];
     int64_t idx[P];
-    const double s_prev = DEFER ? *s_in : 0.0;
 #pragma unroll
     for (int k = 0; k < P; ++k) {
-        const int64_t i0 = base + threadIdx.x + 256 * k;
-        valid[k] = i0 < n;
-        idx[k] = valid[k] ? i0 : n - 1;
-        // particle_filter.py:222 (a resampled step starts from 1/NP) / :235-236
-        if (rflag) pw[k] = pc.np_recip;
-        else pw[k] = DEFER ? norm_w(w_un[idx[k]], s_prev, pc.np_recip) : w_in[idx[k]];
+        valid[k] = i0 + k < n;
+        idx[k] = valid[k] ? i0 + k : n - 1;
     }
-    if (!DEFER && !valid[0]) return;
+
+    // ---- previous weights: particle_filter.py:222 (a resampled step starts
+    //      from 1/NP) / :235-236
+    double pw[P];
+    if (DEFER) {
+        const double2 wu = *reinterpret_cast<const double2*>(w_un + i0);
+        const double s_prev = *s_in;
+        pw[0] = rflag ? pc.np_recip : norm_w(wu.x, s_prev, pc.np_recip);
+        pw[P - 1] = rflag ? pc.np_recip : norm_w(wu.y, s_prev, pc.np_recip);
+    } else {
+        pw[0] = rflag ? pc.np_recip : w_in[idx[0]];
+    }
+
+    // ---- source particles: the resample gather (rflag 1: search the exact
+    //      cumsum here; 2: already gathered) or the particles themselves
+    double x[P], y[P], th[P];
+    if (DEFER && rflag == 1 && !flags[kFlagFallback]) {
+        // the expand pass's inverse map: run starts in mark[], the block's
+        // first source in carry[]; a running max over the block's positions
+        __shared__ int32_t s_wmax[4];
+        const uint32_t mgen = (uint32_t)flags[kFlagMarkGen];
+        int32_t r[P];
+#pragma unroll
+        for (int k = 0; k < P; ++k) {
+            const int64_t mk = valid[k] ? dp.mark[i0 + k] : -1;
+            r[k] = ((uint64_t)mk >> 32) == mgen ? (int32_t)mk : -1;
+            if (k > 0) r[k] = r[k] > r[k - 1] ? r[k] : r[k - 1];
+        }
+        const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+        int32_t v = r[P - 1];
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const int32_t o = __shfl_up(v, d, 64);
+            if (lane >= d) v = o > v ? o : v;
+        }
+        if (lane == 63) s_wmax[wave] = v;
+        int32_t before = __shfl_up(v, 1, 64);
+        if (lane == 0) before = -1;
+        __syncthreads();
+        int32_t run = dp.carry[blockIdx.x];
+        for (int w = 0; w < wave; ++w) run = s_wmax[w] > run ? s_wmax[w] : run;
+        run = before > run ? before : run;
+#pragma unroll
+        for (int k = 0; k < P; ++k) {
+            int64_t src = r[k] > run ? r[k] : run;
+            if (src >= n) {
+                src = n - 1;                                     // IndexError in the reference
+                if (valid[k]) atomicOr(&flags[kFlagStatus], 1);
+            }
+            src = src < 0 ? 0 : src;
+            x[k] = xs[src];
+            y[k] = ys[src];
+            th[k] = ts[src];
+        }
+    } else if (rflag == 1) {
+        // bracket: the sources of the block's first and last positions (two
+        // lanes of different waves search the whole cumsum); every lane then
+        // searches only between them (the index map is monotone), a few
+        // probes when the weight is concentrated -- which it is whenever
+        // ESS < NP/100 triggered the resample
+        __shared__ int64_t s_br[2];
+        const double ofs = resample_offset(io.ofs[st], pc.np_recip, seed, rstep);
+        const int64_t ilast = (base + 256 * P < n ? base + 256 * P : n) - 1;
+        if (threadIdx.x == 0) s_br[0] = search_c(c, 0, n, (double)base * pc.rstep + ofs);
+        if (threadIdx.x == 64 || (blockDim.x <= 64 && threadIdx.x == 0))
+            s_br[1] = search_c(c, 0, n, (double)ilast * pc.rstep + ofs);
+        __syncthreads();
+        int64_t lo = s_br[0];
+        const int64_t hi = s_br[1] < n ? s_br[1] + 1 : n;
+#pragma unroll
+        for (int k = 0; k < P; ++k) {
+            int64_t src = search_c(c, lo, hi, (double)idx[k] * pc.rstep + ofs);   // arange value + ofs
+            lo = src;
+            if (src >= n) {
+                src = n - 1;                                     // IndexError in the reference
+                if (valid[k]) atomicOr(&flags[kFlagStatus], 1);
+            }
+            x[k] = xs[src];
+            y[k] = ys[src];
+            th[k] = ts[src];
+        }
+    } else if (DEFER) {
+        const double2 a = *reinterpret_cast<const double2*>(xs + i0);
+        const double2 b = *reinterpret_cast<const double2*>(ys + i0);
+        const double2 t2 = *reinterpret_cast<const double2*>(ts + i0);
+        x[0] = a.x;
+        x[P - 1] = a.y;
+        y[0] = b.x;
+        y[P - 1] = b.y;
+        th[0] = t2.x;
+        th[P - 1] = t2.y;
+    } else {
+        x[0] = xs[idx[0]];
+        y[0] = ys[idx[0]];
+        th[0] = ts[idx[0]];
+    }
+
+    // ---- standard normals of the motion noise
+    double g[P][3];
+    if (MOTION == kMotionNone) {
+#pragma unroll
+        for (int k = 0; k < P; ++k) g[k][0] = g[k][1] = g[k][2] = 0.0;
+    } else if (HOSTNOISE) {
+#pragma unroll
+        for (int k = 0; k < P; ++k) {
+            g[k][0] = noise[3 * idx[k] + 0];
+            g[k][1] = noise[3 * idx[k] + 1];
+            g[k][2] = noise[3 * idx[k] + 2];
+        }
+    } else {
+        const uint64_t gi = (uint64_t)(pc.gbase + i0);
+        double h[6];
+#ifdef SLAM_PROBE_NO_RNG                                      // instruction-count probe only
+        for (int j = 0; j < 6; ++j) h[j] = 0.0;
+#else
+        pair_normals(gi >> 1, rstep, seed, h);
+#endif
+        if (DEFER) {                                          // gi even: the whole pair
+#pragma unroll
+            for (int j = 0; j < 6; ++j) g[j / 3][j % 3] = h[j];
+        } else {
+            const bool odd = gi & 1;
+#pragma unroll
+            for (int j = 0; j < 3; ++j) g[0][j] = odd ? h[3 + j] : h[j];
+        }
+        if (MOTION == SLAM_MOTION_LINEAR) {                   // noise_j = sum_k g_k q[k][j]
+#pragma unroll
+            for (int k = 0; k < P; ++k) {
+                const double h0 = g[k][0], h1 = g[k][1], h2 = g[k][2];
+                g[k][0] = h0 * pc.q[0] + h1 * pc.q[3] + h2 * pc.q[6];
+                g[k][1] = h0 * pc.q[1] + h1 * pc.q[4] + h2 * pc.q[7];
+                g[k][2] = h0 * pc.q[2] + h1 * pc.q[5] + h2 * pc.q[8];
+            }
+        }
+    }
+
+    // ---- predict (control of this step: particle_filter.py:46-58 / motion_model.py:40-45)
+    const double v = io.ctl[2 * st], om = io.ctl[2 * st + 1];
+    double xv[P], yv[P], tv[P], sp[P], cp[P];
 #pragma unroll
     for (int k = 0; k < P; ++k)
-        particle_predict<MOTION, HOSTNOISE>(idx[k], valid[k], n, st, rstep, rflag, xs, ys, ts, xo,
-                                            yo, to, c, flags, noise, io, pc, seed, xv[k], yv[k],
-                                            tv[k]);
-    likelihood_lanes<LIK, P>(xv, yv, tv, lm, zs, lc, bn);
+        predict_particle<MOTION>(x[k], y[k], th[k], v, om, g[k][0], g[k][1], g[k][2], pc, xv[k],
+                                 yv[k], tv[k], sp[k], cp[k]);
+    if (DEFER) {                       // padded arrays: the pair is stored whole
+        *reinterpret_cast<double2*>(xo + i0) = double2{xv[0], xv[P - 1]};
+        *reinterpret_cast<double2*>(yo + i0) = double2{yv[0], yv[P - 1]};
+        *reinterpret_cast<double2*>(to + i0) = double2{tv[0], tv[P - 1]};
+    } else if (valid[0]) {
+        xo[i0] = xv[0];
+        yo[i0] = yv[0];
+        to[i0] = tv[0];
+    }
+
+    // ---- likelihood and weight (particle_filter.py:170-198)
+    double bn[P];
+    likelihood_lanes<LIK, P>(xv, yv, sp, cp, lm, zs, lc, bn);
     double wv[P];
 #pragma unroll
-    for (int k = 0; k < P; ++k) {
-        wv[k] = pw[k] * bn[k];                                  // particle_filter.py:194
-        if (valid[k]) w_un[idx[k]] = wv[k];
-    }
+    for (int k = 0; k < P; ++k) wv[k] = valid[k] ? pw[k] * bn[k] : 0.0;   // particle_filter.py:194
     if constexpr (DEFER) {
+        *reinterpret_cast<double2*>(w_un + i0) = double2{wv[0], wv[P - 1]};
 #ifndef SLAM_NO_EPILOGUE
         defer_epilogue(base, n, wv, xv, yv, tv, refp, dp);
 #endif
+    } else if (valid[0]) {
+        w_un[i0] = wv[0];
     }
 }
 
@@ -741,6 +873,7 @@ __device__ void write_result(const BlockPartial& r, const double* xs, const doub
     o.status = flags[kFlagStatus];
     o.n_special = flags[kFlagNSpecial];
     flags[kFlagResample] = o.resample_next;
+    flags[kFlagMarkGen] = flags[kFlagMarkGen] + 1;
     flags[kFlagStatus] = 0;
     refp[0] = o.x_est[0];
     refp[1] = o.x_est[1];
@@ -770,6 +903,7 @@ __device__ void write_result_xe(const BlockPartial& r, const double* xe, double*
     o.status = flags[kFlagStatus];
     o.n_special = flags[kFlagNSpecial];
     flags[kFlagResample] = o.resample_next;
+    flags[kFlagMarkGen] = flags[kFlagMarkGen] + 1;
     flags[kFlagStatus] = 0;
     refp[0] = o.x_est[0];
     refp[1] = o.x_est[1];
@@ -1220,10 +1354,10 @@ __global__ __launch_bounds__(kScanThreads) void scan_expand_kernel(
 
 // ====================================================================
 // Lean exact cumsum (single-GPU handles): no per-element scratch.  Pass A
-// classifies each 2048-element tile and stages its few special elements;
-// pass B places them in global order and folds them (last block); pass C
-// re-runs the identical classification and writes c.  Reads w twice,
-// writes c once: 24 B per element instead of ~60.
+// classifies each 2048-element tile and stages its few special elements; its
+// last block places them in global order and folds them; pass C re-runs the
+// identical classification and writes c.  Reads w twice, writes c once: 24 B
+// per element instead of ~60, two launches.
 // ====================================================================
 struct TileScan {
     uint64_t kex;            // exclusive prefix of the tile-local increments (this lane)
@@ -1291,21 +1425,142 @@ __device__ __forceinline__ void tile_classify(const double* __restrict__ w_un,
     ts.fex = block_excl_scan<int32_t, kScanThreads>(fsum, shf, ftile);
 }
 
-// Pass A: classify, stage the tile's specials (local P), tile totals; the
-// last block scans the totals (boffk, bofff, ktot, nspec).
+// double from/to lane l (uniform result, SGPR-held)
+__device__ __forceinline__ double readlane_d(const double v, const int l) {
+    const int lo = __builtin_amdgcn_readlane(__double2loint(v), l);
+    const int hi = __builtin_amdgcn_readlane(__double2hiint(v), l);
+    return __hiloint2double(hi, lo);
+}
+
+// The lean path's place + fold (last block of pass A): the M specials, in
+// global order, are located in the tiles' staging areas (tile offsets bofff in
+// LDS, searched per lane), given their global P, and folded by wave 0 in
+// chunks of 64: lane l precomputes everything that does not depend on the
+// running sum (the exact run increment K u of the following regular run, the
+// binade bounds the checks use), then the running sum walks the 64 lanes --
+// two dependent adds per special, operands read from the lanes into SGPRs.
+// Bit-identical to serial_fold; a failed run check takes the same fallback
+// (the plain sequential recurrence, flagged).
+constexpr int kFoldTilesLds = 4096;
+__device__ void lean_place_fold(const SpecialIn* __restrict__ stage,
+                                const uint64_t* __restrict__ boffk,
+                                const int32_t* __restrict__ bofff, const int ntiles,
+                                const int32_t M, const uint64_t ktot, const int64_t n,
+                                SpecialOut* __restrict__ out, int32_t* __restrict__ flags,
+                                const double* __restrict__ w_un, const double* __restrict__ s_in,
+                                const double np_recip, double* __restrict__ c) {
+    __shared__ int32_t s_off[kFoldTilesLds];
+    __shared__ int s_bad;
+    const bool in_lds = ntiles <= kFoldTilesLds;
+    if (in_lds)
+        for (int k = threadIdx.x; k < ntiles; k += blockDim.x) s_off[k] = ld_wt_i(&bofff[k]);
+    if (threadIdx.x == 0) {
+        s_bad = 0;
+        flags[kFlagNSpecial] = M;
+    }
+    __syncthreads();
+    if (threadIdx.x < 64) {
+        const int lane = threadIdx.x;
+        // special m: its tile (last tile whose offset is <= m), then the staged record
+        auto load_special = [&](const int64_t m, SpecialIn& e) {
+            int lo = 0, hi = ntiles - 1;
+            while (lo < hi) {
+                const int mid = (lo + hi + 1) >> 1;
+                const int32_t o = in_lds ? s_off[mid] : ld_wt_i(&bofff[mid]);
+                if (o <= m) lo = mid;
+                else hi = mid - 1;
+            }
+            const int32_t o = in_lds ? s_off[lo] : ld_wt_i(&bofff[lo]);
+            e = ld_wt_struct(&stage[(int64_t)lo * kScanBlock + (m - o)]);
+            e.P += ld_wt(&boffk[lo]);
+        };
+        double s = 0.0;
+        bool bad = false;
+        for (int64_t t0 = 0; t0 < M; t0 += 64) {
+            const int64_t m = t0 + lane;
+            SpecialIn e{};
+            if (m < M) load_special(m, e);
+            SpecialIn e63{};
+            if (lane == 63 && m + 1 < M) load_special(m + 1, e63);
+            // the following special's index and prefix (or the end of the array)
+            int64_t nidx = __shfl_down((long long)e.idx, 1, 64);
+            uint64_t nP = (uint64_t)__shfl_down((long long)e.P, 1, 64);
+            if (lane == 63) {
+                nidx = e63.idx;
+                nP = e63.P;
+            }
+            if (m + 1 >= M) {
+                nidx = n;
+                nP = ktot;
+            }
+            const bool run = (m < M) && (nidx - e.idx > 1);
+            const uint64_t K = nP - e.P;
+            const int E = e.E;
+            double lo = -__builtin_inf(), hi = __builtin_inf(), ku = 0.0;
+            if (run) {
+                lo = (E == -1022) ? 0.0 : ldexp(1.0, E);
+                hi = (E == -1022) ? 0x1p-1021 : ldexp(1.0, E + 1);
+                ku = (double)K * ldexp(1.0, E - 52);
+                if ((double)K >= 0x1p53) bad = true;
+            }
+            const double w = (m < M) ? e.w : 0.0;
+            double cs = 0.0;
+            const int lim = (M - t0 < 64) ? (int)(M - t0) : 64;
+#pragma unroll 8
+            for (int l = 0; l < lim; ++l) {
+                s = s + readlane_d(w, l);                 // the special element's own add
+                if (lane == l) cs = s;
+                const double blo = readlane_d(lo, l), bhi = readlane_d(hi, l);
+                if (!(s >= blo) || !(s < bhi)) bad = true;    // its run keeps the binade
+                s = s + readlane_d(ku, l);                // the run: K ulps, exact
+                if (!(s < bhi)) bad = true;
+            }
+            if (m < M) {
+                SpecialOut o;
+                o.cs = cs;
+                o.P = e.P;
+                o.E = e.E;
+                o.pad = 0;
+                out[m] = o;
+            }
+        }
+        if (__any(bad) && lane == 0) s_bad = 1;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        if (s_bad) {
+            flags[kFlagStatus] |= 2;
+            flags[kFlagFallback] = 1;
+            double r = 0.0;
+            for (int64_t i = 0; i < n; ++i) {
+                r = r + norm_w(w_un[i], *s_in, np_recip);
+                c[i] = r;
+            }
+        } else {
+            flags[kFlagFallback] = 0;
+        }
+    }
+}
+
+// Pass A: classify, stage the tile's specials (local P, write-through), tile
+// totals; the last block scans the totals (boffk, bofff, ktot, nspec), moves
+// the staged specials into one ordered list with global P and folds it
+// (serial_fold) -- the place-and-fold step inside the same launch.
 __global__ __launch_bounds__(kScanThreads) void scan_lean_classify_kernel(
     const double* __restrict__ w_un, const double* __restrict__ s_in, const double np_recip,
     const int64_t n, const double* __restrict__ boff, const double delta,
     SpecialIn* __restrict__ stage, uint64_t* __restrict__ bk, int32_t* __restrict__ bf,
     uint64_t* __restrict__ boffk, int32_t* __restrict__ bofff, uint64_t* __restrict__ ktot,
-    int32_t* __restrict__ nspec, unsigned* __restrict__ counter,
-    const int32_t* __restrict__ flags, const int32_t force) {
+    int32_t* __restrict__ nspec, unsigned* __restrict__ counter, int32_t* __restrict__ flags,
+    const int32_t force, SpecialIn* __restrict__ spec, SpecialOut* __restrict__ spec_out,
+    double* __restrict__ c) {
     if (!force && flags[kFlagResample] != 1) return;
     __shared__ double sv[kScanBlock + kScanBlock / 8];
     __shared__ double shd[kScanThreads / 64 + 1];
     __shared__ uint64_t shk[kScanThreads / 64 + 1];
     __shared__ int32_t shf[kScanThreads / 64 + 1];
     const int64_t b = blockIdx.x;
+    if (b == 0) PROBE_AT(0);
     TileScan ts;
     uint64_t ktile;
     int32_t ftile;
@@ -1323,7 +1578,7 @@ __global__ __launch_bounds__(kScanThreads) void scan_lean_classify_kernel(
             r.w = ts.v[k];
             r.E = ts.E[k];
             r.pad = 0;
-            stage[b * kScanBlock + fex] = r;
+            st_wt_struct(&stage[b * kScanBlock + fex], r);
             ++fex;
         }
     }
@@ -1332,40 +1587,48 @@ __global__ __launch_bounds__(kScanThreads) void scan_lean_classify_kernel(
         st_wt_i(&bf[b], ftile);
     }
     if (!arrive_last(counter)) return;
+    PROBE_AT(1);
     block_scan_array<uint64_t, kScanThreads>(bk, boffk, gridDim.x, ktot, shk);
     __syncthreads();
     block_scan_array<int32_t, kScanThreads>(bf, bofff, gridDim.x, nspec, shf);
-}
-
-// Pass B: staged specials to their global slots (P made global); the last
-// block folds them in order.
-__global__ __launch_bounds__(kScanThreads) void scan_lean_place_kernel(
-    const SpecialIn* __restrict__ stage, const int32_t* __restrict__ bf,
-    const uint64_t* __restrict__ boffk, const int32_t* __restrict__ bofff,
-    SpecialIn* __restrict__ spec, SpecialOut* __restrict__ spec_out,
-    const int32_t* __restrict__ nspec_p, const uint64_t* __restrict__ ktot_p, const int64_t n,
-    int32_t* __restrict__ flags, const double* __restrict__ w_un,
-    const double* __restrict__ s_in, const double np_recip, double* __restrict__ c,
-    unsigned* __restrict__ counter, const int32_t force) {
-    if (!force && flags[kFlagResample] != 1) return;
-    const int64_t b = blockIdx.x;
-    const int32_t cnt = bf[b];
-    for (int j = threadIdx.x; j < cnt; j += blockDim.x) {
-        SpecialIn r = stage[b * kScanBlock + j];
-        r.P += boffk[b];
-        st_wt_struct(&spec[bofff[b] + j], r);
-    }
-    if (!arrive_last(counter)) return;
-    serial_fold(spec, spec_out, *nspec_p, *ktot_p, n, flags, w_un, c, n, true, s_in, np_recip);
+    __syncthreads();
+    PROBE_AT(2);
+    lean_place_fold(stage, boffk, bofff, (int)gridDim.x, *nspec, *ktot, n, spec_out, flags, w_un,
+                    s_in, np_recip, c);
+    PROBE_AT(4);
 }
 
 // Pass C: identical classification, then every c_i from the specials.
+// Number of systematic positions at or below v: #{i in [0, n) :
+// fl(fl(i (1/NP)) + ofs) <= v} (particle_filter.py:213-215; the positions are
+// monotone in i).  An estimate from the inverse, then exact steps.
+__device__ __forceinline__ int64_t positions_upto(const double v, const int64_t n,
+                                                  const double rstep, const double ofs) {
+    if (!(v >= ofs)) return 0;
+    double e = floor((v - ofs) * (double)n) + 1.0;
+    e = e < 0.0 ? 0.0 : (e > (double)n ? (double)n : e);
+    int64_t i = (int64_t)e;
+    while (i > 0 && (double)(i - 1) * rstep + ofs > v) --i;
+    while (i < n && (double)i * rstep + ofs <= v) ++i;
+    return i;
+}
+
+// Pass C: identical classification, then every c_i from the specials -- and
+// the inverse of the resample map for the fused kernel: element j is the
+// source of the positions i with c_{j-1} < pos_i <= c_j (the lower_bound of
+// particle_filter.py:218-220), a run [s_j, e_j) with s_j = #positions <=
+// c_{j-1}.  A selected element marks the start of its run (mark[s_j] = tagged
+// j) and gives every fused block whose first position lies in the run its
+// carry (carry[fb] = j); positions past the last cumulative weight (the
+// reference's IndexError) are marked with j = n.  The fused block then reads
+// its marks and carry and takes a running max -- no search.
 __global__ __launch_bounds__(kScanThreads) void scan_lean_expand_kernel(
     const double* __restrict__ w_un, const double* __restrict__ s_in, const double np_recip,
     const int64_t n, const double* __restrict__ boff, const double delta,
     const uint64_t* __restrict__ boffk, const int32_t* __restrict__ bofff,
     const SpecialOut* __restrict__ so, double* __restrict__ c, const int32_t* __restrict__ flags,
-    const int32_t force) {
+    const int32_t force, const StepIO io, const PredictConst pc, const uint64_t seed,
+    int64_t* __restrict__ mark, int32_t* __restrict__ carry) {
     if (!force && flags[kFlagResample] != 1) return;
     if (flags[kFlagFallback]) return;
     __shared__ double sv[kScanBlock + kScanBlock / 8];
@@ -1373,6 +1636,11 @@ __global__ __launch_bounds__(kScanThreads) void scan_lean_expand_kernel(
     __shared__ uint64_t shk[kScanThreads / 64 + 1];
     __shared__ int32_t shf[kScanThreads / 64 + 1];
     const int64_t b = blockIdx.x;
+    const int t = threadIdx.x;
+    if (b == 0) PROBE_AT(5);
+    // the step's systematic offset and mark tag, fetched up front
+    const double ofs = mark ? resample_offset(io.ofs[io.ctr[0]], pc.np_recip, seed, (uint32_t)io.ctr[1]) : 0.0;
+    const int64_t gen = (int64_t)(uint32_t)flags[kFlagMarkGen] << 32;
     TileScan ts;
     uint64_t ktile;
     int32_t ftile;
@@ -1395,14 +1663,64 @@ __global__ __launch_bounds__(kScanThreads) void scan_lean_expand_kernel(
     // back through the padded LDS tile so the global stores are coalesced
     __syncthreads();
 #pragma unroll
-    for (int k = 0; k < kScanPer; ++k) sv[9 * threadIdx.x + k] = out[k];
+    for (int k = 0; k < kScanPer; ++k) sv[9 * t + k] = out[k];
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < kScanPer; ++k) {
-        const int e = threadIdx.x + kScanThreads * k;
+        const int e = t + kScanThreads * k;
         const int64_t i = b * kScanBlock + e;
         if (i < n) c[i] = sv[e + (e >> 3)];
     }
+    PROBE_MAX(6);
+    if (!mark) return;
+    // ---- inverse map: runs of this lane's elements 8t .. 8t+7
+    const int64_t j0 = b * kScanBlock + 8 * t;
+    const int lane = t & 63;
+    double cprev;
+    if (t > 0) {
+        cprev = sv[9 * (t - 1) + 7];
+    } else if (b == 0) {
+        cprev = -__builtin_inf();
+    } else {                                 // element j0 - 1 from its run's special
+        const SpecialOut& p = so[bofff[b] - 1];
+        cprev = p.cs + (double)(boffk[b] - p.P) * ldexp(1.0, p.E - 52);
+    }
+    int64_t sj = positions_upto(cprev, n, pc.rstep, ofs);
+#pragma unroll
+    for (int k = 0; k < kScanPer; ++k) {
+        const int64_t j = j0 + k;
+        const bool ok = j < n;
+        const int64_t ej = ok ? positions_upto(out[k], n, pc.rstep, ofs) : sj;
+        // the fused blocks whose first position lies in the run (or, past the
+        // last element, in the positions beyond the last cumulative weight)
+        int64_t flo = 0, fhi = 0, val = j;
+        if (ok && ej > sj) {
+            mark[sj] = gen | j;
+            flo = (sj + kPartPer - 1) / kPartPer;
+            fhi = (ej + kPartPer - 1) / kPartPer;
+        }
+        if (ok && j == n - 1 && ej < n) {
+            mark[ej] = gen | n;
+        }
+        // carries, written by the whole wave (a heavy element may own many)
+        uint64_t act = __ballot(fhi > flo);
+        while (act) {
+            const int l = __ffsll((unsigned long long)act) - 1;
+            act &= act - 1;
+            const int64_t L = __shfl(flo, l, 64), H = __shfl(fhi, l, 64);
+            const int32_t J = (int32_t)__shfl(val, l, 64);
+            for (int64_t f = L + lane; f < H; f += 64) carry[f] = J;
+        }
+        const bool beyond = ok && j == n - 1 && ej < n;
+        if (__any(beyond)) {
+            const int l = __ffsll((unsigned long long)__ballot(beyond)) - 1;
+            const int64_t e2 = __shfl(ej, l, 64);
+            for (int64_t f = (e2 + kPartPer - 1) / kPartPer + lane; f * kPartPer < n; f += 64)
+                carry[f] = (int32_t)n;
+        }
+        sj = ej;
+    }
+    PROBE_MAX(7);
 }
 
 // gather for the stand-alone resampling stage (particle_filter.py:216-222)
