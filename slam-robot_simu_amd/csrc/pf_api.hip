@@ -103,6 +103,7 @@ struct slam_pf {
     ShardScratch sh;
     // deferred normalisation (single-GPU handles): current weights = w_un / s_cur
     bool deferred = false;
+    bool scan_merged = false;   // exact cumsum in one launch (co-resident grid)
     double* s_cur = nullptr;
     DeferParts dp{};
     int32_t nb_part = 0;
@@ -264,6 +265,15 @@ int launch_scans(slam_pf* h, int32_t force, bool with_s1) {
         const int rc = launch_bsum(h);
         if (rc) return rc;
     }
+    if (h->deferred && h->scan_merged) {
+        unsigned* tk = h->tk + 2 * kTicketWords;
+        scan_lean_merged_kernel<<<nb, kScanThreads, 0, s>>>(
+            h->w_un, h->s_cur, h->pc.np_recip, n, h->boff, delta, h->stage, h->bk, h->bf, h->boffk,
+            h->bofff, h->ktot, h->nspec, tk, h->flags, force, h->spec_out, h->c, step_io(h), h->pc,
+            h->cfg.seed, h->dp.mark, h->dp.carry, h->flags + kFlagScanToken);
+        SLAM_HIP_TRY(hipGetLastError());
+        return SLAM_OK;
+    }
     if (h->deferred) {
         unsigned* tk = h->tk + 2 * kTicketWords;
         scan_lean_classify_kernel<<<nb, kScanThreads, 0, s>>>(
@@ -385,6 +395,8 @@ int sync_results(slam_pf* h, int32_t first, int32_t count, slam_pf_result* out) 
     int rc = SLAM_OK;
     for (int i = 0; i < count; ++i) {
         if (out) out[i] = h->res_host[i];
+        if (h->res_host[i].status & 8)
+            rc = fail(SLAM_ERR_HIP, "exact-cumsum launch: release token timed out");
         if (h->res_host[i].status & 1)
             rc = fail(SLAM_ERR_INDEX, "resample position beyond the last cumulative weight "
                                       "(IndexError in particle_filter.py:219); clamped to NP-1");
@@ -430,6 +442,16 @@ int create_impl(const slam_pf_config* cfg, int64_t n_local, int64_t n_global, in
     h->nb_norm = (int32_t)((n + kNormPer - 1) / kNormPer);
     h->nb_part = (int32_t)((n + kPartPer - 1) / kPartPer);
     h->deferred = deferred;
+    {
+        // merged exact-cumsum launch only when its whole grid is co-resident
+        // (its blocks wait for the last one); otherwise two launches
+        int per_cu = 0, cus = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, scan_lean_merged_kernel,
+                                                         kScanThreads, 0) == hipSuccess &&
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) ==
+                hipSuccess)
+            h->scan_merged = deferred && (int64_t)h->nb_scan <= (int64_t)per_cu * cus / 2;
+    }
     hipError_t e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking);
     if (e != hipSuccess) {
         delete h;

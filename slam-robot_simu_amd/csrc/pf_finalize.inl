@@ -28,9 +28,12 @@ __device__ long long g_fin_probe[16];
 #define FIN_STAMP(k) do { } while (0)
 #endif
 
-constexpr int kFinThreads = 512;
+#ifndef SLAM_FIN_THREADS
+#define SLAM_FIN_THREADS 512
+#endif
+constexpr int kFinThreads = SLAM_FIN_THREADS;
 constexpr int kFinWaves = kFinThreads / 64;
-constexpr int kFinRegBlocks = 4;            // fused blocks held in registers per lane (2048)
+constexpr int kFinRegBlocks = 2048 / kFinThreads;   // fused blocks held in registers per lane (2048)
 constexpr int kFinLeafLanes = 4;            // lanes per 8192-element buffer (16 leaves each)
 constexpr int kFinBufPerRound = kFinThreads / kFinLeafLanes;   // 128 buffers per round
 constexpr int kFinCand = 8;                 // argmax candidate records staged in LDS

@@ -104,6 +104,7 @@ enum : int {
     kFlagNSpecial = 2,
     kFlagFallback = 3,
     kFlagMarkGen = 4,       // tag of the resample-run marks, advanced by every step end
+    kFlagScanToken = 5,     // release token of the merged exact-cumsum launch
     kFlagWords = 8,
 };
 

@@ -501,16 +501,22 @@ __global__ __launch_bounds__(256) SLAM_FUSED_ATTR void pf_fused_kernel(
         idx[k] = valid[k] ? i0 + k : n - 1;
     }
 
-    // ---- previous weights: particle_filter.py:222 (a resampled step starts
-    //      from 1/NP) / :235-236
-    double pw[P];
+    // ---- every load of the lane first (the previous weights and, without a
+    //      resample gather, the particle pair), so that their latency runs
+    //      under the device RNG below; the weights are consumed at the end
+    double wprev[P];
+    double2 pa{}, pb{}, pt{};
     if (DEFER) {
         const double2 wu = *reinterpret_cast<const double2*>(w_un + i0);
-        const double s_prev = *s_in;
-        pw[0] = rflag ? pc.np_recip : norm_w(wu.x, s_prev, pc.np_recip);
-        pw[P - 1] = rflag ? pc.np_recip : norm_w(wu.y, s_prev, pc.np_recip);
+        wprev[0] = wu.x;
+        wprev[P - 1] = wu.y;
+        if (rflag != 1) {
+            pa = *reinterpret_cast<const double2*>(xs + i0);
+            pb = *reinterpret_cast<const double2*>(ys + i0);
+            pt = *reinterpret_cast<const double2*>(ts + i0);
+        }
     } else {
-        pw[0] = rflag ? pc.np_recip : w_in[idx[0]];
+        wprev[0] = w_in[idx[0]];
     }
 
     // ---- source particles: the resample gather (rflag 1: search the exact
@@ -582,15 +588,12 @@ __global__ __launch_bounds__(256) SLAM_FUSED_ATTR void pf_fused_kernel(
             th[k] = ts[src];
         }
     } else if (DEFER) {
-        const double2 a = *reinterpret_cast<const double2*>(xs + i0);
-        const double2 b = *reinterpret_cast<const double2*>(ys + i0);
-        const double2 t2 = *reinterpret_cast<const double2*>(ts + i0);
-        x[0] = a.x;
-        x[P - 1] = a.y;
-        y[0] = b.x;
-        y[P - 1] = b.y;
-        th[0] = t2.x;
-        th[P - 1] = t2.y;
+        x[0] = pa.x;
+        x[P - 1] = pa.y;
+        y[0] = pb.x;
+        y[P - 1] = pb.y;
+        th[0] = pt.x;
+        th[P - 1] = pt.y;
     } else {
         x[0] = xs[idx[0]];
         y[0] = ys[idx[0]];
@@ -656,9 +659,16 @@ __global__ __launch_bounds__(256) SLAM_FUSED_ATTR void pf_fused_kernel(
     // ---- likelihood and weight (particle_filter.py:170-198)
     double bn[P];
     likelihood_lanes<LIK, P>(xv, yv, sp, cp, lm, zs, lc, bn);
+    // previous weights: particle_filter.py:222 (a resampled step starts from
+    // 1/NP) / :235-236 (deferred: w_un / s, NaN -> 1/NP)
     double wv[P];
+    const double s_prev = DEFER ? *s_in : 1.0;
 #pragma unroll
-    for (int k = 0; k < P; ++k) wv[k] = valid[k] ? pw[k] * bn[k] : 0.0;   // particle_filter.py:194
+    for (int k = 0; k < P; ++k) {
+        const double pw = rflag ? pc.np_recip
+                                : (DEFER ? norm_w(wprev[k], s_prev, pc.np_recip) : wprev[k]);
+        wv[k] = valid[k] ? pw * bn[k] : 0.0;                     // particle_filter.py:194
+    }
     if constexpr (DEFER) {
         *reinterpret_cast<double2*>(w_un + i0) = double2{wv[0], wv[P - 1]};
 #ifndef SLAM_NO_EPILOGUE
@@ -757,7 +767,8 @@ __global__ __launch_bounds__(512) void chunk_sum_kernel(
 
 // exclusive scan of a small per-block array (write-through words) by one block
 template <typename T, int NT>
-__device__ void block_scan_array(const T* in, T* out, const int nb, T* total, T* sh) {
+__device__ void block_scan_array(const T* in, T* out, const int nb, T* total, T* sh,
+                                 const bool wt = false) {
     const int per = (nb + NT - 1) / NT;
     const int b0 = threadIdx.x * per;
     auto ld = [](const T* p) -> T {
@@ -775,13 +786,24 @@ __device__ void block_scan_array(const T* in, T* out, const int nb, T* total, T*
         if (b0 + k < nb) loc = loc + ld(in + b0 + k);
     T tot;
     T ex = block_excl_scan<T, NT>(loc, sh, tot);
+    auto st = [wt](T* p, const T v) {
+        if (!wt) {
+            *p = v;
+        } else if constexpr (sizeof(T) == 8) {
+            uint64_t u;
+            __builtin_memcpy(&u, &v, 8);
+            st_wt(p, u);
+        } else {
+            st_wt_i((int32_t*)p, (int32_t)v);
+        }
+    };
     for (int k = 0; k < per; ++k)
         if (b0 + k < nb) {
             const T v = ld(in + b0 + k);
-            out[b0 + k] = ex;
+            st(out + b0 + k, ex);
             ex = ex + v;
         }
-    if (threadIdx.x == 0 && total) *total = tot;
+    if (threadIdx.x == 0 && total) st(total, tot);
 }
 
 // ====================================================================
@@ -1441,7 +1463,7 @@ __device__ __forceinline__ double readlane_d(const double v, const int l) {
 // two dependent adds per special, operands read from the lanes into SGPRs.
 // Bit-identical to serial_fold; a failed run check takes the same fallback
 // (the plain sequential recurrence, flagged).
-constexpr int kFoldTilesLds = 4096;
+constexpr int kFoldTilesLds = 2048;
 __device__ void lean_place_fold(const SpecialIn* __restrict__ stage,
                                 const uint64_t* __restrict__ boffk,
                                 const int32_t* __restrict__ bofff, const int ntiles,
@@ -1506,7 +1528,6 @@ __device__ void lean_place_fold(const SpecialIn* __restrict__ stage,
             const double w = (m < M) ? e.w : 0.0;
             double cs = 0.0;
             const int lim = (M - t0 < 64) ? (int)(M - t0) : 64;
-#pragma unroll 8
             for (int l = 0; l < lim; ++l) {
                 s = s + readlane_d(w, l);                 // the special element's own add
                 if (lane == l) cs = s;
@@ -1521,7 +1542,7 @@ __device__ void lean_place_fold(const SpecialIn* __restrict__ stage,
                 o.P = e.P;
                 o.E = e.E;
                 o.pad = 0;
-                out[m] = o;
+                st_wt_struct(&out[m], o);
             }
         }
         if (__any(bad) && lane == 0) s_bad = 1;
@@ -1530,14 +1551,14 @@ __device__ void lean_place_fold(const SpecialIn* __restrict__ stage,
     if (threadIdx.x == 0) {
         if (s_bad) {
             flags[kFlagStatus] |= 2;
-            flags[kFlagFallback] = 1;
+            st_wt_i(&flags[kFlagFallback], 1);
             double r = 0.0;
             for (int64_t i = 0; i < n; ++i) {
                 r = r + norm_w(w_un[i], *s_in, np_recip);
                 c[i] = r;
             }
         } else {
-            flags[kFlagFallback] = 0;
+            st_wt_i(&flags[kFlagFallback], 0);
         }
     }
 }
@@ -1622,41 +1643,33 @@ __device__ __forceinline__ int64_t positions_upto(const double v, const int64_t 
 // carry (carry[fb] = j); positions past the last cumulative weight (the
 // reference's IndexError) are marked with j = n.  The fused block then reads
 // its marks and carry and takes a running max -- no search.
-__global__ __launch_bounds__(kScanThreads) void scan_lean_expand_kernel(
-    const double* __restrict__ w_un, const double* __restrict__ s_in, const double np_recip,
-    const int64_t n, const double* __restrict__ boff, const double delta,
-    const uint64_t* __restrict__ boffk, const int32_t* __restrict__ bofff,
-    const SpecialOut* __restrict__ so, double* __restrict__ c, const int32_t* __restrict__ flags,
-    const int32_t force, const StepIO io, const PredictConst pc, const uint64_t seed,
-    int64_t* __restrict__ mark, int32_t* __restrict__ carry) {
-    if (!force && flags[kFlagResample] != 1) return;
-    if (flags[kFlagFallback]) return;
-    __shared__ double sv[kScanBlock + kScanBlock / 8];
-    __shared__ double shd[kScanThreads / 64 + 1];
-    __shared__ uint64_t shk[kScanThreads / 64 + 1];
-    __shared__ int32_t shf[kScanThreads / 64 + 1];
-    const int64_t b = blockIdx.x;
+// Pass C's per-tile work once the specials are folded: every c_i of tile b
+// from the tile's classification (ts) and the folded specials, then the
+// inverse resample map of the tile's elements (see below).  wt: the folded
+// data were handed over inside the same launch (write-through loads).
+__device__ void lean_expand_tile(const int64_t b, const TileScan& ts, const int64_t n,
+                                 const uint64_t* __restrict__ boffk,
+                                 const int32_t* __restrict__ bofff,
+                                 const SpecialOut* __restrict__ so, double* __restrict__ c,
+                                 double* sv, int64_t* __restrict__ mark,
+                                 int32_t* __restrict__ carry, const double ofs, const int64_t gen,
+                                 const PredictConst& pc, const bool wt) {
     const int t = threadIdx.x;
-    if (b == 0) PROBE_AT(5);
-    // the step's systematic offset and mark tag, fetched up front
-    const double ofs = mark ? resample_offset(io.ofs[io.ctr[0]], pc.np_recip, seed, (uint32_t)io.ctr[1]) : 0.0;
-    const int64_t gen = (int64_t)(uint32_t)flags[kFlagMarkGen] << 32;
-    TileScan ts;
-    uint64_t ktile;
-    int32_t ftile;
-    tile_classify(w_un, *s_in, np_recip, n, b, boff[b * (kScanBlock / kPartPer)], delta, sv, shd,
-                  shk, shf, ts, ktile, ftile);
-    uint64_t kin = boffk[b] + ts.kex;
-    int32_t m = bofff[b] + ts.fex;
+    auto ld_so = [wt, so](const int32_t m) { return wt ? ld_wt_struct(&so[m]) : so[m]; };
+    const uint64_t bk0 = wt ? ld_wt(&boffk[b]) : boffk[b];
+    const int32_t bf0 = wt ? ld_wt_i(&bofff[b]) : bofff[b];
+    uint64_t kin = bk0 + ts.kex;
+    int32_t m = bf0 + ts.fex;
     double out[kScanPer];
+    SpecialOut p = ld_so(m > 0 ? m - 1 : 0);
 #pragma unroll
     for (int k = 0; k < kScanPer; ++k) {
         kin += ts.kk[k];
         if (ts.ff[k]) {
-            out[k] = so[m].cs;
+            p = ld_so(m);
+            out[k] = p.cs;
             ++m;
         } else {
-            const SpecialOut& p = so[m - 1];
             out[k] = p.cs + (double)(kin - p.P) * ldexp(1.0, p.E - 52);
         }
     }
@@ -1682,8 +1695,8 @@ __global__ __launch_bounds__(kScanThreads) void scan_lean_expand_kernel(
     } else if (b == 0) {
         cprev = -__builtin_inf();
     } else {                                 // element j0 - 1 from its run's special
-        const SpecialOut& p = so[bofff[b] - 1];
-        cprev = p.cs + (double)(boffk[b] - p.P) * ldexp(1.0, p.E - 52);
+        const SpecialOut q = ld_so(bf0 - 1);
+        cprev = q.cs + (double)(bk0 - q.P) * ldexp(1.0, q.E - 52);
     }
     int64_t sj = positions_upto(cprev, n, pc.rstep, ofs);
 #pragma unroll
@@ -1721,6 +1734,125 @@ __global__ __launch_bounds__(kScanThreads) void scan_lean_expand_kernel(
         sj = ej;
     }
     PROBE_MAX(7);
+}
+
+// Pass C (large NP: the separate launch): identical classification, then
+// lean_expand_tile.
+__global__ __launch_bounds__(kScanThreads) void scan_lean_expand_kernel(
+    const double* __restrict__ w_un, const double* __restrict__ s_in, const double np_recip,
+    const int64_t n, const double* __restrict__ boff, const double delta,
+    const uint64_t* __restrict__ boffk, const int32_t* __restrict__ bofff,
+    const SpecialOut* __restrict__ so, double* __restrict__ c, const int32_t* __restrict__ flags,
+    const int32_t force, const StepIO io, const PredictConst pc, const uint64_t seed,
+    int64_t* __restrict__ mark, int32_t* __restrict__ carry) {
+    if (!force && flags[kFlagResample] != 1) return;
+    if (flags[kFlagFallback]) return;
+    __shared__ double sv[kScanBlock + kScanBlock / 8];
+    __shared__ double shd[kScanThreads / 64 + 1];
+    __shared__ uint64_t shk[kScanThreads / 64 + 1];
+    __shared__ int32_t shf[kScanThreads / 64 + 1];
+    const int64_t b = blockIdx.x;
+    if (b == 0) PROBE_AT(5);
+    // the step's systematic offset and mark tag, fetched up front
+    const double ofs = mark ? resample_offset(io.ofs[io.ctr[0]], pc.np_recip, seed, (uint32_t)io.ctr[1]) : 0.0;
+    const int64_t gen = (int64_t)(uint32_t)flags[kFlagMarkGen] << 32;
+    TileScan ts;
+    uint64_t ktile;
+    int32_t ftile;
+    tile_classify(w_un, *s_in, np_recip, n, b, boff[b * (kScanBlock / kPartPer)], delta, sv, shd,
+                  shk, shf, ts, ktile, ftile);
+    lean_expand_tile(b, ts, n, boffk, bofff, so, c, sv, mark, carry, ofs, gen, pc, false);
+}
+
+// Passes A and C in ONE launch (NP up to the co-resident grid, checked on the
+// host): classify and stage; the last block scans, places and folds and then
+// releases the others, which waited on a write-through token with their
+// tile's classification still in registers, and every block expands its tile.
+// The wait is bounded: a token that never arrives sets status bit 3 and the
+// block skips its expansion instead of hanging the device.
+__global__ __launch_bounds__(kScanThreads) void scan_lean_merged_kernel(
+    const double* __restrict__ w_un, const double* __restrict__ s_in, const double np_recip,
+    const int64_t n, const double* __restrict__ boff, const double delta,
+    SpecialIn* __restrict__ stage, uint64_t* __restrict__ bk, int32_t* __restrict__ bf,
+    uint64_t* __restrict__ boffk, int32_t* __restrict__ bofff, uint64_t* __restrict__ ktot,
+    int32_t* __restrict__ nspec, unsigned* __restrict__ counter, int32_t* __restrict__ flags,
+    const int32_t force, SpecialOut* __restrict__ spec_out, double* __restrict__ c,
+    const StepIO io, const PredictConst pc, const uint64_t seed, int64_t* __restrict__ mark,
+    int32_t* __restrict__ carry, int32_t* __restrict__ token_word) {
+    if (!force && flags[kFlagResample] != 1) return;
+    __shared__ double sv[kScanBlock + kScanBlock / 8];
+    __shared__ double shd[kScanThreads / 64 + 1];
+    __shared__ uint64_t shk[kScanThreads / 64 + 1];
+    __shared__ int32_t shf[kScanThreads / 64 + 1];
+    __shared__ int s_go;
+    const int64_t b = blockIdx.x;
+    if (b == 0) PROBE_AT(0);
+    const int32_t token = ld_wt_i(token_word) + 1;     // read before this block arrives
+    const double ofs = resample_offset(io.ofs[io.ctr[0]], pc.np_recip, seed, (uint32_t)io.ctr[1]);
+    const int64_t gen = (int64_t)(uint32_t)flags[kFlagMarkGen] << 32;
+    TileScan ts;
+    uint64_t ktile;
+    int32_t ftile;
+    tile_classify(w_un, *s_in, np_recip, n, b, boff[b * (kScanBlock / kPartPer)], delta, sv, shd,
+                  shk, shf, ts, ktile, ftile);
+    {
+        uint64_t kex = ts.kex;
+        int32_t fex = ts.fex;
+#pragma unroll
+        for (int k = 0; k < kScanPer; ++k) {
+            kex += ts.kk[k];
+            if (ts.ff[k]) {
+                SpecialIn r;
+                r.idx = b * kScanBlock + 8 * threadIdx.x + k;
+                r.P = kex;                              // tile-local inclusive prefix
+                r.w = ts.v[k];
+                r.E = ts.E[k];
+                r.pad = 0;
+                st_wt_struct(&stage[b * kScanBlock + fex], r);
+                ++fex;
+            }
+        }
+    }
+    if (threadIdx.x == 0) {
+        st_wt(&bk[b], ktile);
+        st_wt_i(&bf[b], ftile);
+    }
+    if (arrive_last(counter)) {
+        PROBE_AT(1);
+        block_scan_array<uint64_t, kScanThreads>(bk, boffk, gridDim.x, ktot, shk, true);
+        __syncthreads();
+        block_scan_array<int32_t, kScanThreads>(bf, bofff, gridDim.x, nspec, shf, true);
+        __syncthreads();
+        PROBE_AT(2);
+        lean_place_fold(stage, boffk, bofff, (int)gridDim.x, ld_wt_i(nspec), ld_wt(ktot), n,
+                        spec_out, flags, w_un, s_in, np_recip, c);
+        PROBE_AT(4);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            st_wt_i(token_word, token);
+            s_go = 1;
+        }
+    } else if (threadIdx.x == 0) {
+        int go = 0;
+        for (int it = 0; it < (1 << 22); ++it) {
+            if (ld_wt_i(token_word) == token) {
+                go = 1;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(2);
+        }
+        if (!go) atomicOr(&flags[kFlagStatus], 8);   // token never came: skip, do not hang
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        s_go = go;
+    }
+    __syncthreads();
+    if (b == 0) PROBE_AT(5);
+    if (!s_go || ld_wt_i(&flags[kFlagFallback])) return;
+    lean_expand_tile(b, ts, n, boffk, bofff, spec_out, c, sv, mark, carry, ofs, gen, pc, true);
 }
 
 // gather for the stand-alone resampling stage (particle_filter.py:216-222)
