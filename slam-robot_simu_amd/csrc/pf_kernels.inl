@@ -184,20 +184,26 @@ __device__ __forceinline__ void max_first(double& v, int64_t& i, const double ov
 }
 
 // Deferred-path epilogue of a 256-lane, kPartPer-particle fused block (see
-// DeferParts).  Lane t holds particles kDeferPPT t + k (k < kDeferPPT); invalid ones carry
-// w = 0.  Every sum has a fixed order: per lane over k, then 16 lane-strided
-// segments (conflict-free LDS reads) left to right, then the 16 segments.
+// DeferParts).  Lane t holds particles kDeferPPT t + k (k < kDeferPPT); invalid
+// ones carry w = 0.  Three barriers: (1) the wave maxima, (2) the lane-pair
+// moment sums and the wave argmax candidates, (3) the segment sums and leaf
+// accumulators.  Every sum has a fixed order: per lane over k, lane pairs
+// (2l, 2l+1), 16 pair-strided segments of 8 (conflict-free LDS reads) left to
+// right, then the 16 segments.
 __device__ void defer_epilogue(const int64_t base, const int64_t n, const double* wv,
                                const double* xv, const double* yv, const double* tv,
                                const double* __restrict__ refp, const DeferParts& dp) {
+    constexpr int kQ = 11;
+    constexpr int kLeaves = kPartPer / 128;
     __shared__ double s_w[kPartPer];
-    __shared__ double s_q[6 * 256];
-    __shared__ double s_seg[6 * 16];
-    __shared__ double s_acc[64];
+    __shared__ double s_q[kQ * 128];
+    __shared__ double s_seg[kQ * 16];
+    __shared__ double s_acc[8 * kLeaves];
     __shared__ double s_mv[4], s_pre[4];
     __shared__ int64_t s_mi[4];
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-    // lane max and its first particle, then the block max
+    const int blk = blockIdx.x;
+    // lane max and its first particle, then the wave max
     double m = -1.0;
     int64_t mi = INT64_MAX;
 #pragma unroll
@@ -214,9 +220,9 @@ __device__ void defer_epilogue(const int64_t base, const int64_t n, const double
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) mv = fmax(mv, __shfl_xor(mv, d, 64));
     if (lane == 0) s_mv[wave] = mv;
-    __syncthreads();
+    __syncthreads();                                                    // (1)
     const double M = fmax(fmax(s_mv[0], s_mv[1]), fmax(s_mv[2], s_mv[3]));
-    // first index holding M: min over the lanes whose max equals M
+    // first index holding M in this wave
     int64_t cand = (m == M) ? mi : INT64_MAX;
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
@@ -224,11 +230,12 @@ __device__ void defer_epilogue(const int64_t base, const int64_t n, const double
         cand = o < cand ? o : cand;
     }
     if (lane == 0) s_mi[wave] = cand;
+    // moments scaled by the block max, lane-pair sums into LDS
     const double rs = (M > 0.0) ? 1.0 / M : 0.0;
     const double r0 = refp[0], r1 = refp[1], r2 = refp[2];
-    double q[11];
+    double q[kQ];
 #pragma unroll
-    for (int j = 0; j < 11; ++j) q[j] = 0.0;
+    for (int j = 0; j < kQ; ++j) q[j] = 0.0;
 #pragma unroll
     for (int k = 0; k < kDeferPPT; ++k) {
         const bool ok = base + kDeferPPT * t + k < n;
@@ -247,12 +254,16 @@ __device__ void defer_epilogue(const int64_t base, const int64_t n, const double
         q[9] += ud1 * d2;
         q[10] += ud2 * d2;
     }
-    const int blk = blockIdx.x;
-    constexpr int kLeaves = kPartPer / 128;
-    // round 1: sw, sw2, m1[3] (+ the np.sum leaves' accumulators on lanes 128 ..)
 #pragma unroll
-    for (int j = 0; j < 5; ++j) s_q[j * 256 + t] = q[j];
-    __syncthreads();
+    for (int j = 0; j < kQ; ++j) {
+        const double o = __shfl_xor(q[j], 1, 64);
+        q[j] = (lane & 1) ? o + q[j] : q[j] + o;                     // (2l) + (2l+1)
+    }
+    if (!(lane & 1)) {
+#pragma unroll
+        for (int j = 0; j < kQ; ++j) s_q[j * 128 + (t >> 1)] = q[j];
+    }
+    __syncthreads();                                                    // (2)
     // the block's first max index; the largest weight before it; x_est candidate
     int64_t bi = s_mi[0];
 #pragma unroll
@@ -271,22 +282,23 @@ __device__ void defer_epilogue(const int64_t base, const int64_t n, const double
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) pre = fmax(pre, __shfl_xor(pre, d, 64));
     if (lane == 0) s_pre[wave] = pre;
-    if (t < 5 * 16) {
-        const double* a = s_q + (t >> 4) * 256 + (t & 15);
+    if (t < kQ * 16) {
+        // quantity t / 16, segment t % 16: pairs seg, seg + 16, ..., seg + 112
+        const double* a = s_q + (t >> 4) * 128 + (t & 15);
         double acc = a[0];
 #pragma unroll
-        for (int mm = 1; mm < 16; ++mm) acc = acc + a[16 * mm];
+        for (int mm = 1; mm < 8; ++mm) acc = acc + a[16 * mm];
         s_seg[t] = acc;
-    } else if (t >= 128 && t < 128 + 8 * kLeaves) {
-        // leaf (t-128)>>3, accumulator k = t & 7: elements k, k+8, ..., k+120
-        const double* a = s_w + ((t - 128) >> 3) * 128 + (t & 7);
+    } else if (t >= 192 && t < 192 + 8 * kLeaves) {
+        // leaf (t-192)>>3, accumulator k = t & 7: elements k, k+8, ..., k+120
+        const double* a = s_w + ((t - 192) >> 3) * 128 + (t & 7);
         double acc = a[0];
 #pragma unroll
         for (int mm = 1; mm < 16; ++mm) acc = acc + a[8 * mm];
-        s_acc[t - 128] = acc;
+        s_acc[t - 192] = acc;
     }
-    __syncthreads();
-    if (t < 5) {
+    __syncthreads();                                                    // (3)
+    if (t < kQ) {
         double acc = s_seg[16 * t];
         for (int mm = 1; mm < 16; ++mm) acc = acc + s_seg[16 * t + mm];
         dp.ps[t][blk] = acc;
@@ -297,24 +309,6 @@ __device__ void defer_epilogue(const int64_t base, const int64_t n, const double
         dp.pmax[blk] = M;
         dp.pidx[blk] = bi;
         dp.ppre[blk] = fmax(fmax(s_pre[0], s_pre[1]), fmax(s_pre[2], s_pre[3]));
-    }
-    __syncthreads();
-    // round 2: m2[6]
-#pragma unroll
-    for (int j = 0; j < 6; ++j) s_q[j * 256 + t] = q[5 + j];
-    __syncthreads();
-    if (t < 6 * 16) {
-        const double* a = s_q + (t >> 4) * 256 + (t & 15);
-        double acc = a[0];
-#pragma unroll
-        for (int mm = 1; mm < 16; ++mm) acc = acc + a[16 * mm];
-        s_seg[t] = acc;
-    }
-    __syncthreads();
-    if (t < 6) {
-        double acc = s_seg[16 * t];
-        for (int mm = 1; mm < 16; ++mm) acc = acc + s_seg[16 * t + mm];
-        dp.ps[5 + t][blk] = acc;
     }
 }
 
@@ -485,7 +479,7 @@ __global__ __launch_bounds__(256) SLAM_FUSED_ATTR void pf_fused_kernel(
     const double* __restrict__ c, int32_t* __restrict__ flags, const double* __restrict__ noise,
     const double* __restrict__ lm, StepIO io, PredictConst pc, LikConst lc, uint64_t seed,
     const double* __restrict__ s_in, const double* __restrict__ refp, DeferParts dp) {
-    static_assert(!DEFER || kDeferPPT == 2, "the deferred path pairs particles");
+    static_assert(!DEFER || kDeferPPT % 2 == 0, "the deferred path moves particle pairs");
     const int32_t st = io.ctr[0];
     const uint32_t rstep = (uint32_t)io.ctr[1];
     const int32_t rflag = flags[kFlagResample];
@@ -505,15 +499,27 @@ __global__ __launch_bounds__(256) SLAM_FUSED_ATTR void pf_fused_kernel(
     //      resample gather, the particle pair), so that their latency runs
     //      under the device RNG below; the weights are consumed at the end
     double wprev[P];
-    double2 pa{}, pb{}, pt{};
+    double lx[P], ly[P], lt[P];
     if (DEFER) {
-        const double2 wu = *reinterpret_cast<const double2*>(w_un + i0);
-        wprev[0] = wu.x;
-        wprev[P - 1] = wu.y;
+#pragma unroll
+        for (int h = 0; h < P; h += 2) {
+            const double2 wu = *reinterpret_cast<const double2*>(w_un + i0 + h);
+            wprev[h] = wu.x;
+            wprev[h + 1] = wu.y;
+        }
         if (rflag != 1) {
-            pa = *reinterpret_cast<const double2*>(xs + i0);
-            pb = *reinterpret_cast<const double2*>(ys + i0);
-            pt = *reinterpret_cast<const double2*>(ts + i0);
+#pragma unroll
+            for (int h = 0; h < P; h += 2) {
+                const double2 a = *reinterpret_cast<const double2*>(xs + i0 + h);
+                const double2 b = *reinterpret_cast<const double2*>(ys + i0 + h);
+                const double2 c2 = *reinterpret_cast<const double2*>(ts + i0 + h);
+                lx[h] = a.x;
+                lx[h + 1] = a.y;
+                ly[h] = b.x;
+                ly[h + 1] = b.y;
+                lt[h] = c2.x;
+                lt[h + 1] = c2.y;
+            }
         }
     } else {
         wprev[0] = w_in[idx[0]];
@@ -588,12 +594,12 @@ __global__ __launch_bounds__(256) SLAM_FUSED_ATTR void pf_fused_kernel(
             th[k] = ts[src];
         }
     } else if (DEFER) {
-        x[0] = pa.x;
-        x[P - 1] = pa.y;
-        y[0] = pb.x;
-        y[P - 1] = pb.y;
-        th[0] = pt.x;
-        th[P - 1] = pt.y;
+#pragma unroll
+        for (int k = 0; k < P; ++k) {
+            x[k] = lx[k];
+            y[k] = ly[k];
+            th[k] = lt[k];
+        }
     } else {
         x[0] = xs[idx[0]];
         y[0] = ys[idx[0]];
@@ -615,15 +621,19 @@ __global__ __launch_bounds__(256) SLAM_FUSED_ATTR void pf_fused_kernel(
     } else {
         const uint64_t gi = (uint64_t)(pc.gbase + i0);
         double h[6];
-#ifdef SLAM_PROBE_NO_RNG                                      // instruction-count probe only
-        for (int j = 0; j < 6; ++j) h[j] = 0.0;
-#else
-        pair_normals(gi >> 1, rstep, seed, h);
-#endif
-        if (DEFER) {                                          // gi even: the whole pair
+        if (DEFER) {                                          // gi even: whole pairs
 #pragma unroll
-            for (int j = 0; j < 6; ++j) g[j / 3][j % 3] = h[j];
+            for (int pr = 0; pr < P / 2; ++pr) {
+#ifdef SLAM_PROBE_NO_RNG                                      // instruction-count probe only
+                for (int j = 0; j < 6; ++j) h[j] = 0.0;
+#else
+                pair_normals((gi >> 1) + pr, rstep, seed, h);
+#endif
+#pragma unroll
+                for (int j = 0; j < 6; ++j) g[2 * pr + j / 3][j % 3] = h[j];
+            }
         } else {
+            pair_normals(gi >> 1, rstep, seed, h);
             const bool odd = gi & 1;
 #pragma unroll
             for (int j = 0; j < 3; ++j) g[0][j] = odd ? h[3 + j] : h[j];
@@ -647,9 +657,12 @@ __global__ __launch_bounds__(256) SLAM_FUSED_ATTR void pf_fused_kernel(
         predict_particle<MOTION>(x[k], y[k], th[k], v, om, g[k][0], g[k][1], g[k][2], pc, xv[k],
                                  yv[k], tv[k], sp[k], cp[k]);
     if (DEFER) {                       // padded arrays: the pair is stored whole
-        *reinterpret_cast<double2*>(xo + i0) = double2{xv[0], xv[P - 1]};
-        *reinterpret_cast<double2*>(yo + i0) = double2{yv[0], yv[P - 1]};
-        *reinterpret_cast<double2*>(to + i0) = double2{tv[0], tv[P - 1]};
+#pragma unroll
+        for (int h = 0; h < P; h += 2) {
+            *reinterpret_cast<double2*>(xo + i0 + h) = double2{xv[h], xv[h + 1]};
+            *reinterpret_cast<double2*>(yo + i0 + h) = double2{yv[h], yv[h + 1]};
+            *reinterpret_cast<double2*>(to + i0 + h) = double2{tv[h], tv[h + 1]};
+        }
     } else if (valid[0]) {
         xo[i0] = xv[0];
         yo[i0] = yv[0];
@@ -670,7 +683,9 @@ __global__ __launch_bounds__(256) SLAM_FUSED_ATTR void pf_fused_kernel(
         wv[k] = valid[k] ? pw * bn[k] : 0.0;                     // particle_filter.py:194
     }
     if constexpr (DEFER) {
-        *reinterpret_cast<double2*>(w_un + i0) = double2{wv[0], wv[P - 1]};
+#pragma unroll
+        for (int h = 0; h < P; h += 2)
+            *reinterpret_cast<double2*>(w_un + i0 + h) = double2{wv[h], wv[h + 1]};
 #ifndef SLAM_NO_EPILOGUE
         defer_epilogue(base, n, wv, xv, yv, tv, refp, dp);
 #endif
