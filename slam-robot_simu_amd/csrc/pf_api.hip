@@ -270,7 +270,7 @@ int launch_scans(slam_pf* h, int32_t force, bool with_s1) {
         scan_lean_merged_kernel<<<nb, kScanThreads, 0, s>>>(
             h->w_un, h->s_cur, h->pc.np_recip, n, h->boff, delta, h->stage, h->bk, h->bf, h->boffk,
             h->bofff, h->ktot, h->nspec, tk, h->flags, force, h->spec_out, h->c, step_io(h), h->pc,
-            h->cfg.seed, h->dp.mark, h->dp.carry, h->flags + kFlagScanToken);
+            h->cfg.seed, h->dp.mark, h->dp.carry, h->flags + kFlagScanToken, h->nb_part);
         SLAM_HIP_TRY(hipGetLastError());
         return SLAM_OK;
     }
@@ -278,11 +278,11 @@ int launch_scans(slam_pf* h, int32_t force, bool with_s1) {
         unsigned* tk = h->tk + 2 * kTicketWords;
         scan_lean_classify_kernel<<<nb, kScanThreads, 0, s>>>(
             h->w_un, h->s_cur, h->pc.np_recip, n, h->boff, delta, h->stage, h->bk, h->bf, h->boffk,
-            h->bofff, h->ktot, h->nspec, tk, h->flags, force, h->spec_in, h->spec_out, h->c);
+            h->bofff, h->ktot, h->nspec, tk, h->flags, force, h->spec_out, h->c, h->nb_part);
         scan_lean_expand_kernel<<<nb, kScanThreads, 0, s>>>(
             h->w_un, h->s_cur, h->pc.np_recip, n, h->boff, delta, h->boffk, h->bofff, h->spec_out,
             h->c, h->flags, force, step_io(h), h->pc, h->cfg.seed, h->dp.mark,
-            h->dp.carry);
+            h->dp.carry, h->nb_part);
         SLAM_HIP_TRY(hipGetLastError());
         return SLAM_OK;
     }
@@ -480,7 +480,7 @@ int create_impl(const slam_pf_config* cfg, int64_t n_local, int64_t n_global, in
         }
         SLAM_HIP_TRY(hipMemsetAsync(h->w_un, 0, sizeof(double) * npad, h->stream));
     }
-    A(h->c, n);
+    A(h->c, npad);
     A(h->kincl, n);
     A(h->fexcl, n);
     A(h->idx, n);
@@ -497,10 +497,12 @@ int create_impl(const slam_pf_config* cfg, int64_t n_local, int64_t n_global, in
     A(h->dp.carry, h->nb_part + 1);
     SLAM_HIP_TRY(hipMemsetAsync(h->dp.mark, 0xff, sizeof(int64_t) * npad, h->stream));
     SLAM_HIP_TRY(hipMemsetAsync(h->dp.carry, 0, sizeof(int32_t) * (h->nb_part + 1), h->stream));
-    A(h->bk, h->nb_scan);
-    A(h->boffk, h->nb_scan);
-    A(h->bf, h->nb_scan);
-    A(h->bofff, h->nb_scan);
+    // tile totals: 2048-element tiles (shards) or 512-element wave tiles (deferred)
+    const int32_t ntile_max = std::max(h->nb_scan, h->nb_part);
+    A(h->bk, ntile_max);
+    A(h->boffk, ntile_max);
+    A(h->bf, ntile_max);
+    A(h->bofff, ntile_max);
     A(h->ktot, 1);
     A(h->nspec, 1);
     A(h->spec_in, n);

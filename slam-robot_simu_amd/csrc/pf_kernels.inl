@@ -1390,12 +1390,19 @@ __global__ __launch_bounds__(kScanThreads) void scan_expand_kernel(
 }
 
 // ====================================================================
-// Lean exact cumsum (single-GPU handles): no per-element scratch.  Pass A
-// classifies each 2048-element tile and stages its few special elements; its
-// last block places them in global order and folds them; pass C re-runs the
-// identical classification and writes c.  Reads w twice, writes c once: 24 B
-// per element instead of ~60, two launches.
+// Lean exact cumsum (single-GPU handles), one WAVE per 512-element tile (a
+// fused block's particles): no per-element scratch and no block barrier in
+// the per-tile work -- the tile's prefix sums are wave scans.  Pass A
+// classifies each tile and stages its few special elements; its last block
+// places them in global order and folds them; pass C expands c from the
+// classification (kept in registers in the merged launch, recomputed in the
+// two-launch form) and writes the inverse resample map.  Reads w once (twice
+// in the two-launch form), writes c once.
 // ====================================================================
+constexpr int kWaveTile = 64 * kScanPer;                 // 512 elements
+static_assert(kWaveTile == kPartPer, "a scan tile is a fused block (boff, carry indexing)");
+constexpr int kTilesPerBlock = kScanThreads / 64;
+
 struct TileScan {
     uint64_t kex;            // exclusive prefix of the tile-local increments (this lane)
     int32_t fex;             // exclusive prefix of the tile-local special count (this lane)
@@ -1405,39 +1412,45 @@ struct TileScan {
     int E[kScanPer];         // binade of the approximate prefix after the element
 };
 
-// Tile b of the weights w = w_un / s: lane t owns elements 8t .. 8t+7 (read
-// through a padded LDS transpose so the global loads stay coalesced).
-__device__ __forceinline__ void tile_classify(const double* __restrict__ w_un,
-                                              const double s, const double np_recip,
-                                              const int64_t n, const int64_t b,
-                                              const double off, const double delta,
-                                              double* sv, double* shd, uint64_t* shk,
-                                              int32_t* shf, TileScan& ts, uint64_t& ktile,
-                                              int32_t& ftile) {
-    const int t = threadIdx.x;
-    const int64_t base = b * kScanBlock;
+// exclusive wave scan; `total` = the wave's sum (every lane)
+template <typename T>
+__device__ __forceinline__ T wave_excl_scan(const T v, T& total) {
+    const T inc = wave_incl_scan(v);
+    T ex = __shfl_up(inc, 1, 64);
+    if ((threadIdx.x & 63) == 0) ex = T(0);
+    total = __shfl(inc, 63, 64);
+    return ex;
+}
+
+// Tile `tile` of the weights w = w_un / s, lane l owns elements 8l .. 8l+7
+// (four 16-byte loads; w_un is padded to whole tiles).  off: the approximate
+// prefix before the tile (the finalize pass's fused-block prefix).
+__device__ __forceinline__ void wave_tile_classify(const double* __restrict__ w_un,
+                                                   const double s, const double np_recip,
+                                                   const int64_t n, const int64_t tile,
+                                                   const double off, const double delta,
+                                                   TileScan& ts, uint64_t& ktile,
+                                                   int32_t& ftile) {
+    const int lane = threadIdx.x & 63;
+    const int64_t base = tile * kWaveTile + 8 * lane;
 #pragma unroll
-    for (int k = 0; k < kScanPer; ++k) {
-        const int e = t + kScanThreads * k;
-        const int64_t i = base + e;
-        sv[e + (e >> 3)] = (i < n) ? norm_w(w_un[i], s, np_recip) : 0.0;
+    for (int h = 0; h < kScanPer; h += 2) {
+        const double2 w2 = *reinterpret_cast<const double2*>(w_un + base + h);
+        ts.v[h] = (base + h < n) ? norm_w(w2.x, s, np_recip) : 0.0;
+        ts.v[h + 1] = (base + h + 1 < n) ? norm_w(w2.y, s, np_recip) : 0.0;
     }
-    __syncthreads();
     double loc = 0.0;
 #pragma unroll
-    for (int k = 0; k < kScanPer; ++k) {
-        ts.v[k] = sv[9 * t + k];
-        loc += ts.v[k];
-    }
+    for (int k = 0; k < kScanPer; ++k) loc += ts.v[k];
     double dtot;
-    double run = block_excl_scan<double, kScanThreads>(loc, shd, dtot) + off;
+    double run = wave_excl_scan(loc, dtot) + off;
     uint64_t ksum = 0;
     int32_t fsum = 0;
 #pragma unroll
     for (int k = 0; k < kScanPer; ++k) {
         const double prev = run;
         run = run + ts.v[k];
-        const int64_t gi = base + 8 * t + k;
+        const int64_t gi = base + k;
         bool reg = (gi != 0) && (gi < n);
         uint64_t inc = 0;
         const int E = sum_binade(run);
@@ -1458,8 +1471,69 @@ __device__ __forceinline__ void tile_classify(const double* __restrict__ w_un,
         ksum += ts.kk[k];
         fsum += ts.ff[k];
     }
-    ts.kex = block_excl_scan<uint64_t, kScanThreads>(ksum, shk, ktile);
-    ts.fex = block_excl_scan<int32_t, kScanThreads>(fsum, shf, ftile);
+    ts.kex = wave_excl_scan(ksum, ktile);
+    ts.fex = wave_excl_scan(fsum, ftile);
+}
+
+// The four tiles of a block combine their totals (LDS, one barrier): the
+// block's staging area, its (k, f) totals and the tiles' exclusive offsets
+// inside the block.  The last arriver then scans one total per block.
+__device__ __forceinline__ void block_tile_offsets(const uint64_t ktile, const int32_t ftile,
+                                                   uint64_t& kofs, int32_t& fofs,
+                                                   uint64_t& kblk, int32_t& fblk) {
+    __shared__ uint64_t s_kt[kTilesPerBlock];
+    __shared__ int32_t s_ft[kTilesPerBlock];
+    const int wave = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) {
+        s_kt[wave] = ktile;
+        s_ft[wave] = ftile;
+    }
+    __syncthreads();
+    kofs = 0;
+    fofs = 0;
+    kblk = 0;
+    fblk = 0;
+#pragma unroll
+    for (int w = 0; w < kTilesPerBlock; ++w) {
+        if (w < wave) {
+            kofs += s_kt[w];
+            fofs += s_ft[w];
+        }
+        kblk += s_kt[w];
+        fblk += s_ft[w];
+    }
+}
+
+// Stage a classified tile's specials in its block's area (block-local P,
+// write-through); thread 0 publishes the block totals.
+__device__ __forceinline__ void wave_tile_stage(const int64_t tile, const TileScan& ts,
+                                                const uint64_t kofs, const int32_t fofs,
+                                                const uint64_t kblk, const int32_t fblk,
+                                                SpecialIn* __restrict__ stage,
+                                                uint64_t* __restrict__ bk,
+                                                int32_t* __restrict__ bf) {
+    const int lane = threadIdx.x & 63;
+    const int64_t b = blockIdx.x;
+    uint64_t kex = kofs + ts.kex;
+    int32_t fex = fofs + ts.fex;
+#pragma unroll
+    for (int k = 0; k < kScanPer; ++k) {
+        kex += ts.kk[k];
+        if (ts.ff[k]) {
+            SpecialIn r;
+            r.idx = tile * kWaveTile + 8 * lane + k;
+            r.P = kex;                                  // block-local inclusive prefix
+            r.w = ts.v[k];
+            r.E = ts.E[k];
+            r.pad = 0;
+            st_wt_struct(&stage[b * kScanBlock + fex], r);
+            ++fex;
+        }
+    }
+    if (threadIdx.x == 0) {
+        st_wt(&bk[b], kblk);
+        st_wt_i(&bf[b], fblk);
+    }
 }
 
 // double from/to lane l (uniform result, SGPR-held)
@@ -1478,7 +1552,7 @@ __device__ __forceinline__ double readlane_d(const double v, const int l) {
 // two dependent adds per special, operands read from the lanes into SGPRs.
 // Bit-identical to serial_fold; a failed run check takes the same fallback
 // (the plain sequential recurrence, flagged).
-constexpr int kFoldTilesLds = 2048;
+constexpr int kFoldTilesLds = 4096;
 __device__ void lean_place_fold(const SpecialIn* __restrict__ stage,
                                 const uint64_t* __restrict__ boffk,
                                 const int32_t* __restrict__ bofff, const int ntiles,
@@ -1513,24 +1587,20 @@ __device__ void lean_place_fold(const SpecialIn* __restrict__ stage,
         };
         double s = 0.0;
         bool bad = false;
-        for (int64_t t0 = 0; t0 < M; t0 += 64) {
+        // chunks of 63 specials: lane 63 only supplies the next chunk's first
+        for (int64_t t0 = 0; t0 < M; t0 += 63) {
             const int64_t m = t0 + lane;
             SpecialIn e{};
             if (m < M) load_special(m, e);
-            SpecialIn e63{};
-            if (lane == 63 && m + 1 < M) load_special(m + 1, e63);
             // the following special's index and prefix (or the end of the array)
             int64_t nidx = __shfl_down((long long)e.idx, 1, 64);
             uint64_t nP = (uint64_t)__shfl_down((long long)e.P, 1, 64);
-            if (lane == 63) {
-                nidx = e63.idx;
-                nP = e63.P;
-            }
             if (m + 1 >= M) {
                 nidx = n;
                 nP = ktot;
             }
-            const bool run = (m < M) && (nidx - e.idx > 1);
+            const bool mine = (lane < 63) && (m < M);
+            const bool run = mine && (nidx - e.idx > 1);
             const uint64_t K = nP - e.P;
             const int E = e.E;
             double lo = -__builtin_inf(), hi = __builtin_inf(), ku = 0.0;
@@ -1540,9 +1610,9 @@ __device__ void lean_place_fold(const SpecialIn* __restrict__ stage,
                 ku = (double)K * ldexp(1.0, E - 52);
                 if ((double)K >= 0x1p53) bad = true;
             }
-            const double w = (m < M) ? e.w : 0.0;
+            const double w = mine ? e.w : 0.0;
             double cs = 0.0;
-            const int lim = (M - t0 < 64) ? (int)(M - t0) : 64;
+            const int lim = (M - t0 < 63) ? (int)(M - t0) : 63;
             for (int l = 0; l < lim; ++l) {
                 s = s + readlane_d(w, l);                 // the special element's own add
                 if (lane == l) cs = s;
@@ -1551,7 +1621,7 @@ __device__ void lean_place_fold(const SpecialIn* __restrict__ stage,
                 s = s + readlane_d(ku, l);                // the run: K ulps, exact
                 if (!(s < bhi)) bad = true;
             }
-            if (m < M) {
+            if (mine) {
                 SpecialOut o;
                 o.cs = cs;
                 o.P = e.P;
@@ -1578,63 +1648,6 @@ __device__ void lean_place_fold(const SpecialIn* __restrict__ stage,
     }
 }
 
-// Pass A: classify, stage the tile's specials (local P, write-through), tile
-// totals; the last block scans the totals (boffk, bofff, ktot, nspec), moves
-// the staged specials into one ordered list with global P and folds it
-// (serial_fold) -- the place-and-fold step inside the same launch.
-__global__ __launch_bounds__(kScanThreads) void scan_lean_classify_kernel(
-    const double* __restrict__ w_un, const double* __restrict__ s_in, const double np_recip,
-    const int64_t n, const double* __restrict__ boff, const double delta,
-    SpecialIn* __restrict__ stage, uint64_t* __restrict__ bk, int32_t* __restrict__ bf,
-    uint64_t* __restrict__ boffk, int32_t* __restrict__ bofff, uint64_t* __restrict__ ktot,
-    int32_t* __restrict__ nspec, unsigned* __restrict__ counter, int32_t* __restrict__ flags,
-    const int32_t force, SpecialIn* __restrict__ spec, SpecialOut* __restrict__ spec_out,
-    double* __restrict__ c) {
-    if (!force && flags[kFlagResample] != 1) return;
-    __shared__ double sv[kScanBlock + kScanBlock / 8];
-    __shared__ double shd[kScanThreads / 64 + 1];
-    __shared__ uint64_t shk[kScanThreads / 64 + 1];
-    __shared__ int32_t shf[kScanThreads / 64 + 1];
-    const int64_t b = blockIdx.x;
-    if (b == 0) PROBE_AT(0);
-    TileScan ts;
-    uint64_t ktile;
-    int32_t ftile;
-    tile_classify(w_un, *s_in, np_recip, n, b, boff[b * (kScanBlock / kPartPer)], delta, sv, shd,
-                  shk, shf, ts, ktile, ftile);
-    uint64_t kex = ts.kex;
-    int32_t fex = ts.fex;
-#pragma unroll
-    for (int k = 0; k < kScanPer; ++k) {
-        kex += ts.kk[k];
-        if (ts.ff[k]) {
-            SpecialIn r;
-            r.idx = b * kScanBlock + 8 * threadIdx.x + k;
-            r.P = kex;                                  // tile-local inclusive prefix
-            r.w = ts.v[k];
-            r.E = ts.E[k];
-            r.pad = 0;
-            st_wt_struct(&stage[b * kScanBlock + fex], r);
-            ++fex;
-        }
-    }
-    if (threadIdx.x == 0) {
-        st_wt(&bk[b], ktile);
-        st_wt_i(&bf[b], ftile);
-    }
-    if (!arrive_last(counter)) return;
-    PROBE_AT(1);
-    block_scan_array<uint64_t, kScanThreads>(bk, boffk, gridDim.x, ktot, shk);
-    __syncthreads();
-    block_scan_array<int32_t, kScanThreads>(bf, bofff, gridDim.x, nspec, shf);
-    __syncthreads();
-    PROBE_AT(2);
-    lean_place_fold(stage, boffk, bofff, (int)gridDim.x, *nspec, *ktot, n, spec_out, flags, w_un,
-                    s_in, np_recip, c);
-    PROBE_AT(4);
-}
-
-// Pass C: identical classification, then every c_i from the specials.
 // Number of systematic positions at or below v: #{i in [0, n) :
 // fl(fl(i (1/NP)) + ofs) <= v} (particle_filter.py:213-215; the positions are
 // monotone in i).  An estimate from the inverse, then exact steps.
@@ -1649,30 +1662,28 @@ __device__ __forceinline__ int64_t positions_upto(const double v, const int64_t 
     return i;
 }
 
-// Pass C: identical classification, then every c_i from the specials -- and
-// the inverse of the resample map for the fused kernel: element j is the
-// source of the positions i with c_{j-1} < pos_i <= c_j (the lower_bound of
-// particle_filter.py:218-220), a run [s_j, e_j) with s_j = #positions <=
-// c_{j-1}.  A selected element marks the start of its run (mark[s_j] = tagged
-// j) and gives every fused block whose first position lies in the run its
-// carry (carry[fb] = j); positions past the last cumulative weight (the
-// reference's IndexError) are marked with j = n.  The fused block then reads
-// its marks and carry and takes a running max -- no search.
-// Pass C's per-tile work once the specials are folded: every c_i of tile b
-// from the tile's classification (ts) and the folded specials, then the
-// inverse resample map of the tile's elements (see below).  wt: the folded
-// data were handed over inside the same launch (write-through loads).
-__device__ void lean_expand_tile(const int64_t b, const TileScan& ts, const int64_t n,
+// Pass C for one tile, once the specials are folded: every c_i from the
+// tile's classification and the folded specials, then the inverse resample
+// map.  Source j serves the positions i with c_{j-1} < pos_i <= c_j (the
+// lower_bound of particle_filter.py:218-220), a run [s_j, e_j) with s_j =
+// #positions <= c_{j-1}.  A selected element marks the start of its run
+// (mark[s_j] = tagged j) and gives every fused block whose first position lies
+// in the run its carry (carry[fb] = j); positions past the last cumulative
+// weight (the reference's IndexError) are marked with j = n.  The fused block
+// then reads its marks and carry and takes a running max -- no search.
+// wt: the folded data were handed over inside the same launch.
+__device__ void wave_tile_expand(const int64_t tile, const TileScan& ts, const int64_t n,
                                  const uint64_t* __restrict__ boffk,
-                                 const int32_t* __restrict__ bofff,
-                                 const SpecialOut* __restrict__ so, double* __restrict__ c,
-                                 double* sv, int64_t* __restrict__ mark,
+                                 const int32_t* __restrict__ bofff, const uint64_t kofs,
+                                 const int32_t fofs, const SpecialOut* __restrict__ so,
+                                 double* __restrict__ c, int64_t* __restrict__ mark,
                                  int32_t* __restrict__ carry, const double ofs, const int64_t gen,
                                  const PredictConst& pc, const bool wt) {
-    const int t = threadIdx.x;
+    const int lane = threadIdx.x & 63;
     auto ld_so = [wt, so](const int32_t m) { return wt ? ld_wt_struct(&so[m]) : so[m]; };
-    const uint64_t bk0 = wt ? ld_wt(&boffk[b]) : boffk[b];
-    const int32_t bf0 = wt ? ld_wt_i(&bofff[b]) : bofff[b];
+    const int64_t b = blockIdx.x;
+    const uint64_t bk0 = (wt ? ld_wt(&boffk[b]) : boffk[b]) + kofs;   // the tile's global offsets
+    const int32_t bf0 = (wt ? ld_wt_i(&bofff[b]) : bofff[b]) + fofs;
     uint64_t kin = bk0 + ts.kex;
     int32_t m = bf0 + ts.fex;
     double out[kScanPer];
@@ -1688,30 +1699,21 @@ __device__ void lean_expand_tile(const int64_t b, const TileScan& ts, const int6
             out[k] = p.cs + (double)(kin - p.P) * ldexp(1.0, p.E - 52);
         }
     }
-    // back through the padded LDS tile so the global stores are coalesced
-    __syncthreads();
+    const int64_t j0 = tile * kWaveTile + 8 * lane;
 #pragma unroll
-    for (int k = 0; k < kScanPer; ++k) sv[9 * t + k] = out[k];
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < kScanPer; ++k) {
-        const int e = t + kScanThreads * k;
-        const int64_t i = b * kScanBlock + e;
-        if (i < n) c[i] = sv[e + (e >> 3)];
-    }
+    for (int h = 0; h < kScanPer; h += 2)          // c is padded to whole tiles
+        *reinterpret_cast<double2*>(c + j0 + h) = double2{out[h], out[h + 1]};
     PROBE_MAX(6);
     if (!mark) return;
-    // ---- inverse map: runs of this lane's elements 8t .. 8t+7
-    const int64_t j0 = b * kScanBlock + 8 * t;
-    const int lane = t & 63;
-    double cprev;
-    if (t > 0) {
-        cprev = sv[9 * (t - 1) + 7];
-    } else if (b == 0) {
-        cprev = -__builtin_inf();
-    } else {                                 // element j0 - 1 from its run's special
-        const SpecialOut q = ld_so(bf0 - 1);
-        cprev = q.cs + (double)(bk0 - q.P) * ldexp(1.0, q.E - 52);
+    // ---- inverse map: runs of this lane's elements
+    double cprev = __shfl_up(out[kScanPer - 1], 1, 64);
+    if (lane == 0) {
+        if (tile == 0) {
+            cprev = -__builtin_inf();
+        } else {                             // element j0 - 1 from its run's special
+            const SpecialOut q = ld_so(bf0 - 1);
+            cprev = q.cs + (double)(bk0 - q.P) * ldexp(1.0, q.E - 52);
+        }
     }
     int64_t sj = positions_upto(cprev, n, pc.rstep, ofs);
 #pragma unroll
@@ -1719,17 +1721,14 @@ __device__ void lean_expand_tile(const int64_t b, const TileScan& ts, const int6
         const int64_t j = j0 + k;
         const bool ok = j < n;
         const int64_t ej = ok ? positions_upto(out[k], n, pc.rstep, ofs) : sj;
-        // the fused blocks whose first position lies in the run (or, past the
-        // last element, in the positions beyond the last cumulative weight)
+        // the fused blocks whose first position lies in the run
         int64_t flo = 0, fhi = 0, val = j;
         if (ok && ej > sj) {
             mark[sj] = gen | j;
             flo = (sj + kPartPer - 1) / kPartPer;
             fhi = (ej + kPartPer - 1) / kPartPer;
         }
-        if (ok && j == n - 1 && ej < n) {
-            mark[ej] = gen | n;
-        }
+        if (ok && j == n - 1 && ej < n) mark[ej] = gen | n;
         // carries, written by the whole wave (a heavy element may own many)
         uint64_t act = __ballot(fhi > flo);
         while (act) {
@@ -1751,38 +1750,88 @@ __device__ void lean_expand_tile(const int64_t b, const TileScan& ts, const int6
     PROBE_MAX(7);
 }
 
-// Pass C (large NP: the separate launch): identical classification, then
-// lean_expand_tile.
+// the last block of pass A: block-total scans, then place + fold
+__device__ __forceinline__ void lean_last_block(uint64_t* __restrict__ bk, int32_t* __restrict__ bf,
+                                                uint64_t* __restrict__ boffk,
+                                                int32_t* __restrict__ bofff,
+                                                uint64_t* __restrict__ ktot,
+                                                int32_t* __restrict__ nspec, const int nblocks,
+                                                const SpecialIn* __restrict__ stage,
+                                                const int64_t n, SpecialOut* __restrict__ spec_out,
+                                                int32_t* __restrict__ flags,
+                                                const double* __restrict__ w_un,
+                                                const double* __restrict__ s_in,
+                                                const double np_recip, double* __restrict__ c) {
+    __shared__ uint64_t shk[kScanThreads / 64 + 1];
+    __shared__ int32_t shf[kScanThreads / 64 + 1];
+    PROBE_AT(1);
+    block_scan_array<uint64_t, kScanThreads>(bk, boffk, nblocks, ktot, shk, true);
+    __syncthreads();
+    block_scan_array<int32_t, kScanThreads>(bf, bofff, nblocks, nspec, shf, true);
+    __syncthreads();
+    PROBE_AT(2);
+    lean_place_fold(stage, boffk, bofff, nblocks, ld_wt_i(nspec), ld_wt(ktot), n, spec_out, flags,
+                    w_un, s_in, np_recip, c);
+    PROBE_AT(4);
+}
+
+// Pass A (two-launch form): classify and stage every tile; the last block
+// scans the tile totals, places and folds.
+__global__ __launch_bounds__(kScanThreads) void scan_lean_classify_kernel(
+    const double* __restrict__ w_un, const double* __restrict__ s_in, const double np_recip,
+    const int64_t n, const double* __restrict__ boff, const double delta,
+    SpecialIn* __restrict__ stage, uint64_t* __restrict__ bk, int32_t* __restrict__ bf,
+    uint64_t* __restrict__ boffk, int32_t* __restrict__ bofff, uint64_t* __restrict__ ktot,
+    int32_t* __restrict__ nspec, unsigned* __restrict__ counter, int32_t* __restrict__ flags,
+    const int32_t force, SpecialOut* __restrict__ spec_out, double* __restrict__ c,
+    const int ntiles) {
+    if (!force && flags[kFlagResample] != 1) return;
+    if (blockIdx.x == 0) PROBE_AT(0);
+    const int64_t tile = (int64_t)blockIdx.x * kTilesPerBlock + (threadIdx.x >> 6);
+    TileScan ts;
+    uint64_t ktile = 0, kofs, kblk;
+    int32_t ftile = 0, fofs, fblk;
+    if (tile < ntiles)
+        wave_tile_classify(w_un, *s_in, np_recip, n, tile, boff[tile], delta, ts, ktile, ftile);
+    block_tile_offsets(ktile, ftile, kofs, fofs, kblk, fblk);
+    if (tile < ntiles) wave_tile_stage(tile, ts, kofs, fofs, kblk, fblk, stage, bk, bf);
+    else if (threadIdx.x == 0) {
+        st_wt(&bk[blockIdx.x], kblk);
+        st_wt_i(&bf[blockIdx.x], fblk);
+    }
+    if (!arrive_last(counter)) return;
+    lean_last_block(bk, bf, boffk, bofff, ktot, nspec, (int)gridDim.x, stage, n, spec_out, flags,
+                    w_un, s_in, np_recip, c);
+}
+
+// Pass C (two-launch form): the identical classification, then the expansion.
 __global__ __launch_bounds__(kScanThreads) void scan_lean_expand_kernel(
     const double* __restrict__ w_un, const double* __restrict__ s_in, const double np_recip,
     const int64_t n, const double* __restrict__ boff, const double delta,
     const uint64_t* __restrict__ boffk, const int32_t* __restrict__ bofff,
     const SpecialOut* __restrict__ so, double* __restrict__ c, const int32_t* __restrict__ flags,
     const int32_t force, const StepIO io, const PredictConst pc, const uint64_t seed,
-    int64_t* __restrict__ mark, int32_t* __restrict__ carry) {
+    int64_t* __restrict__ mark, int32_t* __restrict__ carry, const int ntiles) {
     if (!force && flags[kFlagResample] != 1) return;
     if (flags[kFlagFallback]) return;
-    __shared__ double sv[kScanBlock + kScanBlock / 8];
-    __shared__ double shd[kScanThreads / 64 + 1];
-    __shared__ uint64_t shk[kScanThreads / 64 + 1];
-    __shared__ int32_t shf[kScanThreads / 64 + 1];
-    const int64_t b = blockIdx.x;
-    if (b == 0) PROBE_AT(5);
-    // the step's systematic offset and mark tag, fetched up front
+    const int64_t tile = (int64_t)blockIdx.x * kTilesPerBlock + (threadIdx.x >> 6);
     const double ofs = mark ? resample_offset(io.ofs[io.ctr[0]], pc.np_recip, seed, (uint32_t)io.ctr[1]) : 0.0;
     const int64_t gen = (int64_t)(uint32_t)flags[kFlagMarkGen] << 32;
     TileScan ts;
-    uint64_t ktile;
-    int32_t ftile;
-    tile_classify(w_un, *s_in, np_recip, n, b, boff[b * (kScanBlock / kPartPer)], delta, sv, shd,
-                  shk, shf, ts, ktile, ftile);
-    lean_expand_tile(b, ts, n, boffk, bofff, so, c, sv, mark, carry, ofs, gen, pc, false);
+    uint64_t ktile = 0, kofs, kblk;
+    int32_t ftile = 0, fofs, fblk;
+    if (tile < ntiles)
+        wave_tile_classify(w_un, *s_in, np_recip, n, tile, boff[tile], delta, ts, ktile, ftile);
+    block_tile_offsets(ktile, ftile, kofs, fofs, kblk, fblk);
+    if (tile < ntiles)
+        wave_tile_expand(tile, ts, n, boffk, bofff, kofs, fofs, so, c, mark, carry, ofs, gen, pc,
+                         false);
 }
 
 // Passes A and C in ONE launch (NP up to the co-resident grid, checked on the
 // host): classify and stage; the last block scans, places and folds and then
 // releases the others, which waited on a write-through token with their
-// tile's classification still in registers, and every block expands its tile.
+// tiles' classification still in registers, and every wave expands its tile.
 // The wait is bounded: a token that never arrives sets status bit 3 and the
 // block skips its expansion instead of hanging the device.
 __global__ __launch_bounds__(kScanThreads) void scan_lean_merged_kernel(
@@ -1793,55 +1842,29 @@ __global__ __launch_bounds__(kScanThreads) void scan_lean_merged_kernel(
     int32_t* __restrict__ nspec, unsigned* __restrict__ counter, int32_t* __restrict__ flags,
     const int32_t force, SpecialOut* __restrict__ spec_out, double* __restrict__ c,
     const StepIO io, const PredictConst pc, const uint64_t seed, int64_t* __restrict__ mark,
-    int32_t* __restrict__ carry, int32_t* __restrict__ token_word) {
+    int32_t* __restrict__ carry, int32_t* __restrict__ token_word, const int ntiles) {
     if (!force && flags[kFlagResample] != 1) return;
-    __shared__ double sv[kScanBlock + kScanBlock / 8];
-    __shared__ double shd[kScanThreads / 64 + 1];
-    __shared__ uint64_t shk[kScanThreads / 64 + 1];
-    __shared__ int32_t shf[kScanThreads / 64 + 1];
     __shared__ int s_go;
-    const int64_t b = blockIdx.x;
-    if (b == 0) PROBE_AT(0);
+    if (blockIdx.x == 0) PROBE_AT(0);
     const int32_t token = ld_wt_i(token_word) + 1;     // read before this block arrives
     const double ofs = resample_offset(io.ofs[io.ctr[0]], pc.np_recip, seed, (uint32_t)io.ctr[1]);
     const int64_t gen = (int64_t)(uint32_t)flags[kFlagMarkGen] << 32;
+    const int64_t tile = (int64_t)blockIdx.x * kTilesPerBlock + (threadIdx.x >> 6);
+    const bool active = tile < ntiles;
     TileScan ts;
-    uint64_t ktile;
-    int32_t ftile;
-    tile_classify(w_un, *s_in, np_recip, n, b, boff[b * (kScanBlock / kPartPer)], delta, sv, shd,
-                  shk, shf, ts, ktile, ftile);
-    {
-        uint64_t kex = ts.kex;
-        int32_t fex = ts.fex;
-#pragma unroll
-        for (int k = 0; k < kScanPer; ++k) {
-            kex += ts.kk[k];
-            if (ts.ff[k]) {
-                SpecialIn r;
-                r.idx = b * kScanBlock + 8 * threadIdx.x + k;
-                r.P = kex;                              // tile-local inclusive prefix
-                r.w = ts.v[k];
-                r.E = ts.E[k];
-                r.pad = 0;
-                st_wt_struct(&stage[b * kScanBlock + fex], r);
-                ++fex;
-            }
-        }
-    }
-    if (threadIdx.x == 0) {
-        st_wt(&bk[b], ktile);
-        st_wt_i(&bf[b], ftile);
+    uint64_t ktile = 0, kofs, kblk;
+    int32_t ftile = 0, fofs, fblk;
+    if (active)
+        wave_tile_classify(w_un, *s_in, np_recip, n, tile, boff[tile], delta, ts, ktile, ftile);
+    block_tile_offsets(ktile, ftile, kofs, fofs, kblk, fblk);
+    if (active) wave_tile_stage(tile, ts, kofs, fofs, kblk, fblk, stage, bk, bf);
+    else if (threadIdx.x == 0) {
+        st_wt(&bk[blockIdx.x], kblk);
+        st_wt_i(&bf[blockIdx.x], fblk);
     }
     if (arrive_last(counter)) {
-        PROBE_AT(1);
-        block_scan_array<uint64_t, kScanThreads>(bk, boffk, gridDim.x, ktot, shk, true);
-        __syncthreads();
-        block_scan_array<int32_t, kScanThreads>(bf, bofff, gridDim.x, nspec, shf, true);
-        __syncthreads();
-        PROBE_AT(2);
-        lean_place_fold(stage, boffk, bofff, (int)gridDim.x, ld_wt_i(nspec), ld_wt(ktot), n,
-                        spec_out, flags, w_un, s_in, np_recip, c);
-        PROBE_AT(4);
+        lean_last_block(bk, bf, boffk, bofff, ktot, nspec, (int)gridDim.x, stage, n, spec_out,
+                        flags, w_un, s_in, np_recip, c);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         if (threadIdx.x == 0) {
@@ -1865,9 +1888,10 @@ __global__ __launch_bounds__(kScanThreads) void scan_lean_merged_kernel(
         s_go = go;
     }
     __syncthreads();
-    if (b == 0) PROBE_AT(5);
-    if (!s_go || ld_wt_i(&flags[kFlagFallback])) return;
-    lean_expand_tile(b, ts, n, boffk, bofff, spec_out, c, sv, mark, carry, ofs, gen, pc, true);
+    if (blockIdx.x == 0) PROBE_AT(5);
+    if (!active || !s_go || ld_wt_i(&flags[kFlagFallback])) return;
+    wave_tile_expand(tile, ts, n, boffk, bofff, kofs, fofs, spec_out, c, mark, carry, ofs, gen, pc,
+                     true);
 }
 
 // gather for the stand-alone resampling stage (particle_filter.py:216-222)
