@@ -364,12 +364,19 @@ __global__ __launch_bounds__(256) void eks_apply_kernel(const double* __restrict
     }
 }
 
+// Two workgroups per CU (4 waves per SIMD, <= 128 VGPRs): measured 2.33 ms per
+// C4 update against 2.79 ms at the compiler's default of one workgroup per CU
+// (144 VGPRs) -- the small spill of the bound costs less than the lost overlap.
+#ifndef SLAM_EKS_WPE
+#define SLAM_EKS_WPE 4
+#endif
+#define SLAM_EKS_ATTR __attribute__((amdgpu_waves_per_eu(SLAM_EKS_WPE)))
 // P[i][j] -= sum_u K[i][u] PHt[j][u] for i >= j, one 128 x 128 lower tile per
 // workgroup.  fp64 MFMA 16x16x4: A = K rows (lane l: row l&15, k l>>4),
 // B = PHt^T (lane l: k l>>4, column l&15), D: column l&15, row (l>>4) + 4 r.
 // Tiles are numbered so that each XCD (blockIdx % 8) takes a contiguous range
 // of tile rows and reuses its K rows through its own L2.
-__global__ __launch_bounds__(kEksThreads) void eks_rank_update_kernel(
+__global__ __launch_bounds__(kEksThreads) SLAM_EKS_ATTR void eks_rank_update_kernel(
     double* __restrict__ P, const int64_t n, const int64_t ld, const double* __restrict__ kg,
     const double* __restrict__ pht, const int32_t M, const int64_t n_tiles) {
     __shared__ double Ks[kEksTile * kEksKS];    // K rows of the tile, one k-chunk
@@ -388,11 +395,21 @@ __global__ __launch_bounds__(kEksThreads) void eks_rank_update_kernel(
     const int wc = (wave & 1) * 64;         // wave's 64 columns
     const int lr = lane & 15, lk = lane >> 4;
     typedef double double4v __attribute__((ext_vector_type(4)));
+    // the P tile is the accumulators' starting value (loaded first, so its HBM
+    // latency runs under the K / PH^T staging and the MFMAs); K is staged
+    // negated, so the MFMAs leave P - K (PH^T)^T in place
+    const bool diag = (ti == tj);
     double4v acc[2][4];
 #pragma unroll
     for (int a = 0; a < 2; ++a)
 #pragma unroll
-        for (int b = 0; b < 4; ++b) acc[a][b] = double4v{0.0, 0.0, 0.0, 0.0};
+        for (int b = 0; b < 4; ++b)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int64_t gi = r0 + wr + 16 * a + lk + 4 * r;
+                const int64_t gj = c0 + wc + 16 * b + lr;
+                acc[a][b][r] = (gi < n && gj < n && (!diag || gj <= gi)) ? P[gi * ld + gj] : 0.0;
+            }
     const double* ksrc = kg + r0 * M;
     const double* hsrc = pht + c0 * M;
     for (int kc = 0; kc < M; kc += kEksKC) {
@@ -403,7 +420,7 @@ __global__ __launch_bounds__(kEksThreads) void eks_rank_update_kernel(
             const int idx = tid + s * kEksThreads;
             const int r = idx / kEksKC, q = idx % kEksKC;
             const bool ok = q < kw;
-            Ks[r * kEksKS + q] = ok ? ksrc[(int64_t)r * M + kc + q] : 0.0;
+            Ks[r * kEksKS + q] = ok ? -ksrc[(int64_t)r * M + kc + q] : 0.0;
             Hs[r * kEksKS + q] = ok ? hsrc[(int64_t)r * M + kc + q] : 0.0;
         }
         __syncthreads();
@@ -420,7 +437,6 @@ __global__ __launch_bounds__(kEksThreads) void eks_rank_update_kernel(
                     acc[a][b] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[a], fb[b], acc[a][b], 0, 0, 0);
         }
     }
-    const bool diag = (ti == tj);
 #pragma unroll
     for (int a = 0; a < 2; ++a)
 #pragma unroll
@@ -429,10 +445,7 @@ __global__ __launch_bounds__(kEksThreads) void eks_rank_update_kernel(
             for (int r = 0; r < 4; ++r) {
                 const int64_t gi = r0 + wr + 16 * a + lk + 4 * r;
                 const int64_t gj = c0 + wc + 16 * b + lr;
-                if (gi < n && gj < n && (!diag || gj <= gi)) {
-                    double* p = P + gi * ld + gj;
-                    *p = *p - acc[a][b][r];
-                }
+                if (gi < n && gj < n && (!diag || gj <= gi)) P[gi * ld + gj] = acc[a][b][r];
             }
 }
 
