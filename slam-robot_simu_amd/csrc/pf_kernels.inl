@@ -1862,6 +1862,7 @@ __global__ __launch_bounds__(kScanThreads) void scan_lean_merged_kernel(
         st_wt(&bk[blockIdx.x], kblk);
         st_wt_i(&bf[blockIdx.x], fblk);
     }
+    PROBE_MAX(12);
     if (arrive_last(counter)) {
         lean_last_block(bk, bf, boffk, bofff, ktot, nspec, (int)gridDim.x, stage, n, spec_out,
                         flags, w_un, s_in, np_recip, c);
