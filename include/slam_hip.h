@@ -118,6 +118,9 @@ int slam_pf_enable_timing(slam_pf* h, int32_t on);
 int slam_pf_timing(slam_pf* h, int32_t kernel, double* total_ms, int64_t* launches);
 /* slam_pf_run replays one captured hipGraph per step (default on). */
 int slam_pf_set_graphs(slam_pf* h, int32_t on);
+/* Exact cumsum of a resample step in one launch (on = default where the grid
+ * is co-resident; SLAM_ERR_ARG elsewhere) or in two; bit-identical results. */
+int slam_pf_set_scan_merged(slam_pf* h, int32_t on);
 /* external != 0: run on the caller's HIP stream (e.g. torch.cuda.current_stream();
  * NULL = the default stream).  external == 0: a private stream again. */
 int slam_pf_set_stream(slam_pf* h, void* hip_stream, int32_t external);

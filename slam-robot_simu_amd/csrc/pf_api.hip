@@ -104,6 +104,7 @@ struct slam_pf {
     // deferred normalisation (single-GPU handles): current weights = w_un / s_cur
     bool deferred = false;
     bool scan_merged = false;   // exact cumsum in one launch (co-resident grid)
+    bool scan_merged_ok = false;  // the merged launch is allowed for this handle
     double* s_cur = nullptr;
     DeferParts dp{};
     int32_t nb_part = 0;
@@ -450,7 +451,8 @@ int create_impl(const slam_pf_config* cfg, int64_t n_local, int64_t n_global, in
                                                          kScanThreads, 0) == hipSuccess &&
             hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) ==
                 hipSuccess)
-            h->scan_merged = deferred && (int64_t)h->nb_scan <= (int64_t)per_cu * cus / 2;
+            h->scan_merged_ok = deferred && (int64_t)h->nb_scan <= (int64_t)per_cu * cus / 2;
+        h->scan_merged = h->scan_merged_ok;
     }
     hipError_t e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking);
     if (e != hipSuccess) {
@@ -917,6 +919,15 @@ int slam_pf_enable_timing(slam_pf* h, int32_t on) {
 int slam_pf_set_graphs(slam_pf* h, int32_t on) {
     SLAM_ARG_CHECK(h, "slam_pf_set_graphs: NULL handle");
     h->use_graph = on != 0;
+    return SLAM_OK;
+}
+
+int slam_pf_set_scan_merged(slam_pf* h, int32_t on) {
+    SLAM_ARG_CHECK(h, "slam_pf_set_scan_merged: NULL handle");
+    SLAM_ARG_CHECK(!on || h->scan_merged_ok,
+                   "slam_pf_set_scan_merged: the merged launch needs a single-GPU handle whose "
+                   "scan grid is co-resident");
+    h->scan_merged = on != 0;
     return SLAM_OK;
 }
 

@@ -89,6 +89,7 @@ SIGNATURES = {
     "slam_pf_enable_timing": (C.c_int, [_P, C.c_int32]),
     "slam_pf_timing": (C.c_int, [_P, C.c_int32, _D, _I64]),
     "slam_pf_set_graphs": (C.c_int, [_P, C.c_int32]),
+    "slam_pf_set_scan_merged": (C.c_int, [_P, C.c_int32]),
     "slam_pf_set_stream": (C.c_int, [_P, _P, C.c_int32]),
     "slam_pf_create_shard": (C.c_int, [C.POINTER(PFConfig), C.c_int64, C.c_int64, C.c_int64,
                                        C.c_int32, _D, C.c_int, C.POINTER(_P)]),

@@ -169,6 +169,11 @@ class DeviceParticleFilter:
         self.resample_next = bool(res[k - 1].resample_next)
         return [self._res(r) for r in res] if want_results else None
 
+    def set_scan_merged(self, on=True):
+        """Exact cumsum of a resample step in one launch (default where the
+        grid is co-resident) or two; the results are bit-identical."""
+        check(self._lib.slam_pf_set_scan_merged(self._h, int(bool(on))), "slam_pf_set_scan_merged")
+
     def enable_timing(self, on=True):
         check(self._lib.slam_pf_enable_timing(self._h, int(bool(on))), "slam_pf_enable_timing")
 

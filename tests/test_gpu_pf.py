@@ -175,3 +175,33 @@ def test_device_rng_run_tracks_truth(slamhip_pf, motion):
     err = np.array([np.hypot(*(o["x_est"][:2] - x[:2])) for o, x in zip(out, xs)])
     assert np.all(np.isfinite(err)) and np.median(err) < 0.5
     assert sum(o["resampled"] for o in out) >= 1
+
+
+def test_scan_merged_matches_two_launch(slamhip_pf):
+    """The one-launch exact cumsum (co-resident grid) and the two-launch form
+    must give bit-identical runs: same seed, same resampling decisions."""
+    rs = np.random.RandomState(4)
+    n, nl, steps = 1 << 20, 100, 24
+    lm = rs.uniform(-10, 10, (nl, 2))
+    p = po.PFParams(n_particles=n, landmarks=lm, motion="velocity")
+    world = po.PFWorld(p)
+    np.random.seed(11)
+    zs = []
+    for _ in range(steps):
+        world.advance()
+        zs.append(world.observe())
+    ctl = np.tile([p.vel, p.omega], (steps, 1))
+    outs, states = [], []
+    for merged in (True, False):
+        with slamhip_pf.DeviceParticleFilter(n, lm, motion="velocity", seed=5) as d:
+            d.set_scan_merged(merged)
+            d.load_observations(np.array(zs))
+            outs.append(d.run(0, ctl))
+            states.append(d.get_state())
+    assert sum(o["resampled"] for o in outs[0]) >= 1
+    for a, b in zip(*outs):
+        np.testing.assert_array_equal(a["x_est"], b["x_est"])
+        np.testing.assert_array_equal(a["cov"], b["cov"])
+        assert a["max_idx"] == b["max_idx"] and a["resampled"] == b["resampled"]
+    for a, b in zip(*states):
+        np.testing.assert_array_equal(a, b)
