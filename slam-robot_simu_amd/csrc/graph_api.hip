@@ -37,7 +37,8 @@ struct slam_graph {
     int32_t* piv = nullptr;
     double* luout = nullptr;       // [0..2] LU, [3..4] Lanczos
     // PCG
-    double *minv = nullptr, *r = nullptr, *z = nullptr, *p = nullptr, *q = nullptr;
+    double *minv = nullptr, *r = nullptr, *z = nullptr, *p = nullptr, *p2 = nullptr;
+    double* q = nullptr;
     double* part = nullptr;
     PcgState* st = nullptr;
     hipEvent_t ev[5] = {};
@@ -160,8 +161,9 @@ int build_structure(slam_graph* h, int64_t E, const slam_graph_edge* ed) {
     GTRY(galloc(h, &h->r, n));
     GTRY(galloc(h, &h->z, n));
     GTRY(galloc(h, &h->p, n));
+    GTRY(galloc(h, &h->p2, n));
     GTRY(galloc(h, &h->q, n));
-    GTRY(galloc(h, &h->part, 2 * (int64_t)nblk(n) + 2));
+    GTRY(galloc(h, &h->part, 3 * (int64_t)nblk(n, kPcgThreads) + 3));
     GTRY(galloc(h, &h->st, 1));
     GTRY(galloc(h, &h->luout, 8));
     if (n <= kGraphDenseMax) {
@@ -246,45 +248,27 @@ int solve_dense(slam_graph* h, double* stats, bool* solved) {
     return SLAM_OK;
 }
 
-__global__ void graph_negate_kernel(const int64_t n, const double* __restrict__ b,
-                                    double* __restrict__ r) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) r[i] = -b[i];
-}
-
-// PCG on H delta = -b with block-Jacobi (large trajectories)
+// PCG on H delta = -b with block-Jacobi (large trajectories): two launches per
+// iteration, enqueued in chunks between host polls of the device state.
 int solve_pcg(slam_graph* h, double* stats, bool* solved, int32_t* iters) {
     const int64_t n = 3 * h->nt;
-    const unsigned nb = nblk(n);
+    const unsigned nb = nblk(n, kPcgThreads);
     hipLaunchKernelGGL(graph_block_inv_kernel, dim3(nblk(h->nt)), dim3(256), 0, h->stream, h->nt,
                        h->dslot, h->val, h->minv);
-    SLAM_HIP_TRY(hipMemsetAsync(h->delta, 0, n * sizeof(double), h->stream));
-    hipLaunchKernelGGL(graph_negate_kernel, dim3(nb), dim3(256), 0, h->stream, n, h->b, h->r);
-    hipLaunchKernelGGL(graph_pcg_precond_kernel, dim3(nb), dim3(256), 0, h->stream, n, h->minv,
-                       h->r, h->z, h->part, h->st, 1);
-    hipLaunchKernelGGL(graph_pcg_scalar_kernel, dim3(1), dim3(1024), 0, h->stream, (int64_t)nb,
-                       h->part, h->st, 2, h->cfg.pcg_tol, h->cfg.pcg_max_iter);
-    hipLaunchKernelGGL(graph_pcg_dir_kernel, dim3(nb), dim3(256), 0, h->stream, n, h->p, h->z,
-                       h->st, 1);
+    hipLaunchKernelGGL(graph_pcg_start_kernel, dim3(nb), dim3(kPcgThreads), 0, h->stream, n,
+                       h->minv, h->b, h->delta, h->r, h->z, h->part);
     SLAM_HIP_TRY(hipGetLastError());
     PcgState s{};
     const int chunk = 16;
-    for (int it = 0; it < h->cfg.pcg_max_iter; it += chunk) {
-        for (int k = 0; k < chunk; ++k) {
-            hipLaunchKernelGGL(graph_pcg_spmv_kernel, dim3(nb), dim3(256), 0, h->stream, n, h->rptr,
-                               h->scol, h->val, h->p, h->q, h->part, h->st);
-            hipLaunchKernelGGL(graph_pcg_scalar_kernel, dim3(1), dim3(1024), 0, h->stream,
-                               (int64_t)nb, h->part, h->st, 0, h->cfg.pcg_tol,
-                               h->cfg.pcg_max_iter);
-            hipLaunchKernelGGL(graph_pcg_axpy_kernel, dim3(nb), dim3(256), 0, h->stream, n,
-                               h->delta, h->r, h->p, h->q, h->st);
-            hipLaunchKernelGGL(graph_pcg_precond_kernel, dim3(nb), dim3(256), 0, h->stream, n,
-                               h->minv, h->r, h->z, h->part, h->st, 0);
-            hipLaunchKernelGGL(graph_pcg_scalar_kernel, dim3(1), dim3(1024), 0, h->stream,
-                               (int64_t)nb, h->part, h->st, 1, h->cfg.pcg_tol,
-                               h->cfg.pcg_max_iter);
-            hipLaunchKernelGGL(graph_pcg_dir_kernel, dim3(nb), dim3(256), 0, h->stream, n, h->p,
-                               h->z, h->st, 0);
+    for (int32_t k0 = 0;; k0 += chunk) {
+        for (int32_t k = k0; k < k0 + chunk; ++k) {
+            double* pk = (k & 1) ? h->p2 : h->p;
+            double* pprev = (k & 1) ? h->p : h->p2;
+            hipLaunchKernelGGL(graph_pcg_dir_spmv_kernel, dim3(nb), dim3(kSpmvThreads), 0,
+                               h->stream, h->nt, k, h->rptr, h->scol, h->val, h->z, pprev, pk, h->q,
+                               h->part, h->st, h->cfg.pcg_tol, h->cfg.pcg_max_iter);
+            hipLaunchKernelGGL(graph_pcg_step_kernel, dim3(nb), dim3(kPcgThreads), 0, h->stream,
+                               n, k, h->minv, pk, h->q, h->delta, h->r, h->z, h->part, h->st);
         }
         SLAM_HIP_TRY(hipGetLastError());
         SLAM_HIP_TRY(hipMemcpyAsync(&s, h->st, sizeof(PcgState), hipMemcpyDeviceToHost, h->stream));

@@ -244,6 +244,29 @@ __device__ __forceinline__ double block_sum_fixed(double v, double* sh) {
     return r;
 }
 
+template <int NT>
+__device__ __forceinline__ void block_sum2_fixed(double& a, double& b, double* sh) {
+    // two sums through one LDS round; sh holds 2 * NT / 64 doubles
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+        a += __shfl_xor(a, d, 64);
+        b += __shfl_xor(b, d, 64);
+    }
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) {
+        sh[threadIdx.x >> 6] = a;
+        sh[NT / 64 + (threadIdx.x >> 6)] = b;
+    }
+    __syncthreads();
+    a = 0.0;
+    b = 0.0;
+    for (int w = 0; w < NT / 64; ++w) {
+        a += sh[w];
+        b += sh[NT / 64 + w];
+    }
+    __syncthreads();
+}
+
 // --------------------------------------------------- dense LU (getrf)
 // One workgroup.  A (n x n row-major) is overwritten by L\U, piv[k] = row
 // swapped with k.  out: [0] = sign, [1] = sum log|u_kk|, [2] = 1 if a zero pivot.
@@ -523,154 +546,197 @@ __global__ __launch_bounds__(kGraphThreads) void graph_lanczos_kernel(
 }
 
 // ------------------------------------------------------------------ PCG
-// y = H x on the block-sparse matrix (one lane per scalar row).
-__device__ __forceinline__ double bsr_row_dot(const int64_t r3, const int64_t* rptr,
-                                              const int64_t* col, const double* val,
-                                              const double* x) {
-    const int64_t r = r3 / 3;
-    const int a = (int)(r3 - 3 * r);
-    double acc = 0.0;
-    for (int64_t s = rptr[r]; s < rptr[r + 1]; ++s) {
-        const double* v = val + s * 9 + 3 * a;
-        const double* xc = x + 3 * col[s];
-        acc = fma(v[0], xc[0], acc);
-        acc = fma(v[1], xc[1], acc);
-        acc = fma(v[2], xc[2], acc);
-    }
-    return acc;
-}
-
-// partial sums of 1024-element blocks (fixed order), finished by graph_pcg_scalar_kernel
-template <int NT>
-__device__ __forceinline__ void write_partial(double v, double* sh, double* part) {
-    const double s = block_sum_fixed<NT>(v, sh);
-    if (threadIdx.x == 0) part[blockIdx.x] = s;
-}
+// Two launches per CG iteration.  The scalar recurrences (alpha, beta, the
+// convergence test) are folded redundantly by every workgroup from the
+// previous launch's per-workgroup partials, in one fixed order, so all
+// workgroups take identical decisions without a one-workgroup scalar launch
+// between the vector passes.  A workgroup covers 64 whole poses (192 scalar
+// rows), so the block-Jacobi preconditioner stays workgroup-local.
+constexpr int kPcgThreads = 192;
 
 struct PcgState {
-    double rho, alpha, beta, rr0, rr;
+    double rho[2];                  // rho_k = r_k . z_k in slot k & 1
+    double rr0, rr;
     int32_t iter, done, status, pad;
 };
 
-// q = H p ; partial p.q
-__global__ __launch_bounds__(256) void graph_pcg_spmv_kernel(
-    const int64_t n, const int64_t* __restrict__ rptr, const int64_t* __restrict__ col,
-    const double* __restrict__ val, const double* __restrict__ p, double* __restrict__ q,
-    double* __restrict__ part, const PcgState* __restrict__ st) {
-    __shared__ double sh[4];
-    if (st->done) return;
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    double pq = 0.0;
-    if (i < n) {
-        const double v = bsr_row_dot(i, rptr, col, val, p);
-        q[i] = v;
-        pq = v * p[i];
-    }
-    write_partial<256>(pq, sh, part);
+// partial arrays: [0, nb) p.q ; [nb, 2nb) r.z ; [2nb, 3nb) r.r
+__device__ __forceinline__ double pcg_fold(const double* __restrict__ part, const int64_t nb,
+                                           double* sh) {
+    double a = 0.0;
+    for (int64_t k = threadIdx.x; k < nb; k += kPcgThreads) a += part[k];
+    return block_sum_fixed<kPcgThreads>(a, sh);
 }
 
-// z = M^-1 r (3x3 block inverses), partial r.z and r.r
-__global__ __launch_bounds__(256) void graph_pcg_precond_kernel(
-    const int64_t n, const double* __restrict__ minv, const double* __restrict__ r,
-    double* __restrict__ z, double* __restrict__ part2, const PcgState* __restrict__ st,
-    const int32_t first) {
-    __shared__ double sh[4];
-    if (!first && st->done) return;
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+__device__ __forceinline__ bool pcg_lead() { return blockIdx.x == 0 && threadIdx.x == 0; }
+
+// x = 0, r = -b, z = M^-1 r ; partials r.z, r.r
+__global__ __launch_bounds__(kPcgThreads) void graph_pcg_start_kernel(
+    const int64_t n, const double* __restrict__ minv, const double* __restrict__ b,
+    double* __restrict__ x, double* __restrict__ r, double* __restrict__ z,
+    double* __restrict__ part) {
+    __shared__ double sh[2 * kPcgThreads / 64];
+    __shared__ double rs[kPcgThreads];
+    const int64_t nb = gridDim.x;
+    const int64_t i = (int64_t)blockIdx.x * kPcgThreads + threadIdx.x;
+    double ri = 0.0;
+    if (i < n) {
+        ri = -b[i];
+        r[i] = ri;
+        x[i] = 0.0;
+    }
+    rs[threadIdx.x] = ri;
+    __syncthreads();
     double rz = 0.0, rr = 0.0;
     if (i < n) {
-        const int64_t b = i / 3;
-        const int a = (int)(i - 3 * b);
-        const double* m = minv + b * 9 + 3 * a;
-        const double* rb = r + 3 * b;
-        double acc = m[0] * rb[0];
-        acc = fma(m[1], rb[1], acc);
-        acc = fma(m[2], rb[2], acc);
-        z[i] = acc;
-        rz = acc * r[i];
-        rr = r[i] * r[i];
+        const int a = (int)(i % 3);
+        const double* m = minv + (i - a) * 3 + 3 * a;
+        const double* rb = rs + threadIdx.x - a;
+        double zi = m[0] * rb[0];
+        zi = fma(m[1], rb[1], zi);
+        zi = fma(m[2], rb[2], zi);
+        z[i] = zi;
+        rz = zi * ri;
+        rr = ri * ri;
     }
-    const double s1 = block_sum_fixed<256>(rz, sh);
-    const double s2 = block_sum_fixed<256>(rr, sh);
+    block_sum2_fixed<kPcgThreads>(rz, rr, sh);
     if (threadIdx.x == 0) {
-        part2[2 * blockIdx.x] = s1;
-        part2[2 * blockIdx.x + 1] = s2;
+        part[nb + blockIdx.x] = rz;
+        part[2 * nb + blockIdx.x] = rr;
     }
 }
 
-// x += alpha p ; r -= alpha q
-__global__ __launch_bounds__(256) void graph_pcg_axpy_kernel(const int64_t n,
-                                                             double* __restrict__ x,
-                                                             double* __restrict__ r,
-                                                             const double* __restrict__ p,
-                                                             const double* __restrict__ q,
-                                                             const PcgState* __restrict__ st) {
+// iteration k, first launch: rho_k and the convergence test from the r.z / r.r
+// partials, p_k = z + beta p_{k-1} (formed on the fly for the gathered
+// columns, written for the own rows into the other ping-pong buffer),
+// q = H p_k ; partial p.q.  SpMV: a group of 4 lanes per block row, each lane
+// one whole 3x3 block at a time (72 contiguous bytes, adjacent lanes adjacent
+// blocks), the three row sums folded over the group by a fixed xor tree.
+constexpr int kSpmvThreads = 256, kSpmvGroup = 4;    // 64 poses per workgroup
+static_assert(kSpmvThreads / kSpmvGroup * 3 == kPcgThreads, "same workgroup count");
+
+__global__ __launch_bounds__(kSpmvThreads) void graph_pcg_dir_spmv_kernel(
+    const int64_t nt, const int32_t k, const int64_t* __restrict__ rptr,
+    const int64_t* __restrict__ col, const double* __restrict__ val,
+    const double* __restrict__ z, const double* __restrict__ pold, double* __restrict__ pnew,
+    double* __restrict__ q, double* __restrict__ part, PcgState* __restrict__ st,
+    const double tol, const int32_t max_iter) {
+    __shared__ double sh[2 * kSpmvThreads / 64];
+    if (k > 0 && st->done) return;
+    const int64_t nb = gridDim.x;
+    double rz = 0.0, rr = 0.0;
+    for (int64_t j = threadIdx.x; j < nb; j += kSpmvThreads) {
+        rz += part[nb + j];
+        rr += part[2 * nb + j];
+    }
+    block_sum2_fixed<kSpmvThreads>(rz, rr, sh);
+    double beta = 0.0;
+    int status = 0;
+    if (k == 0) {
+        if (rr == 0.0) status = 1;
+    } else {
+        if (rr <= tol * tol * st->rr0) status = 1;
+        else if (k >= max_iter) status = 3;
+        beta = rz / st->rho[(k - 1) & 1];
+    }
+    if (pcg_lead()) {
+        st->rho[k & 1] = rz;
+        st->rr = rr;
+        st->iter = k;
+        if (k == 0) st->rr0 = rr;
+        st->status = status;
+        st->done = status != 0;
+    }
+    if (status) return;
+    const int g = threadIdx.x & (kSpmvGroup - 1);
+    const int64_t rw = (int64_t)blockIdx.x * (kSpmvThreads / kSpmvGroup) + threadIdx.x / kSpmvGroup;
+    double a0 = 0.0, a1 = 0.0, a2 = 0.0;
+    if (rw < nt) {
+        const int64_t s1 = rptr[rw + 1];
+        for (int64_t s = rptr[rw] + g; s < s1; s += kSpmvGroup) {
+            const double* v = val + s * 9;
+            const int64_t c = 3 * col[s];
+            double p0 = z[c], p1 = z[c + 1], p2 = z[c + 2];
+            if (k > 0) {
+                p0 = fma(beta, pold[c], p0);
+                p1 = fma(beta, pold[c + 1], p1);
+                p2 = fma(beta, pold[c + 2], p2);
+            }
+            a0 = fma(v[0], p0, a0);
+            a0 = fma(v[1], p1, a0);
+            a0 = fma(v[2], p2, a0);
+            a1 = fma(v[3], p0, a1);
+            a1 = fma(v[4], p1, a1);
+            a1 = fma(v[5], p2, a1);
+            a2 = fma(v[6], p0, a2);
+            a2 = fma(v[7], p1, a2);
+            a2 = fma(v[8], p2, a2);
+        }
+    }
+#pragma unroll
+    for (int d = 1; d < kSpmvGroup; d <<= 1) {
+        a0 += __shfl_xor(a0, d, 64);
+        a1 += __shfl_xor(a1, d, 64);
+        a2 += __shfl_xor(a2, d, 64);
+    }
+    double pq = 0.0;
+    if (rw < nt && g < 3) {
+        const double acc = (g == 0) ? a0 : (g == 1) ? a1 : a2;
+        const int64_t i = 3 * rw + g;
+        const double pi = (k > 0) ? fma(beta, pold[i], z[i]) : z[i];
+        pnew[i] = pi;
+        q[i] = acc;
+        pq = acc * pi;
+    }
+    pq = block_sum_fixed<kSpmvThreads>(pq, sh);
+    if (threadIdx.x == 0) part[blockIdx.x] = pq;
+}
+
+// iteration k, second launch: alpha = rho_k / p.q (curvature gate), x += alpha p,
+// r -= alpha q, z = M^-1 r ; partials r.z, r.r
+__global__ __launch_bounds__(kPcgThreads) void graph_pcg_step_kernel(
+    const int64_t n, const int32_t k, const double* __restrict__ minv,
+    const double* __restrict__ p, const double* __restrict__ q, double* __restrict__ x,
+    double* __restrict__ r, double* __restrict__ z, double* __restrict__ part,
+    PcgState* __restrict__ st) {
+    __shared__ double sh[2 * kPcgThreads / 64];
+    __shared__ double rs[kPcgThreads];
     if (st->done) return;
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const double a = st->alpha;
-    x[i] = fma(a, p[i], x[i]);
-    r[i] = fma(-a, q[i], r[i]);
-}
-
-// p = z + beta p
-__global__ __launch_bounds__(256) void graph_pcg_dir_kernel(const int64_t n,
-                                                            double* __restrict__ p,
-                                                            const double* __restrict__ z,
-                                                            const PcgState* __restrict__ st,
-                                                            const int32_t first) {
-    if (!first && st->done) return;
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    p[i] = first ? z[i] : fma(st->beta, p[i], z[i]);
-}
-
-// one workgroup: fold the partials in block order and update the scalars.
-// mode 0: alpha = rho / p.q ; mode 1: rho' = r.z, beta, convergence ; mode 2: init.
-__global__ __launch_bounds__(1024) void graph_pcg_scalar_kernel(const int64_t nparts,
-                                                                const double* __restrict__ part,
-                                                                PcgState* __restrict__ st,
-                                                                const int32_t mode,
-                                                                const double tol,
-                                                                const int32_t max_iter) {
-    __shared__ double sh[16];
-    if (mode != 2 && st->done) return;
-    const int stride = (mode == 0) ? 1 : 2;
-    double a = 0.0, b = 0.0;
-    for (int64_t k = threadIdx.x; k < nparts; k += blockDim.x) {
-        a += part[stride * k];
-        if (stride == 2) b += part[2 * k + 1];
-    }
-    a = block_sum_fixed<1024>(a, sh);
-    b = block_sum_fixed<1024>(b, sh);
-    if (threadIdx.x != 0) return;
-    if (mode == 0) {
-        if (!(a > 0.0)) {            // not positive definite along p
+    const int64_t nb = gridDim.x;
+    const double pq = pcg_fold(part, nb, sh);
+    if (!(pq > 0.0)) {                  // not positive definite along p
+        if (pcg_lead()) {
             st->done = 1;
             st->status = 2;
-            return;
         }
-        st->alpha = st->rho / a;
-    } else if (mode == 1) {
-        st->beta = a / st->rho;
-        st->rho = a;
-        st->rr = b;
-        st->iter += 1;
-        if (b <= tol * tol * st->rr0) {
-            st->done = 1;
-            st->status = 1;
-        } else if (st->iter >= max_iter) {
-            st->done = 1;
-            st->status = 3;
-        }
-    } else {
-        st->rho = a;
-        st->rr0 = b;
-        st->rr = b;
-        st->iter = 0;
-        st->status = 0;
-        st->done = (b == 0.0) ? 1 : 0;
-        if (b == 0.0) st->status = 1;
+        return;
+    }
+    const double alpha = st->rho[k & 1] / pq;
+    const int64_t i = (int64_t)blockIdx.x * kPcgThreads + threadIdx.x;
+    double ri = 0.0;
+    if (i < n) {
+        x[i] = fma(alpha, p[i], x[i]);
+        ri = fma(-alpha, q[i], r[i]);
+        r[i] = ri;
+    }
+    rs[threadIdx.x] = ri;
+    __syncthreads();
+    double rz = 0.0, rr = 0.0;
+    if (i < n) {
+        const int a = (int)(i % 3);
+        const double* m = minv + (i - a) * 3 + 3 * a;
+        const double* rb = rs + threadIdx.x - a;
+        double zi = m[0] * rb[0];
+        zi = fma(m[1], rb[1], zi);
+        zi = fma(m[2], rb[2], zi);
+        z[i] = zi;
+        rz = zi * ri;
+        rr = ri * ri;
+    }
+    block_sum2_fixed<kPcgThreads>(rz, rr, sh);
+    if (threadIdx.x == 0) {
+        part[nb + blockIdx.x] = rz;
+        part[2 * nb + blockIdx.x] = rr;
     }
 }
 
