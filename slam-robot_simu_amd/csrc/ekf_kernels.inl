@@ -408,11 +408,19 @@ __global__ __launch_bounds__(kEksThreads) SLAM_EKS_ATTR void eks_rank_update_ker
             for (int r = 0; r < 4; ++r) {
                 const int64_t gi = r0 + wr + 16 * a + lk + 4 * r;
                 const int64_t gj = c0 + wc + 16 * b + lr;
+#ifdef EKS_PROBE_NOMEM
+                acc[a][b][r] = (double)(gi ^ gj);
+#else
                 acc[a][b][r] = (gi < n && gj < n && (!diag || gj <= gi)) ? P[gi * ld + gj] : 0.0;
+#endif
             }
     const double* ksrc = kg + r0 * M;
     const double* hsrc = pht + c0 * M;
+#ifdef EKS_PROBE_NOMFMA
+    for (int kc = 0; kc < 0; kc += kEksKC) {
+#else
     for (int kc = 0; kc < M; kc += kEksKC) {
+#endif
         const int kw = min(kEksKC, M - kc);             // multiple of 4
         __syncthreads();
 #pragma unroll
@@ -445,7 +453,11 @@ __global__ __launch_bounds__(kEksThreads) SLAM_EKS_ATTR void eks_rank_update_ker
             for (int r = 0; r < 4; ++r) {
                 const int64_t gi = r0 + wr + 16 * a + lk + 4 * r;
                 const int64_t gj = c0 + wc + 16 * b + lr;
+#ifdef EKS_PROBE_NOMEM
+                if (acc[a][b][r] == 1.2345) P[gi * ld + gj] = acc[a][b][r];
+#else
                 if (gi < n && gj < n && (!diag || gj <= gi)) P[gi * ld + gj] = acc[a][b][r];
+#endif
             }
 }
 

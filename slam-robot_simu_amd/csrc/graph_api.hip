@@ -298,8 +298,10 @@ int do_update(slam_graph* h, double* stats) {
     else GTRY(solve_pcg(h, stats, &solved, &iters));
     SLAM_HIP_TRY(hipEventRecord(h->ev[3], h->stream));
     if (solved) {
-        hipLaunchKernelGGL(graph_pose_update_kernel, dim3(1), dim3(1024), 0, h->stream, h->nt,
-                           h->times, h->delta, h->poses, h->dsum);
+        hipLaunchKernelGGL(graph_pose_update_kernel, dim3(nblk(h->nt)), dim3(256), 0, h->stream,
+                           h->nt, h->times, h->delta, h->poses, h->part);
+        hipLaunchKernelGGL(graph_dsum_kernel, dim3(1), dim3(1024), 0, h->stream,
+                           (int64_t)nblk(h->nt), h->part, h->dsum);
         SLAM_HIP_TRY(hipGetLastError());
         SLAM_HIP_TRY(hipMemcpyAsync(&stats[1], h->dsum, sizeof(double), hipMemcpyDeviceToHost,
                                     h->stream));

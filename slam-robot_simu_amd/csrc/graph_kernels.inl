@@ -560,12 +560,28 @@ struct PcgState {
     int32_t iter, done, status, pad;
 };
 
-// partial arrays: [0, nb) p.q ; [nb, 2nb) r.z ; [2nb, 3nb) r.r
+// partial arrays: [0, nb) p.q ; [nb, 2nb) r.z ; [2nb, 3nb) r.r.  The strided
+// sequential sum of each lane is read four loads at a time (missing terms
+// add +0.0), the same order as the plain loop.
+template <int NT>
+__device__ __forceinline__ double pcg_fold_lane(const double* __restrict__ part, const int64_t nb) {
+    double a = 0.0;
+    for (int64_t k = threadIdx.x; k < nb; k += 4 * NT) {
+        const double v0 = part[k];
+        const double v1 = (k + NT < nb) ? part[k + NT] : 0.0;
+        const double v2 = (k + 2 * NT < nb) ? part[k + 2 * NT] : 0.0;
+        const double v3 = (k + 3 * NT < nb) ? part[k + 3 * NT] : 0.0;
+        a += v0;
+        a += v1;
+        a += v2;
+        a += v3;
+    }
+    return a;
+}
+
 __device__ __forceinline__ double pcg_fold(const double* __restrict__ part, const int64_t nb,
                                            double* sh) {
-    double a = 0.0;
-    for (int64_t k = threadIdx.x; k < nb; k += kPcgThreads) a += part[k];
-    return block_sum_fixed<kPcgThreads>(a, sh);
+    return block_sum_fixed<kPcgThreads>(pcg_fold_lane<kPcgThreads>(part, nb), sh);
 }
 
 __device__ __forceinline__ bool pcg_lead() { return blockIdx.x == 0 && threadIdx.x == 0; }
@@ -609,11 +625,49 @@ __global__ __launch_bounds__(kPcgThreads) void graph_pcg_start_kernel(
 // iteration k, first launch: rho_k and the convergence test from the r.z / r.r
 // partials, p_k = z + beta p_{k-1} (formed on the fly for the gathered
 // columns, written for the own rows into the other ping-pong buffer),
-// q = H p_k ; partial p.q.  SpMV: a group of 4 lanes per block row, each lane
+// q = H p_k ; partial p.q.  SpMV: a group of 8 lanes per block row, each lane
 // one whole 3x3 block at a time (72 contiguous bytes, adjacent lanes adjacent
 // blocks), the three row sums folded over the group by a fixed xor tree.
-constexpr int kSpmvThreads = 256, kSpmvGroup = 4;    // 64 poses per workgroup
+constexpr int kSpmvThreads = 512, kSpmvGroup = 8;    // 64 poses per workgroup
 static_assert(kSpmvThreads / kSpmvGroup * 3 == kPcgThreads, "same workgroup count");
+
+// one 3x3 block of a row with its gathered z / p_{k-1} columns
+struct PcgBlock {
+    double v[9], zc[3], pc[3];
+};
+
+__device__ __forceinline__ void pcg_load_block(PcgBlock& B, const int64_t s, const int32_t k,
+                                               const int64_t* __restrict__ col,
+                                               const double* __restrict__ val,
+                                               const double* __restrict__ z,
+                                               const double* __restrict__ pold) {
+    const double* v = val + s * 9;
+#pragma unroll
+    for (int j = 0; j < 9; ++j) B.v[j] = v[j];
+    const int64_t c = 3 * col[s];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+        B.zc[j] = z[c + j];
+        B.pc[j] = (k > 0) ? pold[c + j] : 0.0;
+    }
+}
+
+__device__ __forceinline__ void pcg_apply_block(const PcgBlock& B, const int32_t k,
+                                                const double beta, double& a0, double& a1,
+                                                double& a2) {
+    double p[3];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) p[j] = (k > 0) ? fma(beta, B.pc[j], B.zc[j]) : B.zc[j];
+    a0 = fma(B.v[0], p[0], a0);
+    a0 = fma(B.v[1], p[1], a0);
+    a0 = fma(B.v[2], p[2], a0);
+    a1 = fma(B.v[3], p[0], a1);
+    a1 = fma(B.v[4], p[1], a1);
+    a1 = fma(B.v[5], p[2], a1);
+    a2 = fma(B.v[6], p[0], a2);
+    a2 = fma(B.v[7], p[1], a2);
+    a2 = fma(B.v[8], p[2], a2);
+}
 
 __global__ __launch_bounds__(kSpmvThreads) void graph_pcg_dir_spmv_kernel(
     const int64_t nt, const int32_t k, const int64_t* __restrict__ rptr,
@@ -624,11 +678,8 @@ __global__ __launch_bounds__(kSpmvThreads) void graph_pcg_dir_spmv_kernel(
     __shared__ double sh[2 * kSpmvThreads / 64];
     if (k > 0 && st->done) return;
     const int64_t nb = gridDim.x;
-    double rz = 0.0, rr = 0.0;
-    for (int64_t j = threadIdx.x; j < nb; j += kSpmvThreads) {
-        rz += part[nb + j];
-        rr += part[2 * nb + j];
-    }
+    double rz = pcg_fold_lane<kSpmvThreads>(part + nb, nb);
+    double rr = pcg_fold_lane<kSpmvThreads>(part + 2 * nb, nb);
     block_sum2_fixed<kSpmvThreads>(rz, rr, sh);
     double beta = 0.0;
     int status = 0;
@@ -650,27 +701,15 @@ __global__ __launch_bounds__(kSpmvThreads) void graph_pcg_dir_spmv_kernel(
     if (status) return;
     const int g = threadIdx.x & (kSpmvGroup - 1);
     const int64_t rw = (int64_t)blockIdx.x * (kSpmvThreads / kSpmvGroup) + threadIdx.x / kSpmvGroup;
+    const bool own = rw < nt && g < 3;
+    const int64_t i = 3 * rw + g;
     double a0 = 0.0, a1 = 0.0, a2 = 0.0;
     if (rw < nt) {
         const int64_t s1 = rptr[rw + 1];
         for (int64_t s = rptr[rw] + g; s < s1; s += kSpmvGroup) {
-            const double* v = val + s * 9;
-            const int64_t c = 3 * col[s];
-            double p0 = z[c], p1 = z[c + 1], p2 = z[c + 2];
-            if (k > 0) {
-                p0 = fma(beta, pold[c], p0);
-                p1 = fma(beta, pold[c + 1], p1);
-                p2 = fma(beta, pold[c + 2], p2);
-            }
-            a0 = fma(v[0], p0, a0);
-            a0 = fma(v[1], p1, a0);
-            a0 = fma(v[2], p2, a0);
-            a1 = fma(v[3], p0, a1);
-            a1 = fma(v[4], p1, a1);
-            a1 = fma(v[5], p2, a1);
-            a2 = fma(v[6], p0, a2);
-            a2 = fma(v[7], p1, a2);
-            a2 = fma(v[8], p2, a2);
+            PcgBlock B;
+            pcg_load_block(B, s, k, col, val, z, pold);
+            pcg_apply_block(B, k, beta, a0, a1, a2);
         }
     }
 #pragma unroll
@@ -680,9 +719,8 @@ __global__ __launch_bounds__(kSpmvThreads) void graph_pcg_dir_spmv_kernel(
         a2 += __shfl_xor(a2, d, 64);
     }
     double pq = 0.0;
-    if (rw < nt && g < 3) {
+    if (own) {
         const double acc = (g == 0) ? a0 : (g == 1) ? a1 : a2;
-        const int64_t i = 3 * rw + g;
         const double pi = (k > 0) ? fma(beta, pold[i], z[i]) : z[i];
         pnew[i] = pi;
         q[i] = acc;
@@ -701,6 +739,20 @@ __global__ __launch_bounds__(kPcgThreads) void graph_pcg_step_kernel(
     PcgState* __restrict__ st) {
     __shared__ double sh[2 * kPcgThreads / 64];
     __shared__ double rs[kPcgThreads];
+    // own operands first: their loads run under the p.q fold
+    const int64_t i = (int64_t)blockIdx.x * kPcgThreads + threadIdx.x;
+    double xi = 0.0, ri = 0.0, pi = 0.0, qi = 0.0, m0 = 0.0, m1 = 0.0, m2 = 0.0;
+    if (i < n) {
+        xi = x[i];
+        ri = r[i];
+        pi = p[i];
+        qi = q[i];
+        const int a = (int)(i % 3);
+        const double* m = minv + (i - a) * 3 + 3 * a;
+        m0 = m[0];
+        m1 = m[1];
+        m2 = m[2];
+    }
     if (st->done) return;
     const int64_t nb = gridDim.x;
     const double pq = pcg_fold(part, nb, sh);
@@ -712,23 +764,19 @@ __global__ __launch_bounds__(kPcgThreads) void graph_pcg_step_kernel(
         return;
     }
     const double alpha = st->rho[k & 1] / pq;
-    const int64_t i = (int64_t)blockIdx.x * kPcgThreads + threadIdx.x;
-    double ri = 0.0;
     if (i < n) {
-        x[i] = fma(alpha, p[i], x[i]);
-        ri = fma(-alpha, q[i], r[i]);
+        x[i] = fma(alpha, pi, xi);
+        ri = fma(-alpha, qi, ri);
         r[i] = ri;
     }
     rs[threadIdx.x] = ri;
     __syncthreads();
     double rz = 0.0, rr = 0.0;
     if (i < n) {
-        const int a = (int)(i % 3);
-        const double* m = minv + (i - a) * 3 + 3 * a;
-        const double* rb = rs + threadIdx.x - a;
-        double zi = m[0] * rb[0];
-        zi = fma(m[1], rb[1], zi);
-        zi = fma(m[2], rb[2], zi);
+        const double* rb = rs + threadIdx.x - (int)(i % 3);
+        double zi = m0 * rb[0];
+        zi = fma(m1, rb[1], zi);
+        zi = fma(m2, rb[2], zi);
         z[i] = zi;
         rz = zi * ri;
         rr = ri * ri;
@@ -751,15 +799,16 @@ __global__ __launch_bounds__(256) void graph_block_inv_kernel(const int64_t nb,
 }
 
 // ------------------------------------------------------- pose update
-// updateEstPose :499-502 and Σδ² (:513, fixed-order), one workgroup.
-__global__ __launch_bounds__(1024) void graph_pose_update_kernel(const int64_t nt,
-                                                                 const int64_t* __restrict__ times,
-                                                                 const double* __restrict__ delta,
-                                                                 double* __restrict__ poses,
-                                                                 double* __restrict__ dsum) {
-    __shared__ double sh[16];
+// updateEstPose :499-502 and the per-workgroup partials of Σδ² (:513), one lane per pose.
+__global__ __launch_bounds__(256) void graph_pose_update_kernel(const int64_t nt,
+                                                                const int64_t* __restrict__ times,
+                                                                const double* __restrict__ delta,
+                                                                double* __restrict__ poses,
+                                                                double* __restrict__ part) {
+    __shared__ double sh[4];
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
     double s = 0.0;
-    for (int64_t i = threadIdx.x; i < nt; i += blockDim.x) {
+    if (i < nt) {
         double* p = poses + 3 * times[i];
         const double d0 = delta[3 * i], d1 = delta[3 * i + 1], d2 = delta[3 * i + 2];
         p[0] = p[0] + d0;
@@ -769,6 +818,17 @@ __global__ __launch_bounds__(1024) void graph_pose_update_kernel(const int64_t n
         s = fma(d1, d1, s);
         s = fma(d2, d2, s);
     }
+    s = block_sum_fixed<256>(s, sh);
+    if (threadIdx.x == 0) part[blockIdx.x] = s;
+}
+
+// Σδ² from the pose-update partials, fixed order, one workgroup
+__global__ __launch_bounds__(1024) void graph_dsum_kernel(const int64_t nparts,
+                                                         const double* __restrict__ part,
+                                                         double* __restrict__ dsum) {
+    __shared__ double sh[16];
+    double s = 0.0;
+    for (int64_t k = threadIdx.x; k < nparts; k += 1024) s += part[k];
     s = block_sum_fixed<1024>(s, sh);
     if (threadIdx.x == 0) *dsum = s;
 }
