@@ -28,6 +28,7 @@ struct slam_ekfslam {
     slam_ekfslam_config cfg;
     int device = 0;
     int64_t n_lm = 0, n = 0, ld = 0, n_pad = 0;
+    int64_t pipe_grid = 0;         // persistent rank-update grid (resident workgroups, x8)
     hipStream_t stream = nullptr;
     double* P = nullptr;           // n x ld, lower triangle current
     double* mu = nullptr;          // n
@@ -147,9 +148,18 @@ int eks_update(slam_ekfslam* h, int32_t k, const int64_t* ids, const double* obs
     SLAM_HIP_TRY(hipEventRecord(h->ev[3], h->stream));
     const int64_t nt = h->n_pad / kEksTile;
     const int64_t tiles = nt * (nt + 1) / 2;
-    const int64_t grid = (tiles + 7) / 8 * 8;
-    hipLaunchKernelGGL(eks_rank_update_kernel, dim3((unsigned)grid), dim3(kEksThreads), 0,
-                       h->stream, h->P, h->n, h->ld, h->kg, h->pht, M, tiles);
+#ifndef SLAM_EKS_PIPE
+#define SLAM_EKS_PIPE 1
+#endif
+    if (SLAM_EKS_PIPE && h->pipe_grid > 0 && M <= kEksPipeK) {
+        hipLaunchKernelGGL(eks_rank_update_pipelined_kernel, dim3((unsigned)h->pipe_grid),
+                           dim3(kEksThreads), 0, h->stream, h->P, h->n, h->ld, h->kg, h->pht, M,
+                           tiles);
+    } else {
+        const int64_t grid = (tiles + 7) / 8 * 8;
+        hipLaunchKernelGGL(eks_rank_update_kernel, dim3((unsigned)grid), dim3(kEksThreads), 0,
+                           h->stream, h->P, h->n, h->ld, h->kg, h->pht, M, tiles);
+    }
     SLAM_HIP_TRY(hipEventRecord(h->ev[4], h->stream));
     SLAM_HIP_TRY(hipGetLastError());
     return SLAM_OK;
@@ -327,12 +337,27 @@ int slam_ekfslam_create(const slam_ekfslam_config* cfg, int64_t n_landmarks, int
     h->device = device;
     h->n_lm = n_landmarks;
     h->n = 3 + 3 * n_landmarks;
-    h->ld = (h->n + 7) / 8 * 8;
+    // rows start on 128-byte lines: a tile row segment (16 lanes x 8 B) is one line
+#ifndef SLAM_EKS_LD_ALIGN
+#define SLAM_EKS_LD_ALIGN 16
+#endif
+#ifndef SLAM_EKS_LD_SKEW
+#define SLAM_EKS_LD_SKEW 0
+#endif
+    h->ld = (h->n + SLAM_EKS_LD_ALIGN - 1) / SLAM_EKS_LD_ALIGN * SLAM_EKS_LD_ALIGN + SLAM_EKS_LD_SKEW;
     h->n_pad = (h->n + kEksTile - 1) / kEksTile * kEksTile;
     auto bail = [&](int rc) {
         slam_ekfslam_destroy(h);
         return rc;
     };
+    {
+        int per_cu = 0, cus = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, eks_rank_update_pipelined_kernel,
+                                                         kEksThreads, 0) == hipSuccess &&
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) ==
+                hipSuccess)
+            h->pipe_grid = (int64_t)per_cu * cus / 8 * 8;
+    }
     const size_t pbytes = (size_t)h->n * h->ld * sizeof(double);
     const size_t rows = (size_t)h->n_pad * kEksMaxM;
     if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess ||

@@ -479,4 +479,175 @@ __global__ __launch_bounds__(256) void eks_diag_kernel(double* __restrict__ P, c
     if (i < n) P[i * ld + i] = dg[i];
 }
 
+
+// ---------------------------------------------------------------------------
+// Persistent, software-pipelined form of the same update for m <= 64 (the C4
+// case): a workgroup walks the tiles of its XCD's band with a fixed stride and
+// stages the whole k-range of K / PH^T in LDS at once (133 KB: one workgroup
+// per CU, 2 waves per SIMD, up to 256 registers per lane).  While the MFMAs of
+// tile t run, the P tile and the K / PH^T rows of tile t+1 are already in
+// flight into a second register set.  The MFMA sequence per tile (k ascending
+// in steps of 4) is the one of eks_rank_update_kernel: identical results.
+constexpr int kEksPipeK = 64;
+constexpr int kEksPipeKS = kEksPipeK + 1;
+typedef double eks_d4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ void eks_tile_rc(const int64_t L, int64_t& ti, int64_t& tj) {
+    ti = (int64_t)((sqrt(8.0 * (double)L + 1.0) - 1.0) * 0.5);
+    while (ti * (ti + 1) / 2 > L) --ti;
+    while ((ti + 1) * (ti + 2) / 2 <= L) ++ti;
+    tj = L - ti * (ti + 1) / 2;
+}
+
+__device__ __forceinline__ void eks_tile_load(eks_d4 (&t)[2][4], const double* __restrict__ P,
+                                              const int64_t n, const int64_t ld, const int64_t r0,
+                                              const int64_t c0, const bool diag, const int wr,
+                                              const int wc, const int lr, const int lk) {
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int64_t gi = r0 + wr + 16 * a + lk + 4 * r;
+                const int64_t gj = c0 + wc + 16 * b + lr;
+                t[a][b][r] = (gi < n && gj < n && (!diag || gj <= gi)) ? P[gi * ld + gj] : 0.0;
+            }
+}
+
+constexpr int kEksPipePer = kEksTile * kEksPipeK / kEksThreads;     // 16 per lane and operand
+
+__device__ __forceinline__ void eks_stage_load(double (&kv)[kEksPipePer], double (&hv)[kEksPipePer],
+                                               const double* __restrict__ kg,
+                                               const double* __restrict__ pht, const int32_t M,
+                                               const int64_t r0, const int64_t c0) {
+#pragma unroll
+    for (int s = 0; s < kEksPipePer; ++s) {
+        const int idx = threadIdx.x + s * kEksThreads;
+        const int r = idx / kEksPipeK, q = idx % kEksPipeK;
+        const bool ok = q < M;
+        kv[s] = ok ? -kg[(r0 + r) * M + q] : 0.0;       // K staged negated
+        hv[s] = ok ? pht[(c0 + r) * M + q] : 0.0;
+    }
+}
+
+__device__ __forceinline__ void eks_stage_store(const double (&kv)[kEksPipePer],
+                                                const double (&hv)[kEksPipePer], double* Ks,
+                                                double* Hs) {
+#pragma unroll
+    for (int s = 0; s < kEksPipePer; ++s) {
+        const int idx = threadIdx.x + s * kEksThreads;
+        const int r = idx / kEksPipeK, q = idx % kEksPipeK;
+        Ks[r * kEksPipeKS + q] = kv[s];
+        Hs[r * kEksPipeKS + q] = hv[s];
+    }
+}
+
+__device__ __forceinline__ void eks_frag_load(double (&fa)[2], double (&fb)[4], const double* Ks,
+                                              const double* Hs, const int k0, const int wr,
+                                              const int wc, const int lr, const int lk) {
+#pragma unroll
+    for (int a = 0; a < 2; ++a) fa[a] = Ks[(wr + 16 * a + lr) * kEksPipeKS + k0 + lk];
+#pragma unroll
+    for (int b = 0; b < 4; ++b) fb[b] = Hs[(wc + 16 * b + lr) * kEksPipeKS + k0 + lk];
+}
+
+__device__ __forceinline__ void eks_frag_mfma(eks_d4 (&acc)[2][4], const double (&fa)[2],
+                                              const double (&fb)[4]) {
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b)
+            acc[a][b] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[a], fb[b], acc[a][b], 0, 0, 0);
+}
+
+__global__ __launch_bounds__(kEksThreads) __attribute__((amdgpu_waves_per_eu(2)))
+void eks_rank_update_pipelined_kernel(double* __restrict__ P, const int64_t n, const int64_t ld,
+                                      const double* __restrict__ kg,
+                                      const double* __restrict__ pht, const int32_t M,
+                                      const int64_t n_tiles) {
+    __shared__ double Ks[kEksTile * kEksPipeKS];
+    __shared__ double Hs[kEksTile * kEksPipeKS];
+    const int64_t per_xcd = (n_tiles + 7) / 8;
+    const int64_t xcd = blockIdx.x % 8, stride = gridDim.x / 8;
+    const int64_t Lend = min(n_tiles, (xcd + 1) * per_xcd);
+    int64_t L = xcd * per_xcd + blockIdx.x / 8;
+    if (L >= Lend) return;
+    const int tid = threadIdx.x;
+    const int lane = tid & 63, wave = tid >> 6;
+    const int wr = (wave >> 1) * 32, wc = (wave & 1) * 64;
+    const int lr = lane & 15, lk = lane >> 4;
+    int64_t ti, tj;
+    eks_tile_rc(L, ti, tj);
+    eks_d4 acc[2][4], pre[2][4];
+    double kv[kEksPipePer], hv[kEksPipePer];
+    eks_stage_load(kv, hv, kg, pht, M, ti * kEksTile, tj * kEksTile);
+    eks_tile_load(acc, P, n, ld, ti * kEksTile, tj * kEksTile, ti == tj, wr, wc, lr, lk);
+    eks_stage_store(kv, hv, Ks, Hs);
+    __syncthreads();
+    for (;;) {
+        const int64_t r0 = ti * kEksTile, c0 = tj * kEksTile;
+        const bool diag = (ti == tj);
+        const int64_t Ln = L + stride;
+        const bool more = Ln < Lend;
+        int64_t tin = 0, tjn = 0;
+        if (more) {
+            eks_tile_rc(Ln, tin, tjn);
+            eks_stage_load(kv, hv, kg, pht, M, tin * kEksTile, tjn * kEksTile);
+#ifndef EKS_PROBE_NOMEM
+            eks_tile_load(pre, P, n, ld, tin * kEksTile, tjn * kEksTile, tin == tjn, wr, wc, lr,
+                          lk);
+#endif
+        }
+        // k ascending in steps of 4; the fragments of step k+4 are read from
+        // LDS while the MFMAs of step k run (two register sets)
+        double fa0[2], fb0[4], fa1[2], fb1[4];
+#ifdef EKS_PROBE_NOMFMA
+        const int32_t Mk = 0;
+#else
+        const int32_t Mk = M;
+#endif
+        eks_frag_load(fa0, fb0, Ks, Hs, 0, wr, wc, lr, lk);
+        int k0 = 0;
+        for (; k0 + 4 < Mk; k0 += 8) {
+            eks_frag_load(fa1, fb1, Ks, Hs, k0 + 4, wr, wc, lr, lk);
+            eks_frag_mfma(acc, fa0, fb0);
+            if (k0 + 8 < Mk) eks_frag_load(fa0, fb0, Ks, Hs, k0 + 8, wr, wc, lr, lk);
+            eks_frag_mfma(acc, fa1, fb1);
+        }
+        if (k0 < Mk) eks_frag_mfma(acc, fa0, fb0);
+#pragma unroll
+        for (int a = 0; a < 2; ++a)
+#pragma unroll
+            for (int b = 0; b < 4; ++b)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int64_t gi = r0 + wr + 16 * a + lk + 4 * r;
+                    const int64_t gj = c0 + wc + 16 * b + lr;
+#ifdef EKS_PROBE_NOMEM
+                    if (acc[a][b][r] == 1.2345) P[gi * ld + gj] = acc[a][b][r];
+#else
+                    if (gi < n && gj < n && (!diag || gj <= gi)) P[gi * ld + gj] = acc[a][b][r];
+#endif
+                }
+        if (!more) break;
+        __syncthreads();                // every wave is done reading this tile's K / PH^T
+        eks_stage_store(kv, hv, Ks, Hs);
+        __syncthreads();
+#pragma unroll
+        for (int a = 0; a < 2; ++a)
+#pragma unroll
+            for (int b = 0; b < 4; ++b) {
+#ifdef EKS_PROBE_NOMEM
+                acc[a][b] += 1.0;
+#else
+                acc[a][b] = pre[a][b];
+#endif
+            }
+        L = Ln;
+        ti = tin;
+        tj = tjn;
+    }
+}
+
 }  // namespace slam
