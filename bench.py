@@ -137,7 +137,10 @@ def bench_ekf_batch(batch=1 << 20, steps=64, device=0):
             "ms_per_launch": dt * 1e3,
             "roofline": {"bound": "hbm", "achieved": byt / dt / 1e9, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": byt / dt / 1e9 / HBM_PEAK_GBS,
-                         "note": "40 algorithmic B per filter-step (z in, x_hat out)"}}
+                         "note": "40 algorithmic B per filter-step (z in, x_hat out); the kernel "
+                                 "is fp64-VALU issue bound in practice: ~300 VALU instructions "
+                                 "per filter-step in the ISA (~142 algorithmic flops), "
+                                 "prefetching z or a lean sincos did not move it"}}
 
 
 def _scan_measure(pose, lmk):

@@ -143,7 +143,8 @@ int eks_update(slam_ekfslam* h, int32_t k, const int64_t* ids, const double* obs
     hipLaunchKernelGGL(eks_gain_kernel, dim3(1), dim3(1024), sbytes, h->stream, h->pht, h->ids,
                        h->hs, h->rd, k, M, h->sinv);
     SLAM_HIP_TRY(hipEventRecord(h->ev[2], h->stream));
-    hipLaunchKernelGGL(eks_apply_kernel, dim3((unsigned)((h->n_pad + 255) / 256)), dim3(256),
+    const int64_t apply_grid = std::min<int64_t>(512, (h->n_pad + 15) / 16);
+    hipLaunchKernelGGL(eks_apply_kernel, dim3((unsigned)apply_grid), dim3(kEksApplyThreads),
                        sbytes, h->stream, h->pht, h->sinv, h->e, h->n, h->n_pad, M, h->kg, h->mu);
     SLAM_HIP_TRY(hipEventRecord(h->ev[3], h->stream));
     const int64_t nt = h->n_pad / kEksTile;

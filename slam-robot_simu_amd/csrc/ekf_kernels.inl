@@ -325,42 +325,78 @@ __global__ __launch_bounds__(1024) void eks_gain_kernel(const double* __restrict
 }
 
 // K = PHt S^-1 (rows of n_pad), mu += K e, yaw wrapped.
-__global__ __launch_bounds__(256) void eks_apply_kernel(const double* __restrict__ pht,
-                                                        const double* __restrict__ sinv,
-                                                        const double* __restrict__ e,
-                                                        const int64_t n, const int64_t n_pad,
-                                                        const int32_t M, double* __restrict__ kg,
-                                                        double* __restrict__ mu) {
+// K = PHt Sinv and mu += K e: one wave per row (rows strided over a resident
+// grid), lane j forms K[i][j] and K[i][j + 64]; the PHt row is loaded once,
+// coalesced, and its entries broadcast through SGPRs (v_readlane), Sinv is
+// read from LDS along its rows.  Both sums run in the order of the one-lane-
+// per-row form (v ascending from 0 with fma; dmu over u ascending).
+constexpr int kEksApplyThreads = 1024;
+
+__device__ __forceinline__ double readlane_d(const double x, const int l) {
+    const long long b = __double_as_longlong(x);
+    const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffffLL), l);
+    const int hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
+__global__ __launch_bounds__(kEksApplyThreads) void eks_apply_kernel(
+    const double* __restrict__ pht, const double* __restrict__ sinv, const double* __restrict__ e,
+    const int64_t n, const int64_t n_pad, const int32_t M, double* __restrict__ kg,
+    double* __restrict__ mu) {
     extern __shared__ double Si[];          // M * M
+    __shared__ double es[kEksMaxM];
     for (int idx = threadIdx.x; idx < M * M; idx += blockDim.x) Si[idx] = sinv[idx];
+    if (threadIdx.x < M) es[threadIdx.x] = e[threadIdx.x];
     __syncthreads();
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n_pad) return;
-    const double* prow = pht + i * M;
-    double* krow = kg + i * M;
-    double dmu = 0.0;
-    constexpr int U = 12;
-    for (int u0 = 0; u0 < M; u0 += U) {
-        double acc[U];
+    const int lane = threadIdx.x & 63;
+    // lanes past M work on a clamped column (in-bounds, never stored): no
+    // divergent branches in the loops
+    const int j0 = min(lane, M - 1), j1 = min(lane + 64, M - 1);
+    const bool c0 = lane < M, c1 = lane + 64 < M;
+    const int64_t waves = (int64_t)gridDim.x * (kEksApplyThreads / 64);
+    for (int64_t i = (int64_t)blockIdx.x * (kEksApplyThreads / 64) + (threadIdx.x >> 6);
+         i < n_pad; i += waves) {
+        const double* prow = pht + i * M;
+        const double p0 = prow[j0], p1 = prow[j1];
+        // M and 64 are multiples of 4: four broadcasts and eight LDS reads are
+        // issued per group, the fma chains keep v ascending
+        double k0 = 0.0, k1 = 0.0;
+        for (int v = 0; v < M; v += 4) {
+            const double src = (v < 64) ? p0 : p1;
+            const int l = v & 63;
+            double pv[4], s0[4], s1[4];
 #pragma unroll
-        for (int q = 0; q < U; ++q) acc[q] = 0.0;
-        for (int v = 0; v < M; ++v) {
-            const double pv = prow[v];
-#pragma unroll
-            for (int q = 0; q < U; ++q)
-                if (u0 + q < M) acc[q] = fma(pv, Si[v * M + u0 + q], acc[q]);
-        }
-#pragma unroll
-        for (int q = 0; q < U; ++q)
-            if (u0 + q < M) {
-                krow[u0 + q] = acc[q];
-                dmu = fma(acc[q], e[u0 + q], dmu);
+            for (int t = 0; t < 4; ++t) {
+                pv[t] = readlane_d(src, l + t);
+                s0[t] = Si[(v + t) * M + j0];
+                s1[t] = Si[(v + t) * M + j1];
             }
-    }
-    if (i < n) {
-        double m = mu[i] + dmu;
-        if (i == 2) m = wrap_angle(m);
-        mu[i] = m;
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                k0 = fma(pv[t], s0[t], k0);
+                k1 = fma(pv[t], s1[t], k1);
+            }
+        }
+        double* krow = kg + i * M;
+        if (c0) krow[lane] = k0;
+        if (c1) krow[lane + 64] = k1;
+        if (i < n) {
+            double dmu = 0.0;
+            for (int u = 0; u < M; u += 4) {
+                const double src = (u < 64) ? k0 : k1;
+                const int l = u & 63;
+                double kv[4];
+#pragma unroll
+                for (int t = 0; t < 4; ++t) kv[t] = readlane_d(src, l + t);
+#pragma unroll
+                for (int t = 0; t < 4; ++t) dmu = fma(kv[t], es[u + t], dmu);
+            }
+            if (lane == 0) {
+                double m = mu[i] + dmu;
+                if (i == 2) m = wrap_angle(m);
+                mu[i] = m;
+            }
+        }
     }
 }
 
