@@ -284,7 +284,7 @@ __global__ __launch_bounds__(1024) void eks_gain_kernel(const double* __restrict
                                                         const int32_t k, const int32_t M,
                                                         double* __restrict__ sinv_out) {
     extern __shared__ double S[];           // M * M
-    __shared__ double colp[kEksMaxM];
+    __shared__ double colp[kEksMaxM], rowp[kEksMaxM];
     const int m = 3 * k;
     for (int idx = threadIdx.x; idx < M * M; idx += blockDim.x) {
         const int a = idx / M, u = idx % M;
@@ -306,19 +306,26 @@ __global__ __launch_bounds__(1024) void eks_gain_kernel(const double* __restrict
         S[idx] = v;
     }
     __syncthreads();
+    // Gauss-Jordan without pivoting (S is SPD), two barriers per pivot: the
+    // pivot column and the scaled pivot row are captured from the old values,
+    // then every entry is updated once.  Thread (r, j) of the 16 x 64 grid owns
+    // columns j, j + 64 of rows r, r + 16, ... (no integer division).
+    const int jl = threadIdx.x & 63, rl = threadIdx.x >> 6;
     for (int p = 0; p < M; ++p) {
         const double inv_p = 1.0 / S[p * M + p];
-        for (int i = threadIdx.x; i < M; i += blockDim.x) colp[i] = S[i * M + p];
-        __syncthreads();
-        for (int j = threadIdx.x; j < M; j += blockDim.x)
-            S[p * M + j] = (j == p) ? inv_p : S[p * M + j] * inv_p;
-        __syncthreads();
-        for (int idx = threadIdx.x; idx < M * M; idx += blockDim.x) {
-            const int i = idx / M, j = idx % M;
-            if (i == p) continue;
-            const double f = colp[i];
-            S[idx] = (j == p) ? -f * inv_p : S[idx] - f * S[p * M + j];
+        for (int i = threadIdx.x; i < M; i += blockDim.x) {
+            colp[i] = S[i * M + p];
+            rowp[i] = (i == p) ? inv_p : S[p * M + i] * inv_p;
         }
+        __syncthreads();
+        for (int i = rl; i < M; i += 16)
+            for (int j = jl; j < M; j += 64) {
+                double v;
+                if (i == p) v = rowp[j];
+                else if (j == p) v = -colp[i] * inv_p;
+                else v = S[i * M + j] - colp[i] * rowp[j];
+                S[i * M + j] = v;
+            }
         __syncthreads();
     }
     for (int idx = threadIdx.x; idx < M * M; idx += blockDim.x) sinv_out[idx] = S[idx];
