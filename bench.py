@@ -187,7 +187,7 @@ def bench_ekfslam(n_lm=10000, k=20, steps=6, device=0):
     return {"workload": "EKF-SLAM C4: 10,000 landmarks (n = 30,003, P = 7.2 GB), 20 observed "
                         "per step", "value": 1.0 / float(np.mean(times)), "unit": "updates/s",
             "ms_per_update": float(np.mean(times)) * 1e3, "last_update_breakdown_ms": tm,
-            "roofline": {"bound": "hbm", "kernel": "eks_rank_update_kernel (fp64 MFMA)",
+            "roofline": {"bound": "hbm", "kernel": "eks_rank_update_pipelined_kernel (fp64 MFMA)",
                          "achieved": byt / rk / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": byt / rk / 1e9 / HBM_PEAK_GBS,
                          "tflops": flops / rk / 1e12, "avg_launch_ms": rk * 1e3}}
@@ -224,14 +224,73 @@ def bench_graph(n_poses=50000, iters=3, device=0):
                          "note": "80 B edge + 2 x 24 B poses in, 336 B blocks out per edge"}}
 
 
-def secondary(device=0):
+def _blas_threads():
+    try:
+        from threadpoolctl import threadpool_info
+        return max([d.get("num_threads", 1) for d in threadpool_info()
+                    if d.get("user_api") == "blas"] or [1])
+    except Exception:
+        return None
+
+
+def cpu_ekf_batch(seconds_target=3.0):
+    """The oracle's ekf_update (extended_kalman_filter.py:108-128, NumPy per
+    filter-step, as the reference runs it) on one host core, bounded sample."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import ekf_oracle as eo
+    p = eo.EKFParams()
+    rs = np.random.RandomState(5)
+    x, P = np.array([10.0, 0.0, np.pi / 2]), np.diag([0.01, 0.01, 0.001])
+    zs = rs.standard_normal((4096, 2)) + np.array([10.0, 0.0])
+    steps, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < seconds_target:
+        _, x, P = eo.ekf_update(x, P, zs[steps % len(zs)], p)
+        steps += 1
+    dt = time.perf_counter() - t0
+    return {"value": steps / dt, "unit": "filter-steps/s", "cores": 1, "kind": "port",
+            "sample": f"oracle ekf_update, one filter, {steps} steps, {dt:.1f} s on 1 core"}
+
+
+def cpu_ekfslam(n_lm=1000, k=20):
+    """One EKF-SLAM update of the oracle restatement (dense NumPy, BLAS threads)
+    on a bounded sample: n = 3,003 (the NumPy update is O(n^2 m) and takes
+    minutes at the C4 size), so the unit names the sample size."""
+    import psutil
+    if psutil.virtual_memory().available < 8e9:
+        return {"skipped": "less than 8 GB of host memory available"}
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import ekf_oracle as eo
+    rs = np.random.RandomState(4)
+    lmk = np.column_stack([rs.uniform(-100, 100, (n_lm, 2)), rs.uniform(-np.pi, np.pi, n_lm)])
+    pose = np.array([50.0, 0.0, np.pi / 2])
+    n = 3 + 3 * n_lm
+    mu = np.concatenate([pose, (lmk + rs.normal(0, 0.5, lmk.shape)).ravel()])
+    P = np.diag(np.concatenate([[1e-4, 1e-4, 1e-5], np.full(n - 3, 0.25)]))
+    ids = np.argpartition(np.hypot(lmk[:, 0] - pose[0], lmk[:, 1] - pose[1]), k)[:k]
+    obs = _scan_measure(pose, lmk[ids])
+    q = np.diag([0.1, 0.1, np.deg2rad(0.1)]) ** 2
+    t0 = time.perf_counter()
+    mu, P = eo.ekfslam_step(mu, P, (5.0, 0.1), ids, obs, 0.1, q,
+                            (0.05, np.deg2rad(2.0), np.deg2rad(2.0)))
+    dt = time.perf_counter() - t0
+    del P
+    return {"value": 1.0 / dt, "unit": f"updates/s at n = {n}", "cores": _blas_threads(),
+            "kind": "port",
+            "sample": f"oracle ekfslam_step, n = {n}, k = {k}, one update (dense NumPy / BLAS), "
+                      f"{dt:.2f} s; the C4 rows above are at n = 30,003"}
+
+
+def secondary(device=0, cpu=True):
     out = {}
-    for name, fn in (("ekf_batch", bench_ekf_batch), ("ekfslam_c4", bench_ekfslam),
-                     ("graph_c5", bench_graph)):
+    for name, fn, cfn in (("ekf_batch", bench_ekf_batch, cpu_ekf_batch),
+                          ("ekfslam_c4", bench_ekfslam, cpu_ekfslam),
+                          ("graph_c5", bench_graph, None)):
         try:
             out[name] = fn(device=device)
+            if cpu and cfn is not None:
+                out[name]["cpu_baseline"] = cfn()
         except Exception as e:            # reported, never silently replaced
-            out[name] = {"error": f"{type(e).__name__}: {e}"}
+            out[name] = {**out.get(name, {}), "error": f"{type(e).__name__}: {e}"}
     return out
 
 
@@ -342,7 +401,7 @@ def main():
         line["alt_modes"] = {"product": {"value": NP_PER_GPU * NL * args.steps / e2,
                                          "fused_avg_ms": t2[0][0] / max(t2[0][1], 1)}}
     if rank == 0 and world == 1 and not args.no_secondary:
-        line["secondary"] = secondary(local_rank)
+        line["secondary"] = secondary(local_rank, cpu=not args.no_cpu_baseline)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline()
         line["cpu_baseline"]["gpu_over_cpu"] = value / line["cpu_baseline"]["value"]
