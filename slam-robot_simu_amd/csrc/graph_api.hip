@@ -37,7 +37,7 @@ struct slam_graph {
     int32_t* piv = nullptr;
     double* luout = nullptr;       // [0..2] LU, [3..4] Lanczos
     // PCG
-    double *minv = nullptr, *r = nullptr, *z = nullptr, *p = nullptr, *p2 = nullptr;
+    double *minv = nullptr, *r = nullptr, *z = nullptr, *p = nullptr;
     double* q = nullptr;
     double* part = nullptr;
     PcgState* st = nullptr;
@@ -161,7 +161,6 @@ int build_structure(slam_graph* h, int64_t E, const slam_graph_edge* ed) {
     GTRY(galloc(h, &h->r, n));
     GTRY(galloc(h, &h->z, n));
     GTRY(galloc(h, &h->p, n));
-    GTRY(galloc(h, &h->p2, n));
     GTRY(galloc(h, &h->q, n));
     GTRY(galloc(h, &h->part, 3 * (int64_t)nblk(n, kPcgThreads) + 3));
     GTRY(galloc(h, &h->st, 1));
@@ -262,13 +261,11 @@ int solve_pcg(slam_graph* h, double* stats, bool* solved, int32_t* iters) {
     const int chunk = 16;
     for (int32_t k0 = 0;; k0 += chunk) {
         for (int32_t k = k0; k < k0 + chunk; ++k) {
-            double* pk = (k & 1) ? h->p2 : h->p;
-            double* pprev = (k & 1) ? h->p : h->p2;
             hipLaunchKernelGGL(graph_pcg_dir_spmv_kernel, dim3(nb), dim3(kSpmvThreads), 0,
-                               h->stream, h->nt, k, h->rptr, h->scol, h->val, h->z, pprev, pk, h->q,
+                               h->stream, h->nt, k, h->rptr, h->scol, h->val, h->z, h->p, h->q,
                                h->part, h->st, h->cfg.pcg_tol, h->cfg.pcg_max_iter);
             hipLaunchKernelGGL(graph_pcg_step_kernel, dim3(nb), dim3(kPcgThreads), 0, h->stream,
-                               n, k, h->minv, pk, h->q, h->delta, h->r, h->z, h->part, h->st);
+                               n, k, h->minv, h->p, h->q, h->delta, h->r, h->z, h->part, h->st);
         }
         SLAM_HIP_TRY(hipGetLastError());
         SLAM_HIP_TRY(hipMemcpyAsync(&s, h->st, sizeof(PcgState), hipMemcpyDeviceToHost, h->stream));

@@ -623,58 +623,42 @@ __global__ __launch_bounds__(kPcgThreads) void graph_pcg_start_kernel(
 }
 
 // iteration k, first launch: rho_k and the convergence test from the r.z / r.r
-// partials, p_k = z + beta p_{k-1} (formed on the fly for the gathered
-// columns, written for the own rows into the other ping-pong buffer),
-// q = H p_k ; partial p.q.  SpMV: a group of 8 lanes per block row, each lane
-// one whole 3x3 block at a time (72 contiguous bytes, adjacent lanes adjacent
-// blocks), the three row sums folded over the group by a fixed xor tree.
+// partials, then the direction and its image by the recurrences
+//   p_k = z + beta p_{k-1},   q_k = H p_k = H z + beta q_{k-1}
+// so the SpMV gathers z alone (p and q are updated in place on the own rows);
+// partial p.q.  SpMV: a group of 8 lanes per block row, each lane one whole
+// 3x3 block at a time (72 contiguous bytes, adjacent lanes adjacent blocks),
+// the three row sums folded over the group by a fixed xor tree.
 constexpr int kSpmvThreads = 512, kSpmvGroup = 8;    // 64 poses per workgroup
 static_assert(kSpmvThreads / kSpmvGroup * 3 == kPcgThreads, "same workgroup count");
 
-// one 3x3 block of a row with its gathered z / p_{k-1} columns
-struct PcgBlock {
-    double v[9], zc[3], pc[3];
-};
-
-__device__ __forceinline__ void pcg_load_block(PcgBlock& B, const int64_t s, const int32_t k,
-                                               const int64_t* __restrict__ col,
-                                               const double* __restrict__ val,
-                                               const double* __restrict__ z,
-                                               const double* __restrict__ pold) {
+__device__ __forceinline__ void pcg_block_dot(const int64_t s, const int64_t* __restrict__ col,
+                                              const double* __restrict__ val,
+                                              const double* __restrict__ z, double& a0,
+                                              double& a1, double& a2) {
     const double* v = val + s * 9;
+    double b[9];
 #pragma unroll
-    for (int j = 0; j < 9; ++j) B.v[j] = v[j];
+    for (int j = 0; j < 9; ++j) b[j] = v[j];
     const int64_t c = 3 * col[s];
-#pragma unroll
-    for (int j = 0; j < 3; ++j) {
-        B.zc[j] = z[c + j];
-        B.pc[j] = (k > 0) ? pold[c + j] : 0.0;
-    }
-}
-
-__device__ __forceinline__ void pcg_apply_block(const PcgBlock& B, const int32_t k,
-                                                const double beta, double& a0, double& a1,
-                                                double& a2) {
-    double p[3];
-#pragma unroll
-    for (int j = 0; j < 3; ++j) p[j] = (k > 0) ? fma(beta, B.pc[j], B.zc[j]) : B.zc[j];
-    a0 = fma(B.v[0], p[0], a0);
-    a0 = fma(B.v[1], p[1], a0);
-    a0 = fma(B.v[2], p[2], a0);
-    a1 = fma(B.v[3], p[0], a1);
-    a1 = fma(B.v[4], p[1], a1);
-    a1 = fma(B.v[5], p[2], a1);
-    a2 = fma(B.v[6], p[0], a2);
-    a2 = fma(B.v[7], p[1], a2);
-    a2 = fma(B.v[8], p[2], a2);
+    const double z0 = z[c], z1 = z[c + 1], z2 = z[c + 2];
+    a0 = fma(b[0], z0, a0);
+    a0 = fma(b[1], z1, a0);
+    a0 = fma(b[2], z2, a0);
+    a1 = fma(b[3], z0, a1);
+    a1 = fma(b[4], z1, a1);
+    a1 = fma(b[5], z2, a1);
+    a2 = fma(b[6], z0, a2);
+    a2 = fma(b[7], z1, a2);
+    a2 = fma(b[8], z2, a2);
 }
 
 __global__ __launch_bounds__(kSpmvThreads) void graph_pcg_dir_spmv_kernel(
     const int64_t nt, const int32_t k, const int64_t* __restrict__ rptr,
     const int64_t* __restrict__ col, const double* __restrict__ val,
-    const double* __restrict__ z, const double* __restrict__ pold, double* __restrict__ pnew,
-    double* __restrict__ q, double* __restrict__ part, PcgState* __restrict__ st,
-    const double tol, const int32_t max_iter) {
+    const double* __restrict__ z, double* __restrict__ p, double* __restrict__ q,
+    double* __restrict__ part, PcgState* __restrict__ st, const double tol,
+    const int32_t max_iter) {
     __shared__ double sh[2 * kSpmvThreads / 64];
     if (k > 0 && st->done) return;
     const int64_t nb = gridDim.x;
@@ -701,16 +685,10 @@ __global__ __launch_bounds__(kSpmvThreads) void graph_pcg_dir_spmv_kernel(
     if (status) return;
     const int g = threadIdx.x & (kSpmvGroup - 1);
     const int64_t rw = (int64_t)blockIdx.x * (kSpmvThreads / kSpmvGroup) + threadIdx.x / kSpmvGroup;
-    const bool own = rw < nt && g < 3;
-    const int64_t i = 3 * rw + g;
     double a0 = 0.0, a1 = 0.0, a2 = 0.0;
     if (rw < nt) {
         const int64_t s1 = rptr[rw + 1];
-        for (int64_t s = rptr[rw] + g; s < s1; s += kSpmvGroup) {
-            PcgBlock B;
-            pcg_load_block(B, s, k, col, val, z, pold);
-            pcg_apply_block(B, k, beta, a0, a1, a2);
-        }
+        for (int64_t s = rptr[rw] + g; s < s1; s += kSpmvGroup) pcg_block_dot(s, col, val, z, a0, a1, a2);
     }
 #pragma unroll
     for (int d = 1; d < kSpmvGroup; d <<= 1) {
@@ -719,12 +697,14 @@ __global__ __launch_bounds__(kSpmvThreads) void graph_pcg_dir_spmv_kernel(
         a2 += __shfl_xor(a2, d, 64);
     }
     double pq = 0.0;
-    if (own) {
-        const double acc = (g == 0) ? a0 : (g == 1) ? a1 : a2;
-        const double pi = (k > 0) ? fma(beta, pold[i], z[i]) : z[i];
-        pnew[i] = pi;
-        q[i] = acc;
-        pq = acc * pi;
+    if (rw < nt && g < 3) {
+        const double hz = (g == 0) ? a0 : (g == 1) ? a1 : a2;
+        const int64_t i = 3 * rw + g;
+        const double pi = (k > 0) ? fma(beta, p[i], z[i]) : z[i];
+        const double qi = (k > 0) ? fma(beta, q[i], hz) : hz;
+        p[i] = pi;
+        q[i] = qi;
+        pq = qi * pi;
     }
     pq = block_sum_fixed<kSpmvThreads>(pq, sh);
     if (threadIdx.x == 0) part[blockIdx.x] = pq;
