@@ -138,9 +138,11 @@ def bench_ekf_batch(batch=1 << 20, steps=64, device=0):
             "roofline": {"bound": "hbm", "achieved": byt / dt / 1e9, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": byt / dt / 1e9 / HBM_PEAK_GBS,
                          "note": "40 algorithmic B per filter-step (z in, x_hat out); the kernel "
-                                 "is fp64-VALU issue bound in practice: ~300 VALU instructions "
-                                 "per filter-step in the ISA (~142 algorithmic flops), "
-                                 "prefetching z or a lean sincos did not move it"}}
+                                 "is fp64-VALU issue bound in practice (PMC: 221 VALU "
+                                 "instructions per filter-step before the adjugate / "
+                                 "structural-zero cleanup, ~142 algorithmic flops, ~1.5 GHz "
+                                 "effective clock under fp64 load); prefetching z, coalescing "
+                                 "the x_hat stores through LDS or a lean sincos did not move it"}}
 
 
 def _scan_measure(pose, lmk):

@@ -59,8 +59,12 @@ __device__ __forceinline__ void ekf_filter_step(double& x, double& y, double& t,
     // S = C P_m C^T + R; G = P_m C^T S^-1  (:149-158)
     const double s00 = Pm[0] + c.r[0], s01 = Pm[1] + c.r[1];
     const double s10 = Pm[3] + c.r[2], s11 = Pm[4] + c.r[3];
+    // S^-1 by the adjugate with one correctly rounded reciprocal of det (the
+    // reference's np.linalg.inv takes the LU route: neither form is its
+    // rounding; four divisions cost 26 more fp64 VALU per filter-step)
     const double det = s00 * s11 - s01 * s10;
-    const double i00 = s11 / det, i01 = -s01 / det, i10 = -s10 / det, i11 = s00 / det;
+    const double rdet = 1.0 / det;
+    const double i00 = s11 * rdet, i01 = -s01 * rdet, i10 = -s10 * rdet, i11 = s00 * rdet;
     double G[6];
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
@@ -72,16 +76,15 @@ __device__ __forceinline__ void ekf_filter_step(double& x, double& y, double& t,
     x = xm + fma(G[1], e1, G[0] * e0);
     y = ym + fma(G[3], e1, G[2] * e0);
     t = wrap_angle(tm + fma(G[5], e1, G[4] * e0));
-    // P = (I - G C) P_m  (:128-129)
-    const double M[9] = {1.0 - G[0], -G[1], 0.0, -G[2], 1.0 - G[3], 0.0, -G[4], -G[5], 1.0};
+    // P = (I - G C) P_m  (:128-129); the structural zeros of I - G C (third
+    // column 0, 0, 1) contribute exact +0 / x terms: dropped / added directly
+    const double M[6] = {1.0 - G[0], -G[1], -G[2], 1.0 - G[3], -G[4], -G[5]};
 #pragma unroll
-    for (int i = 0; i < 3; ++i)
-#pragma unroll
-        for (int j = 0; j < 3; ++j) {
-            double acc = M[3 * i] * Pm[j];
-            acc = fma(M[3 * i + 1], Pm[3 + j], acc);
-            P[3 * i + j] = fma(M[3 * i + 2], Pm[6 + j], acc);
-        }
+    for (int j = 0; j < 3; ++j) {
+        P[j] = fma(M[1], Pm[3 + j], M[0] * Pm[j]);
+        P[3 + j] = fma(M[3], Pm[3 + j], M[2] * Pm[j]);
+        P[6 + j] = fma(M[5], Pm[3 + j], M[4] * Pm[j]) + Pm[6 + j];
+    }
     if (xm_out) {
         xm_out[0] = xm;
         xm_out[1] = ym;
