@@ -154,7 +154,7 @@ int eks_update(slam_ekfslam* h, int32_t k, const int64_t* ids, const double* obs
 #endif
     if (SLAM_EKS_PIPE && h->pipe_grid > 0 && M <= kEksPipeK) {
         hipLaunchKernelGGL(eks_rank_update_pipelined_kernel, dim3((unsigned)h->pipe_grid),
-                           dim3(kEksThreads), 0, h->stream, h->P, h->n, h->ld, h->kg, h->pht, M,
+                           dim3(kEksPipeThreads), 0, h->stream, h->P, h->n, h->ld, h->kg, h->pht, M,
                            tiles);
     } else {
         const int64_t grid = (tiles + 7) / 8 * 8;
@@ -354,7 +354,7 @@ int slam_ekfslam_create(const slam_ekfslam_config* cfg, int64_t n_landmarks, int
     {
         int per_cu = 0, cus = 0;
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, eks_rank_update_pipelined_kernel,
-                                                         kEksThreads, 0) == hipSuccess &&
+                                                         kEksPipeThreads, 0) == hipSuccess &&
             hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) ==
                 hipSuccess)
             h->pipe_grid = (int64_t)per_cu * cus / 8 * 8;

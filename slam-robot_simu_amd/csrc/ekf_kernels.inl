@@ -536,6 +536,16 @@ __global__ __launch_bounds__(256) void eks_diag_kernel(double* __restrict__ P, c
 // in steps of 4) is the one of eks_rank_update_kernel: identical results.
 constexpr int kEksPipeK = 64;
 constexpr int kEksPipeKS = kEksPipeK + 1;
+#ifndef SLAM_EKS_PIPE_WC
+#define SLAM_EKS_PIPE_WC 2
+#endif
+// waves: 4 along the rows (32 each) x kEksPipeWC along the columns.  4 x 4
+// (1024 threads, 4 waves per SIMD, 128 VGPRs with a small spill) measured
+// 2.29 ms per C4 rank update against 2.06 ms for 4 x 2.
+constexpr int kEksPipeWC = SLAM_EKS_PIPE_WC;
+constexpr int kEksPipeThreads = 256 * kEksPipeWC;
+constexpr int kEksPipeBB = 8 / kEksPipeWC;          // 16-column MFMA blocks per wave
+constexpr int kEksPipeWPE = kEksPipeWC;             // waves per SIMD of the one workgroup per CU
 typedef double eks_d4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ void eks_tile_rc(const int64_t L, int64_t& ti, int64_t& tj) {
@@ -545,14 +555,14 @@ __device__ __forceinline__ void eks_tile_rc(const int64_t L, int64_t& ti, int64_
     tj = L - ti * (ti + 1) / 2;
 }
 
-__device__ __forceinline__ void eks_tile_load(eks_d4 (&t)[2][4], const double* __restrict__ P,
+__device__ __forceinline__ void eks_tile_load(eks_d4 (&t)[2][kEksPipeBB], const double* __restrict__ P,
                                               const int64_t n, const int64_t ld, const int64_t r0,
                                               const int64_t c0, const bool diag, const int wr,
                                               const int wc, const int lr, const int lk) {
 #pragma unroll
     for (int a = 0; a < 2; ++a)
 #pragma unroll
-        for (int b = 0; b < 4; ++b)
+        for (int b = 0; b < kEksPipeBB; ++b)
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int64_t gi = r0 + wr + 16 * a + lk + 4 * r;
@@ -561,7 +571,7 @@ __device__ __forceinline__ void eks_tile_load(eks_d4 (&t)[2][4], const double* _
             }
 }
 
-constexpr int kEksPipePer = kEksTile * kEksPipeK / kEksThreads;     // 16 per lane and operand
+constexpr int kEksPipePer = kEksTile * kEksPipeK / kEksPipeThreads;  // per lane and operand
 
 __device__ __forceinline__ void eks_stage_load(double (&kv)[kEksPipePer], double (&hv)[kEksPipePer],
                                                const double* __restrict__ kg,
@@ -569,7 +579,7 @@ __device__ __forceinline__ void eks_stage_load(double (&kv)[kEksPipePer], double
                                                const int64_t r0, const int64_t c0) {
 #pragma unroll
     for (int s = 0; s < kEksPipePer; ++s) {
-        const int idx = threadIdx.x + s * kEksThreads;
+        const int idx = threadIdx.x + s * kEksPipeThreads;
         const int r = idx / kEksPipeK, q = idx % kEksPipeK;
         const bool ok = q < M;
         kv[s] = ok ? -kg[(r0 + r) * M + q] : 0.0;       // K staged negated
@@ -582,32 +592,32 @@ __device__ __forceinline__ void eks_stage_store(const double (&kv)[kEksPipePer],
                                                 double* Hs) {
 #pragma unroll
     for (int s = 0; s < kEksPipePer; ++s) {
-        const int idx = threadIdx.x + s * kEksThreads;
+        const int idx = threadIdx.x + s * kEksPipeThreads;
         const int r = idx / kEksPipeK, q = idx % kEksPipeK;
         Ks[r * kEksPipeKS + q] = kv[s];
         Hs[r * kEksPipeKS + q] = hv[s];
     }
 }
 
-__device__ __forceinline__ void eks_frag_load(double (&fa)[2], double (&fb)[4], const double* Ks,
+__device__ __forceinline__ void eks_frag_load(double (&fa)[2], double (&fb)[kEksPipeBB], const double* Ks,
                                               const double* Hs, const int k0, const int wr,
                                               const int wc, const int lr, const int lk) {
 #pragma unroll
     for (int a = 0; a < 2; ++a) fa[a] = Ks[(wr + 16 * a + lr) * kEksPipeKS + k0 + lk];
 #pragma unroll
-    for (int b = 0; b < 4; ++b) fb[b] = Hs[(wc + 16 * b + lr) * kEksPipeKS + k0 + lk];
+    for (int b = 0; b < kEksPipeBB; ++b) fb[b] = Hs[(wc + 16 * b + lr) * kEksPipeKS + k0 + lk];
 }
 
-__device__ __forceinline__ void eks_frag_mfma(eks_d4 (&acc)[2][4], const double (&fa)[2],
-                                              const double (&fb)[4]) {
+__device__ __forceinline__ void eks_frag_mfma(eks_d4 (&acc)[2][kEksPipeBB], const double (&fa)[2],
+                                              const double (&fb)[kEksPipeBB]) {
 #pragma unroll
     for (int a = 0; a < 2; ++a)
 #pragma unroll
-        for (int b = 0; b < 4; ++b)
+        for (int b = 0; b < kEksPipeBB; ++b)
             acc[a][b] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[a], fb[b], acc[a][b], 0, 0, 0);
 }
 
-__global__ __launch_bounds__(kEksThreads) __attribute__((amdgpu_waves_per_eu(2)))
+__global__ __launch_bounds__(kEksPipeThreads) __attribute__((amdgpu_waves_per_eu(kEksPipeWPE)))
 void eks_rank_update_pipelined_kernel(double* __restrict__ P, const int64_t n, const int64_t ld,
                                       const double* __restrict__ kg,
                                       const double* __restrict__ pht, const int32_t M,
@@ -621,11 +631,11 @@ void eks_rank_update_pipelined_kernel(double* __restrict__ P, const int64_t n, c
     if (L >= Lend) return;
     const int tid = threadIdx.x;
     const int lane = tid & 63, wave = tid >> 6;
-    const int wr = (wave >> 1) * 32, wc = (wave & 1) * 64;
+    const int wr = (wave / kEksPipeWC) * 32, wc = (wave % kEksPipeWC) * (16 * kEksPipeBB);
     const int lr = lane & 15, lk = lane >> 4;
     int64_t ti, tj;
     eks_tile_rc(L, ti, tj);
-    eks_d4 acc[2][4], pre[2][4];
+    eks_d4 acc[2][kEksPipeBB], pre[2][kEksPipeBB];
     double kv[kEksPipePer], hv[kEksPipePer];
     eks_stage_load(kv, hv, kg, pht, M, ti * kEksTile, tj * kEksTile);
     eks_tile_load(acc, P, n, ld, ti * kEksTile, tj * kEksTile, ti == tj, wr, wc, lr, lk);
@@ -647,7 +657,7 @@ void eks_rank_update_pipelined_kernel(double* __restrict__ P, const int64_t n, c
         }
         // k ascending in steps of 4; the fragments of step k+4 are read from
         // LDS while the MFMAs of step k run (two register sets)
-        double fa0[2], fb0[4], fa1[2], fb1[4];
+        double fa0[2], fb0[kEksPipeBB], fa1[2], fb1[kEksPipeBB];
 #ifdef EKS_PROBE_NOMFMA
         const int32_t Mk = 0;
 #else
@@ -665,7 +675,7 @@ void eks_rank_update_pipelined_kernel(double* __restrict__ P, const int64_t n, c
 #pragma unroll
         for (int a = 0; a < 2; ++a)
 #pragma unroll
-            for (int b = 0; b < 4; ++b)
+            for (int b = 0; b < kEksPipeBB; ++b)
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     const int64_t gi = r0 + wr + 16 * a + lk + 4 * r;
@@ -683,7 +693,7 @@ void eks_rank_update_pipelined_kernel(double* __restrict__ P, const int64_t n, c
 #pragma unroll
         for (int a = 0; a < 2; ++a)
 #pragma unroll
-            for (int b = 0; b < 4; ++b) {
+            for (int b = 0; b < kEksPipeBB; ++b) {
 #ifdef EKS_PROBE_NOMEM
                 acc[a][b] += 1.0;
 #else
