@@ -43,6 +43,7 @@ struct slam_graph {
     PcgState* st = nullptr;
     hipEvent_t ev[5] = {};
     double last[5] = {0, 0, 0, 0, 0};
+    int32_t pcg_last_iters = 0;    // iteration count of the previous PCG solve
 };
 
 namespace {
@@ -138,6 +139,7 @@ int build_structure(slam_graph* h, int64_t E, const slam_graph_edge* ed) {
     // device buffers
     free_list(h->allocs);
     h->E = E;
+    h->pcg_last_iters = 0;
     h->nt = nt;
     h->n_slots = ns;
     h->times_h = tl;
@@ -258,9 +260,12 @@ int solve_pcg(slam_graph* h, double* stats, bool* solved, int32_t* iters) {
                        h->minv, h->b, h->delta, h->r, h->z, h->part);
     SLAM_HIP_TRY(hipGetLastError());
     PcgState s{};
-    const int chunk = 16;
-    for (int32_t k0 = 0;; k0 += chunk) {
-        for (int32_t k = k0; k < k0 + chunk; ++k) {
+    // The first batch runs through the previous solve's iteration count (the
+    // Gauss-Newton steps of one edge set converge in similar counts), so a
+    // repeated solve usually needs a single host poll; then batches of 8.
+    int32_t k_end = std::max<int32_t>(16, std::min<int32_t>(h->pcg_last_iters + 1, 1024));
+    for (int32_t k0 = 0;; k0 = k_end, k_end += 8) {
+        for (int32_t k = k0; k < k_end; ++k) {
             hipLaunchKernelGGL(graph_pcg_dir_spmv_kernel, dim3(nb), dim3(kSpmvThreads), 0,
                                h->stream, h->nt, k, h->rptr, h->scol, h->val, h->z, h->p, h->q,
                                h->part, h->st, h->cfg.pcg_tol, h->cfg.pcg_max_iter);
@@ -273,6 +278,7 @@ int solve_pcg(slam_graph* h, double* stats, bool* solved, int32_t* iters) {
         if (s.done) break;
     }
     *iters = s.iter;
+    h->pcg_last_iters = (s.status == 1) ? s.iter : 0;
     stats[2] = std::numeric_limits<double>::quiet_NaN();
     stats[3] = std::numeric_limits<double>::quiet_NaN();
     *solved = (s.status == 1);
