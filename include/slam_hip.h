@@ -304,6 +304,22 @@ int slam_graph_get_delta(slam_graph* h, double* delta);
 /* Device time of the last update (ms): out[5] = {linearise, assemble, solve,
  * pose update, PCG iterations}. */
 int slam_graph_timing(slam_graph* h, double* out);
+/* HalfEdge (graph_based_slam.py:259-300) with its Observation (:20-75). */
+typedef struct {
+    int64_t time, pose, landmark;
+    double obs[3];        /* distance, direction, orientation */
+} slam_graph_half;
+
+/* Robot.estimateOpticalTrajectory's pairing (:697-703): for every landmark id
+ * in 0..n_landmarks-1, each 2-combination of its half-edges in recording
+ * order (itertools.combinations), ordered as setPairObs orders it (:371-384:
+ * the later time is "aft", ties keep the combination order).  Half-edges of
+ * other landmark ids never pair.  The half-edges are grouped per landmark on
+ * the host (stable, O(n_halves)); the combinations are expanded on the device,
+ * one lane per edge.  With edges == NULL only *n_edges is returned; otherwise
+ * edges (host, *n_edges records) receives the edge list. */
+int slam_graph_pair_halves(int64_t n_halves, const slam_graph_half* halves, int64_t n_landmarks,
+                           int device, int64_t* n_edges, slam_graph_edge* edges);
 /* One-shot form: poses in/out, stats[4] as slam_graph_update. */
 int slam_graph_linearize_solve(const slam_graph_config* cfg, const slam_graph_edge* edges,
                                int64_t n_edges, double* poses, int64_t n_poses, double* stats,

@@ -490,6 +490,68 @@ int slam_graph_timing(slam_graph* h, double* out) {
     return SLAM_OK;
 }
 
+int slam_graph_pair_halves(int64_t n_halves, const slam_graph_half* halves, int64_t n_landmarks,
+                           int device, int64_t* n_edges, slam_graph_edge* edges) {
+    SLAM_ARG_CHECK(n_edges && n_halves >= 0 && n_landmarks >= 0 && (halves || n_halves == 0),
+                   "slam_graph_pair_halves: bad arguments");
+    // stable grouping by landmark id (counting sort), pair offsets per landmark
+    std::vector<int64_t> lm_start(n_landmarks + 1, 0);
+    for (int64_t q = 0; q < n_halves; ++q) {
+        const int64_t l = halves[q].landmark;
+        if (l >= 0 && l < n_landmarks) lm_start[l + 1]++;
+    }
+    std::vector<int64_t> pair_off(n_landmarks + 1, 0);
+    for (int64_t l = 0; l < n_landmarks; ++l) {
+        const int64_t m = lm_start[l + 1];
+        pair_off[l + 1] = pair_off[l] + m * (m - 1) / 2;
+        lm_start[l + 1] += lm_start[l];
+    }
+    const int64_t E = pair_off[n_landmarks];
+    *n_edges = E;
+    if (!edges || E == 0) return SLAM_OK;
+    std::vector<slam_graph_half> grouped(lm_start[n_landmarks]);
+    {
+        std::vector<int64_t> fill(lm_start.begin(), lm_start.end() - 1);
+        for (int64_t q = 0; q < n_halves; ++q) {
+            const int64_t l = halves[q].landmark;
+            if (l >= 0 && l < n_landmarks) grouped[fill[l]++] = halves[q];
+        }
+    }
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev)
+        return fail(SLAM_ERR_ARG, "slam_graph_pair_halves: no such HIP device");
+    SLAM_HIP_TRY(hipSetDevice(device));
+    int64_t *d_off = nullptr, *d_start = nullptr;
+    slam_graph_half* d_half = nullptr;
+    slam_graph_edge* d_edges = nullptr;
+    int rc = SLAM_OK;
+    if (hipMalloc(&d_off, pair_off.size() * sizeof(int64_t)) != hipSuccess ||
+        hipMalloc(&d_start, lm_start.size() * sizeof(int64_t)) != hipSuccess ||
+        hipMalloc(&d_half, grouped.size() * sizeof(slam_graph_half)) != hipSuccess ||
+        hipMalloc(&d_edges, (size_t)E * sizeof(slam_graph_edge)) != hipSuccess) {
+        rc = fail(SLAM_ERR_HIP, "slam_graph_pair_halves: device allocation failed");
+    } else if (hipMemcpy(d_off, pair_off.data(), pair_off.size() * sizeof(int64_t),
+                         hipMemcpyHostToDevice) != hipSuccess ||
+               hipMemcpy(d_start, lm_start.data(), lm_start.size() * sizeof(int64_t),
+                         hipMemcpyHostToDevice) != hipSuccess ||
+               hipMemcpy(d_half, grouped.data(), grouped.size() * sizeof(slam_graph_half),
+                         hipMemcpyHostToDevice) != hipSuccess) {
+        rc = fail(SLAM_ERR_HIP, "slam_graph_pair_halves: upload failed");
+    } else {
+        hipLaunchKernelGGL(graph_pair_kernel, dim3(nblk(E)), dim3(256), 0, nullptr, E,
+                           n_landmarks, d_off, d_start, d_half, d_edges);
+        if (hipGetLastError() != hipSuccess ||
+            hipMemcpy(edges, d_edges, (size_t)E * sizeof(slam_graph_edge),
+                      hipMemcpyDeviceToHost) != hipSuccess)
+            rc = fail(SLAM_ERR_HIP, "slam_graph_pair_halves: kernel or download failed");
+    }
+    (void)hipFree(d_off);
+    (void)hipFree(d_start);
+    (void)hipFree(d_half);
+    (void)hipFree(d_edges);
+    return rc;
+}
+
 int slam_graph_linearize_solve(const slam_graph_config* cfg, const slam_graph_edge* edges,
                                int64_t n_edges, double* poses, int64_t n_poses, double* stats,
                                int device) {

@@ -181,6 +181,56 @@ __global__ __launch_bounds__(256) void graph_linearize_kernel(const int64_t E,
     }
 }
 
+// --------------------------------------------------------------- pairing
+// estimateOpticalTrajectory :697-703, one lane per output edge e: its landmark
+// l (last pair offset <= e), its rank k among l's pairs, and the combination
+// (i, j), i < j, of itertools.combinations order: row i holds the m - 1 - i
+// pairs (i, i+1 .. m-1), C(i) = i (2m - i - 1) / 2 pairs precede it.
+__device__ __forceinline__ int64_t comb_before(const int64_t i, const int64_t m) {
+    return i * (2 * m - i - 1) / 2;
+}
+
+__global__ __launch_bounds__(256) void graph_pair_kernel(
+    const int64_t E, const int64_t n_lm, const int64_t* __restrict__ pair_off,
+    const int64_t* __restrict__ lm_start, const slam_graph_half* __restrict__ grouped,
+    slam_graph_edge* __restrict__ edges) {
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= E) return;
+    int64_t lo = 0, hi = n_lm;                  // pair_off[lo] <= e < pair_off[hi]
+    while (hi - lo > 1) {
+        const int64_t mid = (lo + hi) >> 1;
+        if (pair_off[mid] <= e) lo = mid;
+        else hi = mid;
+    }
+    const int64_t m = lm_start[lo + 1] - lm_start[lo];
+    const int64_t k = e - pair_off[lo];
+    const double b = (double)(2 * m - 1);
+    int64_t i = (int64_t)((b - sqrt(fmax(b * b - 8.0 * (double)k, 0.0))) * 0.5);
+    if (i < 0) i = 0;
+    if (i > m - 2) i = m - 2;
+    while (i > 0 && comb_before(i, m) > k) --i;
+    while (i < m - 2 && comb_before(i + 1, m) <= k) ++i;
+    const int64_t j = k - comb_before(i, m) + i + 1;
+    const slam_graph_half* ha = grouped + lm_start[lo] + i;
+    const slam_graph_half* hb = grouped + lm_start[lo] + j;
+    if (ha->time > hb->time) {                  // setPairObs :371-384
+        const slam_graph_half* t = ha;
+        ha = hb;
+        hb = t;
+    }
+    slam_graph_edge out;
+    out.time_bfr = ha->time;
+    out.pose_bfr = ha->pose;
+    out.time_aft = hb->time;
+    out.pose_aft = hb->pose;
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+        out.obs_bfr[q] = ha->obs[q];
+        out.obs_aft[q] = hb->obs[q];
+    }
+    edges[e] = out;
+}
+
 // -------------------------------------------------------------- assemble
 // One lane per (block slot, entry): the slot's contributions in edge order
 // (code = 4 e + part), starting from the anchor on slot 0 (:475).

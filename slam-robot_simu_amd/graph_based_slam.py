@@ -17,11 +17,10 @@ between iterations.
 """
 from __future__ import annotations
 
-import itertools
 
 import numpy as np
 
-from slamhip.graph import DeviceGraph
+from slamhip.graph import DeviceGraph, edge_array, pair_halves
 
 DELTA_SUM_TH = 0.01          # graph_based_slam.py:662
 
@@ -76,6 +75,7 @@ class TrajectoryEstimator(object):
         self._rows = []
         self._lm_ids = []
         self._times = []
+        self._device = device
         self._dev = DeviceGraph(solver=solver, device=device)
 
     def addPose(self, aPose, aIsObs):
@@ -127,11 +127,17 @@ class TrajectoryEstimator(object):
         """Robot.estimateOpticalTrajectory (:685-715) for the HalfEdge list
         ``halves``: pairs every landmark's observations once, then iterates on
         the device.  Returns the per-iteration (is_calc, delta_sum, det, cond)."""
-        for lm in range(n_landmarks):
-            mine = [h for h in halves if h.getObs().getLandMarkId() == lm]
-            for a, b in itertools.combinations(mine, 2):
-                self.setPairObs(a, b)
+        rows = [[h.getTime(), h.getRobotPoseId(), h.getObs().getLandMarkId(),
+                 h.getObs().getDist(), h.getObs().getDir(), h.getObs().getOrient()] for h in halves]
+        paired = pair_halves(rows, n_landmarks, device=self._device)     # on the device
+        edges = np.concatenate([edge_array(self._rows), paired]) if self._rows else paired
+        seen = set(self._times)
+        for t in np.unique(np.concatenate([edges["time_bfr"], edges["time_aft"]])).tolist():
+            if t not in seen:
+                self._times.append(t)
+        self._rows = edges
         if len(self._times) * 3 <= 3:
+            self._rows, self._lm_ids, self._times = [], [], []
             return np.zeros((1, 4))
         times = sorted(self._times)
         self._upload_poses()

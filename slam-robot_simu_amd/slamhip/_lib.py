@@ -138,6 +138,7 @@ SIGNATURES = {
     "slam_graph_timing": (C.c_int, [_P, _D]),
     "slam_graph_linearize_solve": (C.c_int, [C.POINTER(GraphConfig), _P, C.c_int64, _D, C.c_int64,
                                              _D, C.c_int]),
+    "slam_graph_pair_halves": (C.c_int, [C.c_int64, _P, C.c_int64, C.c_int, _I64, _P]),
 }
 
 _lib = None

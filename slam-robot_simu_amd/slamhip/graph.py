@@ -15,6 +15,36 @@ EDGE_DTYPE = np.dtype([("time_bfr", "<i8"), ("pose_bfr", "<i8"), ("time_aft", "<
                        ("pose_aft", "<i8"), ("obs_bfr", "<f8", (3,)), ("obs_aft", "<f8", (3,))])
 
 
+HALF_DTYPE = np.dtype([("time", "<i8"), ("pose", "<i8"), ("landmark", "<i8"), ("obs", "<f8", (3,))])
+
+
+def pair_halves(halves, n_landmarks, device=0):
+    """Robot.estimateOpticalTrajectory's pairing (graph_based_slam.py:697-703)
+    on the device: ``halves`` rows [time, pose_id, landmark, dist, dir, orient]
+    (or HALF_DTYPE records) in recording order -> slam_graph_edge records, in
+    the reference's order (landmark, then itertools.combinations), each pair
+    ordered as setPairObs orders it (:371-384)."""
+    if not (isinstance(halves, np.ndarray) and halves.dtype == HALF_DTYPE):
+        rows = np.asarray(halves, dtype=np.float64).reshape(-1, 6)
+        rec = np.zeros(len(rows), dtype=HALF_DTYPE)
+        rec["time"], rec["pose"], rec["landmark"] = rows[:, 0], rows[:, 1], rows[:, 2]
+        rec["obs"] = rows[:, 3:6]
+        halves = rec
+    halves = np.ascontiguousarray(halves)
+    lib = _lib.load()
+    n = C.c_int64(0)
+    check(lib.slam_graph_pair_halves(len(halves), halves.ctypes.data_as(C.c_void_p),
+                                     int(n_landmarks), int(device), C.byref(n), None),
+          "slam_graph_pair_halves")
+    out = np.zeros(n.value, dtype=EDGE_DTYPE)
+    if n.value:
+        check(lib.slam_graph_pair_halves(len(halves), halves.ctypes.data_as(C.c_void_p),
+                                         int(n_landmarks), int(device), C.byref(n),
+                                         out.ctypes.data_as(C.c_void_p)),
+              "slam_graph_pair_halves")
+    return out
+
+
 def edge_array(rows):
     """Edge rows [t_bfr, pose_bfr, d, dir, orient, t_aft, pose_aft, d, dir, orient, (lm)]
     -> slam_graph_edge records."""

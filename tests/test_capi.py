@@ -54,3 +54,11 @@ def test_create_without_device_fails_loudly():
         pytest.skip("a GPU is visible")
     with pytest.raises(_lib.SlamError):
         DeviceParticleFilter(100, [[0.0, 0.0]])
+
+
+def test_graph_record_layouts_match_the_c_structs():
+    """slam_graph_edge (4 int64 + 6 double) and slam_graph_half (3 int64 + 3
+    double) as the NumPy record types the bindings pass through ctypes."""
+    from slamhip.graph import EDGE_DTYPE, HALF_DTYPE
+    assert EDGE_DTYPE.itemsize == 80 and HALF_DTYPE.itemsize == 48
+    assert [HALF_DTYPE.fields[f][1] for f in ("time", "pose", "landmark", "obs")] == [0, 8, 16, 24]
