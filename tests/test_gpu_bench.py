@@ -1,0 +1,35 @@
+"""bench.py's output contract on a real GPU: one JSON line with the metric,
+the whole-job value, the roofline object of the fused kernel and the step
+breakdown (short run: no secondary rows, no CPU baselines)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+from conftest import ROOT
+
+pytestmark = pytest.mark.gpu
+
+
+def test_bench_json_contract():
+    env = dict(os.environ)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "8",
+                        "--warmup", "2", "--no-secondary", "--no-cpu-baseline"],
+                       cwd=ROOT, env=env, capture_output=True, text=True, timeout=100)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    for key in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+                "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config",
+                "roofline"):
+        assert key in d, key
+    assert d["n_gpus"] == 1 and d["steps"] == 8 and d["warmup"] == 2
+    assert d["unit"] == "particle-observation updates/s" and d["value"] > 1e10
+    assert abs(d["value"] - 2 ** 20 * 100 / (d["ms_per_step"] / 1e3)) <= 1e-6 * d["value"]
+    rf = d["roofline"]
+    assert rf["bound"] in ("hbm", "mfma") and 0 < rf["frac"] <= 1
+    assert abs(rf["frac"] - rf["achieved"] / rf["peak"]) < 1e-12
+    assert d["config"]["particles_per_gpu"] == 2 ** 20 and d["config"]["landmarks"] == 100
