@@ -243,11 +243,21 @@ __global__ __launch_bounds__(256) void graph_assemble_h_kernel(
     const int64_t s = t / 9;
     const int q = (int)(t - s * 9);
     double acc = (s == 0 && (q == 0 || q == 4 || q == 8)) ? anchor : 0.0;
-    for (int64_t c = cptr[s]; c < cptr[s + 1]; ++c) {
-        const int64_t code = clist[c];
-        const int64_t e = code >> 2;
-        const int part = (int)(code & 3);
-        acc = acc + blocks[(int64_t)(part * 9 + q) * E + e];
+    // groups of 8 contributions: the codes, then the block entries, are loaded
+    // together (a diagonal slot collects ~8 edges); the adds stay in edge order
+    const int64_t c1 = cptr[s + 1];
+    for (int64_t c0 = cptr[s]; c0 < c1; c0 += 8) {
+        int64_t code[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) code[u] = (c0 + u < c1) ? clist[c0 + u] : -1;
+        double v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+            v[u] = (code[u] >= 0) ? blocks[(int64_t)((int)(code[u] & 3) * 9 + q) * E + (code[u] >> 2)]
+                                  : 0.0;
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+            if (code[u] >= 0) acc = acc + v[u];
     }
     val[t] = acc;
 }
@@ -261,9 +271,19 @@ __global__ __launch_bounds__(256) void graph_assemble_b_kernel(
     const int64_t r = t / 3;
     const int a = (int)(t - r * 3);
     double acc = 0.0;
-    for (int64_t c = bptr[r]; c < bptr[r + 1]; ++c) {
-        const int64_t code = blist[c];
-        acc = acc + blocks[(int64_t)(36 + 3 * (code & 1) + a) * E + (code >> 1)];
+    const int64_t c1 = bptr[r + 1];
+    for (int64_t c0 = bptr[r]; c0 < c1; c0 += 8) {
+        int64_t code[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) code[u] = (c0 + u < c1) ? blist[c0 + u] : -1;
+        double v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+            v[u] = (code[u] >= 0) ? blocks[(int64_t)(36 + 3 * (code[u] & 1) + a) * E + (code[u] >> 1)]
+                                  : 0.0;
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+            if (code[u] >= 0) acc = acc + v[u];
     }
     b[t] = acc;
 }
