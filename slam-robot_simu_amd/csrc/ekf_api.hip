@@ -39,7 +39,6 @@ struct slam_ekfslam {
     double* rd = nullptr;          // M
     double* sinv = nullptr;        // M x M
     int64_t* ids = nullptr;        // k
-    double* obs = nullptr;         // k x 3
     double* diag = nullptr;        // n (init_diag staging)
     hipEvent_t ev[6] = {};
     double last_ms[5] = {0, 0, 0, 0, 0};
@@ -129,12 +128,12 @@ int eks_update(slam_ekfslam* h, int32_t k, const int64_t* ids, const double* obs
         SLAM_ARG_CHECK(ids[t] >= 0 && ids[t] < h->n_lm, "slam_ekfslam_update: landmark id out of range");
     const int32_t m = 3 * k;
     const int32_t M = (m + 3) / 4 * 4;
-    SLAM_HIP_TRY(hipMemcpyAsync(h->ids, ids, k * sizeof(int64_t), hipMemcpyHostToDevice, h->stream));
-    SLAM_HIP_TRY(hipMemcpyAsync(h->obs, obs, 3 * k * sizeof(double), hipMemcpyHostToDevice,
-                                h->stream));
+    EksObs ob{};
+    for (int32_t t = 0; t < k; ++t) ob.ids[t] = ids[t];
+    for (int32_t u = 0; u < 3 * k; ++u) ob.obs[u] = obs[u];
     const EksConst c = eks_const(h->cfg);
     SLAM_HIP_TRY(hipEventRecord(h->ev[0], h->stream));
-    hipLaunchKernelGGL(eks_build_kernel, dim3(1), dim3(128), 0, h->stream, h->mu, h->ids, h->obs, k,
+    hipLaunchKernelGGL(eks_build_kernel, dim3(1), dim3(128), 0, h->stream, h->mu, ob, h->ids, k,
                        M, c, h->hs, h->e, h->rd);
     hipLaunchKernelGGL(eks_pht_kernel, dim3((unsigned)((h->n_pad + 255) / 256)), dim3(256), 0,
                        h->stream, h->P, h->n, h->ld, h->n_pad, h->ids, h->hs, k, M, h->pht);
@@ -371,7 +370,6 @@ int slam_ekfslam_create(const slam_ekfslam_config* cfg, int64_t n_landmarks, int
         hipMalloc(&h->rd, kEksMaxM * sizeof(double)) != hipSuccess ||
         hipMalloc(&h->sinv, kEksMaxM * kEksMaxM * sizeof(double)) != hipSuccess ||
         hipMalloc(&h->ids, (kEksMaxM / 3) * sizeof(int64_t)) != hipSuccess ||
-        hipMalloc(&h->obs, kEksMaxM * sizeof(double)) != hipSuccess ||
         hipMalloc(&h->diag, h->n * sizeof(double)) != hipSuccess)
         return bail(fail(SLAM_ERR_HIP, "slam_ekfslam_create: allocation failed (P is n^2 fp64)"));
     for (auto& e : h->ev)
@@ -395,8 +393,7 @@ int slam_ekfslam_destroy(slam_ekfslam* h) {
     if (!h) return SLAM_OK;
     (void)hipSetDevice(h->device);
     for (void* p : {(void*)h->P, (void*)h->mu, (void*)h->pht, (void*)h->kg, (void*)h->hs,
-                    (void*)h->e, (void*)h->rd, (void*)h->sinv, (void*)h->ids, (void*)h->obs,
-                    (void*)h->diag})
+                    (void*)h->e, (void*)h->rd, (void*)h->sinv, (void*)h->ids, (void*)h->diag})
         if (p) (void)hipFree(p);
     for (auto& e : h->ev)
         if (e) (void)hipEventDestroy(e);

@@ -197,8 +197,15 @@ __global__ void eks_predict_pose_kernel(double* __restrict__ P, const int64_t ld
 // Per observation t (landmark j = ids[t]): predicted ScanSensor measurement,
 // its Jacobians (robot Hr, landmark Hl, 3x3 each), the wrapped innovation and
 // the measurement variance diag(scan_cov(range)).  hs: [k][18]; e, rd: [M].
-__global__ void eks_build_kernel(const double* __restrict__ mu, const int64_t* __restrict__ ids,
-                                 const double* __restrict__ obs, const int32_t k, const int32_t M,
+// The observed ids and measurements travel in the kernel arguments (1.3 KB,
+// no host-to-device copies per update); the ids are stored for the later kernels.
+struct EksObs {
+    int64_t ids[kEksMaxM / 3];
+    double obs[kEksMaxM];
+};
+
+__global__ void eks_build_kernel(const double* __restrict__ mu, const EksObs ob,
+                                 int64_t* __restrict__ ids_out, const int32_t k, const int32_t M,
                                  const EksConst c, double* __restrict__ hs, double* __restrict__ e,
                                  double* __restrict__ rd) {
     const int t = threadIdx.x;
@@ -207,7 +214,9 @@ __global__ void eks_build_kernel(const double* __restrict__ mu, const int64_t* _
         rd[u] = 1.0;
     }
     if (t >= k) return;
-    const int64_t j = ids[t];
+    const int64_t j = ob.ids[t];
+    ids_out[t] = j;
+    const double o[3] = {ob.obs[3 * t], ob.obs[3 * t + 1], ob.obs[3 * t + 2]};
     const double xr = mu[0], yr = mu[1], th = mu[2];
     const double lx = mu[3 + 3 * j], ly = mu[4 + 3 * j], lp = mu[5 + 3 * j];
     const double psi = kHalfPi - th;
@@ -230,7 +239,6 @@ __global__ void eks_build_kernel(const double* __restrict__ mu, const int64_t* _
     H[9] = dx / r;  H[10] = dy / r; H[11] = 0.0;
     H[12] = -dy / q; H[13] = dx / q; H[14] = 0.0;
     H[15] = 0.0;    H[16] = 0.0;    H[17] = 1.0;
-    const double* o = obs + 3 * t;
     e[3 * t] = o[0] - rng;
     e[3 * t + 1] = wrap_angle(o[1] - brg);
     e[3 * t + 2] = wrap_angle(o[2] - ori);
