@@ -367,8 +367,34 @@ def gen_graph(seed=0, demo_frames=18, big_steps=300):
     np.savez_compressed(os.path.join(OUT, "graph.npz"), **out)
 
 
+# ------------------------------------------------------- error ellipse
+def gen_ellipse(seed=5):
+    """mylib/error_ellipse.py: chi-squared lookup at table knots, between
+    knots and at the ends; ellipse parameters of random and degenerate 2x2
+    covariances; calc_chi."""
+    from mylib import error_ellipse
+    rs = np.random.RandomState(seed)
+    ps = np.concatenate([[99.0, 99.9, 0.0, 50.0, 95.0, 2.5, 97.3, 12.34, 0.25, 99.95 - 0.05],
+                         rs.uniform(0.0, 99.9, 40)])
+    chi = np.array([float(error_ellipse.ErrorEllipse(p)._ErrorEllipse__chi) for p in ps])
+    A = rs.normal(size=(200, 2, 2)) * rs.uniform(0.01, 10.0, (200, 1, 1))
+    covs = A @ A.transpose(0, 2, 1)
+    extra = np.array([[[16.0, 5.48], [5.48, 9.0]], [[1.0, 0.0], [0.0, 1.0]],
+                      [[2.0, 0.0], [0.0, 1.0]], [[1.0, 0.0], [0.0, 2.0]],
+                      [[1.0, -0.9], [-0.9, 1.0]], [[1e-8, 0.0], [0.0, 1e4]],
+                      [[3.0, 3.0], [3.0, 3.0]], [[0.0, 0.0], [0.0, 0.0]]])
+    covs = np.concatenate([extra, covs])
+    ee = error_ellipse.ErrorEllipse(99.0)
+    out = np.array([ee.calc_error_ellipse(c) for c in covs], dtype=np.float64)
+    ee95 = error_ellipse.ErrorEllipse(95.0)
+    out95 = np.array([ee95.calc_error_ellipse(c) for c in covs], dtype=np.float64)
+    chi_l = np.array([ee.calc_chi(p, c) for p, c in zip(ps, covs)])
+    np.savez_compressed(os.path.join(OUT, "ellipse.npz"), ps=ps, chi=chi, covs=covs,
+                        out99=out, out95=out95, chi_l=chi_l)
+
+
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["units", "pf_c1", "pf_stages", "motion", "ekf", "graph"]
+    which = sys.argv[1:] or ["units", "pf_c1", "pf_stages", "motion", "ekf", "graph", "ellipse"]
     for w in which:
         print("generating", w, flush=True)
         globals()["gen_" + w]()
