@@ -13,9 +13,12 @@ for every step are simulated on the host and uploaded BEFORE the timed region
 
 N > 1 is launched by torch.distributed.run (one process per GPU).  Each rank
 runs its own 1,048,576-particle filter (weak scaling).  --mode sharded makes the
-ranks one filter over N x 2^20 particles (RCCL exchange of weight partials);
---mode replicas (default until the sharded path is validated on hardware) runs
-independent Monte-Carlo realisations with no data-path collective.
+ranks one filter over N x 2^20 particles (slamhip.shard.ShardedFilter: RCCL
+all-gathers of weight partials / reduction records, all-to-all-v of resampled
+particles; host-driven phases, no step graph); --mode replicas (the default:
+the sharded path is validated on one GPU only -- in-process shards and a
+1-rank RCCL group) runs independent Monte-Carlo realisations with no
+data-path collective.
 """
 from __future__ import annotations
 
@@ -353,7 +356,7 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
-    if world > 1:
+    if world > 1 or ("MASTER_ADDR" in os.environ and "RANK" in os.environ):   # torch.distributed.run
         import torch
         import torch.distributed as dist
         torch.cuda.set_device(local_rank)
@@ -370,7 +373,44 @@ def main():
             dist.barrier()
             torch.cuda.synchronize()
 
+    def measure_sharded(likelihood):
+        # one filter over world x 2^20 particles (BASELINE configs[2]): this
+        # rank's shard through slamhip.shard.ShardedFilter; the exchange is
+        # torch.distributed (RCCL over xGMI) at world > 1, in-process at 1.
+        # Direct launches per phase (the host drives the exchange each step).
+        from slamhip.shard import DeviceShard, LocalComm, ShardedFilter, TorchComm
+        n_global = world * NP_PER_GPU
+        shard = DeviceShard(NP_PER_GPU, n_global, rank * NP_PER_GPU, lm, dt=dt, motion="velocity",
+                            likelihood=likelihood, seed=1234, device=local_rank)
+        comm = TorchComm() if dist is not None else LocalComm(1)
+        filt = ShardedFilter([shard], [rank], comm, n_global)
+        nan = float("nan")
+
+        def run(k0, k1):
+            return [filt.step(ctl[k], zs[k], None, nan) for k in range(k0, k1)]
+
+        run(0, args.warmup)
+        barrier_sync()
+        t0 = time.perf_counter()
+        out = run(args.warmup, args.warmup + args.steps)
+        barrier_sync()
+        elapsed = time.perf_counter() - t0
+        lib = shard.lib
+        import ctypes as C
+        lib.slam_pf_enable_timing(shard._h, 1)
+        run(args.warmup + args.steps, total_steps)
+        timing = {}
+        for k in range(4):
+            ms, cnt = C.c_double(0.0), C.c_int64(0)
+            lib.slam_pf_timing(shard._h, k, C.byref(ms), C.byref(cnt))
+            timing[k] = (ms.value, cnt.value)
+        lib.slam_pf_enable_timing(shard._h, 0)
+        filt.close()
+        return elapsed, out, timing
+
     def measure(likelihood):
+        if args.mode == "sharded":
+            return measure_sharded(likelihood)
         pf = DeviceParticleFilter(NP_PER_GPU, lm, dt=dt, motion="velocity",
                                   likelihood=likelihood, seed=1234 + rank, device=local_rank)
         pf.load_observations(zs)

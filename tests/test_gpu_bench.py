@@ -33,3 +33,29 @@ def test_bench_json_contract():
     assert rf["bound"] in ("hbm", "mfma") and 0 < rf["frac"] <= 1
     assert abs(rf["frac"] - rf["achieved"] / rf["peak"]) < 1e-12
     assert d["config"]["particles_per_gpu"] == 2 ** 20 and d["config"]["landmarks"] == 100
+
+
+def _bench_line(cmd):
+    r = subprocess.run(cmd, cwd=ROOT, env=dict(os.environ), capture_output=True, text=True,
+                       timeout=110)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    return json.loads(lines[0])
+
+
+@pytest.mark.parametrize("launcher", ["direct", "torchrun"])
+def test_bench_sharded_mode(launcher):
+    # --mode sharded: the ShardedFilter orchestration over one shard, in-process
+    # (LocalComm) or as a 1-rank RCCL group (TorchComm over nccl)
+    args = [os.path.join(ROOT, "bench.py"), "--mode", "sharded", "--steps", "6", "--warmup", "2",
+            "--no-secondary", "--no-cpu-baseline"]
+    if launcher == "torchrun":
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+               "--master-addr", "127.0.0.1", "--master-port", "29533"] + args
+    else:
+        cmd = [sys.executable] + args
+    d = _bench_line(cmd)
+    assert d["config"]["parallelism"] == "sharded1"
+    assert d["n_gpus"] == 1 and d["steps"] == 6 and d["value"] > 1e9
+    assert d["resample_steps"] >= 0 and d["roofline"]["avg_launch_ms"] > 0
