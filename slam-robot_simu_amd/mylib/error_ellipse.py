@@ -20,22 +20,28 @@ quirk is kept by default so the angles match the reference's plots;
 """
 import numpy as np
 
-# upper cumulative percentage points [%] (2 degrees of freedom) and their
-# chi-squared values: the table of error_ellipse.py:24-33
-_P = np.array([99.9, 99.5, 99, 98.5, 98, 97.5, 97, 96, 95, 94, 93, 92, 91, 90, 85, 80, 75, 70,
-               65, 60, 55, 50, 45, 40, 35, 30, 25, 20, 15, 10, 9, 8, 7, 6, 5, 4, 3, 2.5, 2, 1.5,
-               1, 0.5, 0], dtype=np.float64)
-_CHI2 = np.array([13.81551056, 10.59663473, 9.210340372, 8.399410156, 7.824046011, 7.377758908,
-                  7.013115795, 6.43775165, 5.991464547, 5.626821434, 5.318520074, 5.051457289,
-                  4.815891217, 4.605170186, 3.79423997, 3.218875825, 2.772588722, 2.407945609,
-                  2.099644249, 1.832581464, 1.597015392, 1.386294361, 1.195674002, 1.021651248,
-                  0.861565832, 0.713349888, 0.575364145, 0.446287103, 0.325037859, 0.210721031,
-                  0.188621359, 0.166763218, 0.145141386, 0.123750807, 0.102586589, 0.081643989,
-                  0.060918415, 0.050635616, 0.040405415, 0.030227276, 0.020100672, 0.010025084,
-                  0], dtype=np.float64)
-_ORDER = np.argsort(_P, kind="mergesort")
-_XS = _P[_ORDER]
-_YS = _CHI2[_ORDER]
+# (upper cumulative percentage point [%], chi-squared value) for 2 degrees of
+# freedom, ascending: the table of error_ellipse.py:24-33 (its literal values,
+# not -2 ln(1 - p/100), so the lookup returns the reference's doubles)
+_TABLE = (
+    (0.0, 0.0), (0.5, 0.010025084), (1.0, 0.020100672),
+    (1.5, 0.030227276), (2.0, 0.040405415), (2.5, 0.050635616),
+    (3.0, 0.060918415), (4.0, 0.081643989), (5.0, 0.102586589),
+    (6.0, 0.123750807), (7.0, 0.145141386), (8.0, 0.166763218),
+    (9.0, 0.188621359), (10.0, 0.210721031), (15.0, 0.325037859),
+    (20.0, 0.446287103), (25.0, 0.575364145), (30.0, 0.713349888),
+    (35.0, 0.861565832), (40.0, 1.021651248), (45.0, 1.195674002),
+    (50.0, 1.386294361), (55.0, 1.597015392), (60.0, 1.832581464),
+    (65.0, 2.099644249), (70.0, 2.407945609), (75.0, 2.772588722),
+    (80.0, 3.218875825), (85.0, 3.79423997), (90.0, 4.605170186),
+    (91.0, 4.815891217), (92.0, 5.051457289), (93.0, 5.318520074),
+    (94.0, 5.626821434), (95.0, 5.991464547), (96.0, 6.43775165),
+    (97.0, 7.013115795), (97.5, 7.377758908), (98.0, 7.824046011),
+    (98.5, 8.399410156), (99.0, 9.210340372), (99.5, 10.59663473),
+    (99.9, 13.81551056),
+)
+_XS = np.array([t[0] for t in _TABLE], dtype=np.float64)
+_YS = np.array([t[1] for t in _TABLE], dtype=np.float64)
 
 
 def chi_squared(p):
@@ -58,8 +64,8 @@ class ErrorEllipse(object):
     (error_ellipse.py:15-68)."""
 
     def __init__(self, p, column_vectors=False):
-        self.p = _P.copy()
-        self.square_x = _CHI2.copy()
+        self.p = _XS[::-1].copy()            # the reference's (descending) order
+        self.square_x = _YS[::-1].copy()
         self.chi_squared_distribution = chi_squared
         self.__chi = chi_squared(p)
         self._column = bool(column_vectors)
