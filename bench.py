@@ -73,9 +73,25 @@ def simulate_world(n_steps, seed=1):
     return lm, zs, (vel, omega, dt)
 
 
-def cpu_baseline(seconds_target=12.0):
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    import platform
+    return platform.processor() or "unknown"
+
+
+def _pinned_init(core):
+    os.sched_setaffinity(0, {core})
+
+
+def _cpu_faithful_sample(seconds_target):
     """The oracle's faithful port (per-particle loop of particle_filter.py:185-192,
-    velocity motion model) on ONE host core over a bounded sample."""
+    velocity motion model) over a bounded sample; runs in a child pinned to one core."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import pf_oracle as po
     n = 1 << 15
@@ -97,10 +113,31 @@ def cpu_baseline(seconds_target=12.0):
         _ = (pf.x[i], pf.y[i], pf.th[i])
         t_used += time.perf_counter() - t0
         steps += 1
+    return n, steps, t_used, sorted(os.sched_getaffinity(0))
+
+
+def cpu_baseline(seconds_target=12.0):
+    """The oracle's faithful port on ONE host core (the reference is
+    single-threaded Python): a spawned child pinned with sched_setaffinity
+    (taskset) to the first core this process may use, BLAS threads 1."""
+    import multiprocessing as mp
+    core = min(os.sched_getaffinity(0))
+    saved = {k: os.environ.get(k) for k in ("OPENBLAS_NUM_THREADS", "OMP_NUM_THREADS")}
+    os.environ.update(OPENBLAS_NUM_THREADS="1", OMP_NUM_THREADS="1")
+    try:
+        with mp.get_context("spawn").Pool(1, initializer=_pinned_init, initargs=(core,)) as pool:
+            n, steps, t_used, cpus = pool.apply(_cpu_faithful_sample, (seconds_target,))
+    finally:
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
     return {"value": n * NL * steps / t_used, "unit": "particle-observation updates/s",
-            "cores": 1, "kind": "port",
+            "cores": 1, "kind": "port", "cpu_model": cpu_model(), "pinned_cpus": cpus,
             "sample": f"oracle faithful per-particle loop, {n} particles x {NL} landmarks x "
-                      f"{steps} steps (velocity model), {t_used:.1f} s on 1 core"}
+                      f"{steps} steps (velocity model), {t_used:.1f} s on core {core} "
+                      "(sched_setaffinity, OPENBLAS_NUM_THREADS=1)"}
 
 
 def _vec_shard_steps(args):
@@ -137,19 +174,43 @@ def cpu_baseline_vectorised(n_per_proc=1 << 15, steps=6):
     busy = max(per)
     return {"value": procs * n_per_proc * NL * steps / busy,
             "unit": "particle-observation updates/s", "cores": procs, "kind": "port",
+            "cpu_model": cpu_model(),
             "sample": f"oracle vectorised NumPy step (velocity model), {procs} processes x "
                       f"{n_per_proc} particles x {NL} landmarks x {steps} steps, slowest "
                       f"process {busy:.1f} s (pool wall {wall:.1f} s incl. start-up)"}
 
 
+PF_SOURCES = ("pf_kernels.inl", "pf_kernels.hpp", "pf_finalize.inl", "fastmath.hpp", "common.hpp",
+              "pf_api.hip")
+
+
+def pf_sources_sha():
+    """sha256 over the sources the fused PF kernel is compiled from."""
+    import hashlib
+    h = hashlib.sha256()
+    for name in PF_SOURCES:
+        with open(os.path.join(ROOT, "slam-robot_simu_amd", "csrc", name), "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()[:16]
+
+
 def load_pmc_traffic():
+    """HBM bytes per launch of the fused kernel from the rocprofv3 PMC passes of
+    tools/pmc.sh (profiles/pmc_traffic.json, FETCH_SIZE x2 + WRITE_SIZE per the
+    microarch guide).  The counters cannot be read from inside this process;
+    the file records the sources it was measured on, and a figure measured on
+    other sources is reported as null (stale), never as this kernel's."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(path) as f:
             d = json.load(f)
-        return d.get("fused_kernel_hbm_bytes_per_launch")
     except Exception:
-        return None
+        return None, "no profiles/pmc_traffic.json"
+    cur = pf_sources_sha()
+    if d.get("sources_sha") != cur:
+        return None, f"stale: measured on sources {d.get('sources_sha')}, current {cur}"
+    return d.get("fused_kernel_hbm_bytes_per_launch"), \
+        f"rocprofv3 PMC ({d.get('source')}), sources {cur}"
 
 
 # ----------------------------------------------------------- secondary rows
@@ -447,7 +508,7 @@ def main():
     value = updates / elapsed
     fused_avg_s = fused_ms / 1e3 / max(fused_n, 1)
     achieved_tf = FLOPS_PER_UPDATE[args.likelihood] * NP_PER_GPU * NL / fused_avg_s / 1e12
-    traffic = load_pmc_traffic()
+    traffic, traffic_src = load_pmc_traffic()
     line = {
         "metric": METRIC,
         "value": value,
@@ -466,10 +527,12 @@ def main():
                                "motion model, systematic resample",
                    "particles_per_gpu": NP_PER_GPU, "landmarks": NL,
                    "likelihood": args.likelihood, "parallelism": f"{args.mode}{world}"},
-        "roofline": {"bound": "mfma", "kernel": "pf_fused_kernel (predict+likelihood)",
+        "roofline": {"bound": "valu_fp64", "kernel": "pf_fused_kernel (predict+likelihood)",
                      "achieved": achieved_tf, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": achieved_tf / FP64_PEAK_TFLOPS, "traffic": traffic,
-                     "note": "fp64-VALU bound; peak = MI355X fp64 (vector = matrix) 78.6 TF; "
+                     "traffic_source": traffic_src,
+                     "note": "fp64-VALU bound (not HBM, not MFMA); peak = MI355X fp64 vector "
+                             "78.6 TF; "
                              f"{FLOPS_PER_UPDATE[args.likelihood]} algorithmic flops/update (fma = 2, exp = div = 1)",
                      "avg_launch_ms": fused_avg_s * 1e3,
                      "hbm_gbs_algorithmic": BYTES_PER_PARTICLE * NP_PER_GPU / fused_avg_s / 1e9},

@@ -31,6 +31,10 @@ extern "C" {
  * reports this code from the call that hit it. */
 #define SLAM_ERR_INDEX (-3)
 #define SLAM_ERR_STATE (-4)
+/* slam_graph_optimize: the PCG solve of an iteration did not converge within
+ * pcg_max_iter (the dense path's singular gate is not an error: is_calc = 0
+ * ends the loop as in graph_based_slam.py:706-709). */
+#define SLAM_ERR_SOLVE (-5)
 #define SLAM_ERR_COMM (-6)
 
 int slam_version(void);
@@ -124,6 +128,18 @@ int slam_pf_set_scan_merged(slam_pf* h, int32_t on);
 /* external != 0: run on the caller's HIP stream (e.g. torch.cuda.current_stream();
  * NULL = the default stream).  external == 0: a private stream again. */
 int slam_pf_set_stream(slam_pf* h, void* hip_stream, int32_t external);
+
+/* ====================================================================
+ * MotionModel -- replaces motion_model.py:14-86 for a batch of poses
+ * (batch = 1 is the reference's single call).
+ *   params:  dt, a1..a6                                   (motion_model.py:20-29)
+ *   poses:   n x 3 (x, y, theta) host array; out: n x 3 (may alias poses)
+ *   normals: n x 3 standard normals, per pose in the draw order (v, w, gamma)
+ *            of moveWithNoise (:46-48; the std handed to normal() is sigma**2,
+ *            kept); NULL: moveWithoutNoise (:64-86).
+ * ==================================================================== */
+int slam_motion_velocity(const double* params, int64_t n, const double* poses, double v, double w,
+                         const double* normals, double* out, int device);
 
 /* ====================================================================
  * Sharded particle filter (BASELINE config 3): one handle per GPU holds
@@ -230,6 +246,9 @@ int slam_ekfslam_set_state(slam_ekfslam* h, const double* mu, const double* P);
 int slam_ekfslam_init_diag(slam_ekfslam* h, const double* mu, const double* p_diag);
 /* P may be NULL; when given it receives the full symmetric n x n matrix. */
 int slam_ekfslam_get_state(slam_ekfslam* h, double* mu, double* P);
+/* k rows of the symmetric P (rows[k] indices; out: k x n), O(k n) -- for
+ * checking a 7.2 GB P without copying it to the host. */
+int slam_ekfslam_get_rows(slam_ekfslam* h, int64_t k, const int64_t* rows, double* out);
 /* Prediction: robot pose through the motion model, P <- F P F^T + Q on the
  * robot rows/columns (O(n)). control = {v, omega}. */
 int slam_ekfslam_predict(slam_ekfslam* h, const double* control);
@@ -285,10 +304,14 @@ int slam_graph_get_poses(slam_graph* h, double* poses);
 int slam_graph_set_edges(slam_graph* h, int64_t n_edges, const slam_graph_edge* edges);
 /* updateEstPose: linearise every edge at the current poses, assemble H and
  * b, gate, solve, update the poses.  stats[4] = {is_calc, sum delta^2, det,
- * cond} (:514); det/cond are NaN on the PCG path. */
+ * cond} (:514).  On the PCG path det/cond are NaN and the reference's gate
+ * (0.1 < det, cond < 1e15, :496) is not formed: is_calc = 1 means PCG
+ * converged with positive curvature, 0 that it hit pcg_max_iter (poses
+ * unchanged). */
 int slam_graph_update(slam_graph* h, double* stats);
 /* estimateOpticalTrajectory's loop: update until sum delta^2 < delta_sum_th
- * (:692-706) or max_iter; stats: max_iter x 4 (or NULL). */
+ * (:692-706) or max_iter; stats: max_iter x 4 (or NULL).  Returns
+ * SLAM_ERR_SOLVE (with *n_iter set) when a PCG solve fails to converge. */
 int slam_graph_optimize(slam_graph* h, double delta_sum_th, int32_t max_iter, double* stats,
                         int32_t* n_iter);
 /* The last assembled system: times (n_times), H (3n_times squared, dense, or

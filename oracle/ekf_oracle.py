@@ -166,3 +166,40 @@ def ekfslam_step(mu, P, control, obs_ids, obs, dt, q_robot, noise):
     mu[2] = wrap_angle(mu[2])
     P = P - K @ S @ K.T
     return mu, P
+
+
+def ekfslam_update_rows(mu, P_idx, P_rows, rows, obs_ids, obs, noise):
+    """The update half of ``ekfslam_step`` evaluated on selected rows of P only
+    (O(n m), for checking an n = 30,003 covariance without an n x n host copy).
+
+    ``P_idx``: rows idx = (0, 1, 2, 3+3j, 4+3j, 5+3j for j in obs_ids) of the
+    symmetric prior P (|idx| x n) -- H is non-zero only in those columns, so
+    P H^T = P_idx^T H_idx^T.  ``P_rows``: the prior's rows ``rows`` (r x n).
+    Returns (mu_new, P_rows_new) with P_new = P - K (P H^T)^T, K = P H^T S^-1
+    (= P - K S K^T of ekfslam_step)."""
+    idx = [0, 1, 2]
+    for j in obs_ids:
+        idx += [3 + 3 * j, 4 + 3 * j, 5 + 3 * j]
+    idx = np.asarray(idx)
+    k = len(obs_ids)
+    m = 3 * k
+    Hs = np.zeros((m, idx.size))
+    innov = np.zeros(m)
+    Rb = np.zeros((m, m))
+    for t, (j, o) in enumerate(zip(obs_ids, obs)):
+        lm = mu[3 + 3 * j:6 + 3 * j]
+        zhat = scan_predict(mu[:3], lm)
+        Hr, Hl = scan_jacobian(mu[:3], lm)
+        Hs[3 * t:3 * t + 3, :3] = Hr
+        Hs[3 * t:3 * t + 3, 3 + 3 * t:6 + 3 * t] = Hl
+        e = o - zhat
+        e[1] = wrap_angle(e[1])
+        e[2] = wrap_angle(e[2])
+        innov[3 * t:3 * t + 3] = e
+        Rb[3 * t:3 * t + 3, 3 * t:3 * t + 3] = scan_cov(o[0], *noise)
+    PHt = P_idx.T @ Hs.T                       # n x m
+    S = Hs @ PHt[idx] + Rb
+    K = PHt @ np.linalg.inv(S)
+    mu = mu + K @ innov
+    mu[2] = wrap_angle(mu[2])
+    return mu, P_rows - K[np.asarray(rows)] @ PHt.T

@@ -456,6 +456,29 @@ int slam_ekfslam_get_state(slam_ekfslam* h, double* mu, double* P) {
     return SLAM_OK;
 }
 
+int slam_ekfslam_get_rows(slam_ekfslam* h, int64_t k, const int64_t* rows, double* out) {
+    SLAM_ARG_CHECK(h && (k == 0 || (rows && out)) && k >= 0, "slam_ekfslam_get_rows: bad argument");
+    for (int64_t r = 0; r < k; ++r)
+        SLAM_ARG_CHECK(rows[r] >= 0 && rows[r] < h->n, "slam_ekfslam_get_rows: row out of range");
+    SLAM_HIP_TRY(hipSetDevice(h->device));
+    // batches of rows through the K scratch (n_pad x kEksMaxM doubles) and the
+    // id scratch (kEksMaxM / 3 int64)
+    const int64_t chunk = std::min<int64_t>(kEksMaxM / 3,
+                                            std::max<int64_t>(1, (h->n_pad * kEksMaxM) / h->n));
+    for (int64_t r0 = 0; r0 < k; r0 += chunk) {
+        const int64_t cnt = std::min<int64_t>(chunk, k - r0);
+        SLAM_HIP_TRY(hipMemcpyAsync(h->ids, rows + r0, cnt * sizeof(int64_t), hipMemcpyHostToDevice,
+                                    h->stream));
+        hipLaunchKernelGGL(eks_gather_rows_kernel, dim3((unsigned)((h->n + 255) / 256), (unsigned)cnt),
+                           dim3(256), 0, h->stream, h->P, h->n, h->ld, h->ids, h->kg);
+        SLAM_HIP_TRY(hipGetLastError());
+        SLAM_HIP_TRY(hipMemcpyAsync(out + r0 * h->n, h->kg, cnt * h->n * sizeof(double),
+                                    hipMemcpyDeviceToHost, h->stream));
+        SLAM_HIP_TRY(hipStreamSynchronize(h->stream));
+    }
+    return SLAM_OK;
+}
+
 int slam_ekfslam_predict(slam_ekfslam* h, const double* control) {
     SLAM_ARG_CHECK(h && control, "slam_ekfslam_predict: NULL argument");
     SLAM_HIP_TRY(hipSetDevice(h->device));

@@ -526,6 +526,18 @@ __global__ __launch_bounds__(256) void eks_symmetrize_kernel(const double* __res
     dst[(int64_t)blockIdx.y * n + j] = psym(P, ld, i, j);
 }
 
+// rows[blockIdx.y] of the symmetric P (row i: the stored lower row, then
+// column i of the lower triangle past the diagonal)
+__global__ __launch_bounds__(256) void eks_gather_rows_kernel(const double* __restrict__ P,
+                                                              const int64_t n, const int64_t ld,
+                                                              const int64_t* __restrict__ rows,
+                                                              double* __restrict__ dst) {
+    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t i = rows[blockIdx.y];
+    if (j >= n) return;
+    dst[(int64_t)blockIdx.y * n + j] = psym(P, ld, i, j);
+}
+
 __global__ __launch_bounds__(256) void eks_diag_kernel(double* __restrict__ P, const int64_t n,
                                                        const int64_t ld,
                                                        const double* __restrict__ dg) {

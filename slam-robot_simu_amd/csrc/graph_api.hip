@@ -44,6 +44,7 @@ struct slam_graph {
     hipEvent_t ev[5] = {};
     double last[5] = {0, 0, 0, 0, 0};
     int32_t pcg_last_iters = 0;    // iteration count of the previous PCG solve
+    bool pcg_failed = false;       // the last update's PCG solve did not converge
 };
 
 namespace {
@@ -282,12 +283,14 @@ int solve_pcg(slam_graph* h, double* stats, bool* solved, int32_t* iters) {
     stats[2] = std::numeric_limits<double>::quiet_NaN();
     stats[3] = std::numeric_limits<double>::quiet_NaN();
     *solved = (s.status == 1);
+    h->pcg_failed = !*solved;
     return SLAM_OK;
 }
 
 int do_update(slam_graph* h, double* stats) {
     stats[0] = stats[1] = stats[2] = stats[3] = 0.0;
     for (double& x : h->last) x = 0.0;
+    h->pcg_failed = false;
     if (h->E == 0 || 3 * h->nt <= 3) return SLAM_OK;        // :469 (leng > 3)
     GTRY(linearize_assemble(h));
     const int64_t n = 3 * h->nt;
@@ -424,6 +427,14 @@ int slam_graph_optimize(slam_graph* h, double delta_sum_th, int32_t max_iter, do
         if (stats) std::memcpy(stats + 4 * it, s, sizeof(s));
         dsum = s[1];
         ++it;
+        // is_calc = 0 ends the loop as in the reference (:706-709: sum delta^2 = 0);
+        // on the PCG path that is a solver failure, not a converged trajectory
+        if (h->pcg_failed) {
+            if (n_iter) *n_iter = it;
+            return fail(SLAM_ERR_SOLVE, "slam_graph_optimize: PCG did not converge within "
+                                        "pcg_max_iter iterations; poses left at the last "
+                                        "converged Gauss-Newton step");
+        }
     }
     if (n_iter) *n_iter = it;
     return SLAM_OK;

@@ -148,6 +148,18 @@ int make_lik_const(slam_pf* h) {
     lc.rd2 = 1.0 / lc.d2;
     lc.iso = (lc.sx2 == lc.sy2 && !lc.has_rho) ? 1 : 0;
     lc.pad = 0;
+    // Log-sum fast-path bound.  A factor is at most 1/den (q >= 0), so the log of
+    // the reference's partial product after landmark k is at least
+    // L - (NL - k) max(0, -ln den).  L >= ln(DBL_MIN) + NL max(0, -ln den) + 1
+    // keeps every partial product of particle_filter.py:192 in the normal range
+    // (the 1-nat margin covers the rounding of both sums); below it the kernel
+    // takes the reference's sequential product.  Past NL max(0, -ln den) = 700
+    // the products may overflow: always the sequential product.
+    const double climb = (double)h->nl * std::max(0.0, -std::log(lc.den));
+    lc.normal_min_l = std::log(std::numeric_limits<double>::min()) + 1.0;
+    lc.neg_ln_den = -std::log(lc.den);
+    lc.fast_min_l = climb > 700.0 ? std::numeric_limits<double>::infinity()
+                                  : lc.normal_min_l + climb;
     return SLAM_OK;
 }
 

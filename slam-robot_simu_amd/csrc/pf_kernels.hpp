@@ -47,6 +47,10 @@ struct LikConst {
     double den, rden;       // 2*pi*sx*sy*sqrt(1-rho**2) and RN(1/den)
     double neg_nl_ln_den;   // -NL*log(den) (log-sum form)
     double rsxsy, rd2;      // RN(1/(sx*sy)), RN(1/d2) (log-sum form)
+    double fast_min_l;      // log-sum form: L >= this -> exp(L); below, logsum_slow
+                            // (every partial product provably stays normal above it)
+    double normal_min_l;    // ln(DBL_MIN) + 1: a log prefix above it is a normal partial product
+    double neg_ln_den;      // -log(den): log-prefix increment per landmark
     int32_t has_rho;
     int32_t iso;            // sx2 == sy2 and rho == 0 (log-sum shortcut)
     int32_t nl;

@@ -379,11 +379,89 @@ __device__ __forceinline__ void predict_particle(const double x, const double y,
     }
 }
 
+// One landmark factor in the reference's rounding order
+// (particle_filter.py:187-191: mylib/transform.py:31-35 then mlab.bivariate_normal).
+__device__ __forceinline__ double ref_q(const double xn, const double yn, const double sp,
+                                        const double cp, const double lx, const double ly,
+                                        const double zx, const double zy, const LikConst& lc);
+
+__device__ __forceinline__ double ref_factor(const double xn, const double yn, const double sp,
+                                             const double cp, const double lx, const double ly,
+                                             const double zx, const double zy, const LikConst& lc) {
+    const double q = ref_q(xn, yn, sp, cp, lx, ly, zx, zy, lc);
+    const double e = lc.has_rho ? exp_lean((-q) / lc.d2) : exp_lean((-q) * 0.5);  // d2 == 2 exactly
+    return div_refined(e, lc.den, lc.rden);
+}
+
+// Log-sum slow path for one particle whose total L may leave the normal range
+// somewhere along the reference's sequential product (particle_filter.py:192).
+// Walk the log prefix s_j = log(f_1 ... f_j) to the first landmark j0 where it
+// drops below ln(DBL_MIN) + 1: up to j0 - 1 the reference's partial product is
+// a normal number equal to exp(s_{j0-1}); from j0 on, the factors are formed
+// and multiplied exactly as the reference does (ref_factor), so the subnormal
+// roundings and the zero set are the reference's.  Once the product is 0 it
+// stays 0 (early exit).  The prefix uses the reference's residuals and q
+// (ref_factor's rounding order) summed in double-double, so exp(s) is within
+// ~1e-13 of the reference's normal-range partial product even for particles
+// metres off every landmark (|s| ~ 700, where a plain fp64 chain of 100 sums
+// is off by ~5e-12).
+__device__ __forceinline__ double ref_q(const double xn, const double yn, const double sp,
+                                        const double cp, const double lx, const double ly,
+                                        const double zx, const double zy, const LikConst& lc) {
+    const double dxw = lx - xn;
+    const double dyw = ly - yn;
+    const double rx = fma(-sp, dyw, cp * dxw);
+    const double ry = fma(cp, dyw, sp * dxw);
+    const double dx = rx - zx;
+    const double dy = ry - zy;
+    double q = div_refined(dx * dx, lc.sx2, lc.rsx2) + div_refined(dy * dy, lc.sy2, lc.rsy2);
+    if (lc.has_rho) q = q - ((lc.rho2 * dx) * dy) / lc.sxsy;
+    return q;
+}
+
+__device__ __forceinline__ double logsum_slow(const double xn, const double yn, const double sp,
+                                              const double cp, const double* __restrict__ lm,
+                                              const double* __restrict__ z, const LikConst& lc) {
+    const int nl = lc.nl;
+    double hi = 0.0, lo = 0.0, s_prev = 0.0;
+    int j0 = nl;
+    for (int j = 0; j < nl; ++j) {
+        const double q = ref_q(xn, yn, sp, cp, lm[2 * j], lm[2 * j + 1], z[2 * j], z[2 * j + 1], lc);
+        const double t = hi + q;                         // TwoSum(hi, q)
+        const double bb = t - hi;
+        lo = lo + ((hi - (t - bb)) + (q - bb));
+        hi = t;
+        const double sq = hi + lo;
+        const double s = lc.has_rho ? fma(-sq, lc.rd2, (double)(j + 1) * lc.neg_ln_den)
+                                    : fma(-0.5, sq, (double)(j + 1) * lc.neg_ln_den);
+        if (!(s >= lc.normal_min_l)) {                   // also NaN
+            j0 = j;
+            break;
+        }
+        s_prev = s;
+    }
+    double acc = exp_lean(s_prev);                       // s_prev = 0 -> exactly 1 (j0 = 0)
+    for (int j = j0; j < nl; ++j) {
+        acc = acc * ref_factor(xn, yn, sp, cp, lm[2 * j], lm[2 * j + 1], z[2 * j], z[2 * j + 1], lc);
+        if (acc == 0.0) break;
+    }
+    return acc;
+}
+
 // Likelihood of P particles of one lane (particle_filter.py:170-192 with
 // mylib/transform.py:31-35 per landmark).  The landmark loop is shared: each
 // landmark and observation is loaded once (scalar loads, uniform across the
 // wave) and applied to the P particles, whose accumulators are independent
 // dependency chains.  sp/cp: sin/cos(pi/2 - th) of each particle.
+//
+// LOGSUM: prod_j exp(-q_j/d2)/den = exp(L), L = -sum_j q_j/d2 - NL ln den, one
+// exp per particle.  Two accumulators per particle (the x and y squares) keep
+// the rounding of the sum within ~5e-13 relative of the weight on the fast path
+// (a single chain reaches 8e-13 at L ~ -650 and 5e-12 at L ~ -700).  A particle whose L is
+// below lc.fast_min_l -- where some partial product of the reference's
+// sequential loop could have left the normal range (subnormal or zero) --
+// takes logsum_slow instead, so the zero set and the subnormal roundings are
+// the reference's (identical zero sets, <= 1e-12 relative).
 template <int LIK, int P>
 __device__ __forceinline__ void likelihood_lanes(const double* xn, const double* yn,
                                                  const double* sp, const double* cp,
@@ -391,37 +469,25 @@ __device__ __forceinline__ void likelihood_lanes(const double* xn, const double*
                                                  const double* __restrict__ z, const LikConst& lc,
                                                  double* bn) {
     const int nl = lc.nl;
-    double acc[P];
     if (LIK == SLAM_LIK_PRODUCT) {
-        // particle_filter.py:185-192 factor by factor, in NumPy's rounding order
+        double acc[P];
 #pragma unroll
         for (int k = 0; k < P; ++k) acc[k] = 1.0;
         for (int j = 0; j < nl; ++j) {
             const double lx = lm[2 * j], ly = lm[2 * j + 1], zx = z[2 * j], zy = z[2 * j + 1];
 #pragma unroll
-            for (int k = 0; k < P; ++k) {
-                const double dxw = lx - xn[k];
-                const double dyw = ly - yn[k];
-                // OpenBLAS dgemm order for (rot @ diff.T): fma(r01, d1, r00*d0)
-                const double rx = fma(-sp[k], dyw, cp[k] * dxw);
-                const double ry = fma(cp[k], dyw, sp[k] * dxw);
-                const double dx = rx - zx;
-                const double dy = ry - zy;
-                double q = div_refined(dx * dx, lc.sx2, lc.rsx2) + div_refined(dy * dy, lc.sy2, lc.rsy2);
-                if (lc.has_rho) q = q - ((lc.rho2 * dx) * dy) / lc.sxsy;
-                const double e = lc.has_rho ? exp((-q) / lc.d2) : exp((-q) * 0.5);  // d2 == 2 exactly
-                const double f = div_refined(e, lc.den, lc.rden);
-                acc[k] = acc[k] * f;                        // ndarray.prod: left to right (1*f = f)
-            }
+            for (int k = 0; k < P; ++k)
+                acc[k] = acc[k] * ref_factor(xn[k], yn[k], sp[k], cp[k], lx, ly, zx, zy, lc);
         }
 #pragma unroll
         for (int k = 0; k < P; ++k) bn[k] = acc[k];
         return;
     }
-    // one exp per particle: prod_j exp(-q_j/d2)/den = exp(-sum_j q_j/d2 - NL ln den)
-#pragma unroll
-    for (int k = 0; k < P; ++k) acc[k] = 0.0;
+    double L[P];
     if (lc.iso) {
+        double a[P][2];
+#pragma unroll
+        for (int k = 0; k < P; ++k) a[k][0] = a[k][1] = 0.0;
 #pragma unroll 4
         for (int j = 0; j < nl; ++j) {
             const double lx = lm[2 * j], ly = lm[2 * j + 1], zx = z[2 * j], zy = z[2 * j + 1];
@@ -431,32 +497,83 @@ __device__ __forceinline__ void likelihood_lanes(const double* xn, const double*
                 const double dyw = ly - yn[k];
                 const double dx = fma(cp[k], dxw, fma(-sp[k], dyw, -zx));
                 const double dy = fma(sp[k], dxw, fma(cp[k], dyw, -zy));
-                acc[k] = fma(dx, dx, acc[k]);
-                acc[k] = fma(dy, dy, acc[k]);
+                a[k][0] = fma(dx, dx, a[k][0]);
+                a[k][1] = fma(dy, dy, a[k][1]);
             }
         }
 #pragma unroll
-        for (int k = 0; k < P; ++k)
-            bn[k] = exp_lean(fma(-0.5, acc[k] * lc.rsx2, lc.neg_nl_ln_den));
-        return;
-    }
-    for (int j = 0; j < nl; ++j) {
-        const double lx = lm[2 * j], ly = lm[2 * j + 1], zx = z[2 * j], zy = z[2 * j + 1];
+        for (int k = 0; k < P; ++k) L[k] = fma(-0.5, (a[k][0] + a[k][1]) * lc.rsx2, lc.neg_nl_ln_den);
+    } else {
+        double a[P][2];
+#pragma unroll
+        for (int k = 0; k < P; ++k) a[k][0] = a[k][1] = 0.0;
+        for (int j = 0; j < nl; j += 2) {
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                if (j + h >= nl) break;
+                const double lx = lm[2 * (j + h)], ly = lm[2 * (j + h) + 1];
+                const double zx = z[2 * (j + h)], zy = z[2 * (j + h) + 1];
+#pragma unroll
+                for (int k = 0; k < P; ++k) {
+                    const double dxw = lx - xn[k];
+                    const double dyw = ly - yn[k];
+                    const double dx = fma(cp[k], dxw, fma(-sp[k], dyw, -zx));
+                    const double dy = fma(sp[k], dxw, fma(cp[k], dyw, -zy));
+                    double q = fma(dx * lc.rsx2, dx, (dy * lc.rsy2) * dy);
+                    if (lc.has_rho) q = q - ((lc.rho2 * dx) * dy) * lc.rsxsy;
+                    a[k][h] = a[k][h] + q;
+                }
+            }
+        }
 #pragma unroll
         for (int k = 0; k < P; ++k) {
-            const double dxw = lx - xn[k];
-            const double dyw = ly - yn[k];
-            const double dx = fma(cp[k], dxw, fma(-sp[k], dyw, -zx));
-            const double dy = fma(sp[k], dxw, fma(cp[k], dyw, -zy));
-            double q = fma(dx * lc.rsx2, dx, (dy * lc.rsy2) * dy);
-            if (lc.has_rho) q = q - ((lc.rho2 * dx) * dy) * lc.rsxsy;
-            acc[k] = acc[k] + q;
+            const double s = a[k][0] + a[k][1];
+            L[k] = lc.has_rho ? fma(-s, lc.rd2, lc.neg_nl_ln_den) : fma(-0.5, s, lc.neg_nl_ln_den);
         }
     }
+    bool slow[P];
+    int any_slow = 0;
 #pragma unroll
-    for (int k = 0; k < P; ++k)
-        bn[k] = exp_lean(lc.has_rho ? fma(-acc[k], lc.rd2, lc.neg_nl_ln_den)
-                                    : fma(-0.5, acc[k], lc.neg_nl_ln_den));
+    for (int k = 0; k < P; ++k) {
+        bn[k] = exp_lean(L[k]);
+        slow[k] = !(L[k] >= lc.fast_min_l);                 // also NaN
+        any_slow |= slow[k] ? 1 : 0;
+    }
+#ifdef SLAM_PROBE_NO_SLOW                                  // timing probe only: not exact
+    any_slow = 0;
+#endif
+    // The few slow particles of the block (bench steady state: ~0.1% of them,
+    // in ~15% of the waves on some steps) are compacted through LDS and taken
+    // one per lane, so a block runs one slow walk in parallel instead of one
+    // per wave and particle slot.  Block-uniform: every lane reaches the barriers.
+    if (__syncthreads_or(any_slow)) {
+        constexpr int kMax = 256 * P;
+        __shared__ int s_nslow;
+        __shared__ double s_pt[4][kMax];
+        __shared__ double s_bn[kMax];
+        if (threadIdx.x == 0) s_nslow = 0;
+        __syncthreads();
+        int slot[P];
+#pragma unroll
+        for (int k = 0; k < P; ++k) {
+            slot[k] = -1;
+            if (slow[k]) {
+                slot[k] = atomicAdd(&s_nslow, 1);
+                s_pt[0][slot[k]] = xn[k];
+                s_pt[1][slot[k]] = yn[k];
+                s_pt[2][slot[k]] = sp[k];
+                s_pt[3][slot[k]] = cp[k];
+            }
+        }
+        __syncthreads();
+        const int ns = s_nslow;
+        for (int t = threadIdx.x; t < ns; t += blockDim.x)
+            s_bn[t] = logsum_slow(s_pt[0][t], s_pt[1][t], s_pt[2][t], s_pt[3][t], lm, z, lc);
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < P; ++k)
+            if (slot[k] >= 0) bn[k] = s_bn[slot[k]];
+    }
 }
 
 // The fused step kernel: [resample gather +] predict + likelihood + weight.
@@ -466,7 +583,12 @@ __device__ __forceinline__ void likelihood_lanes(const double* xn, const double*
 // b kPartPer + kDeferPPT t + k -- 16-byte loads and stores, one device-RNG
 // pair per lane -- and the previous weights are w_un / s (read and rewritten
 // in place), followed by the block epilogue that replaces the normalise pass.
-#ifdef SLAM_FUSED_WPE
+// Four waves per SIMD (<= 128 VGPRs): the log-sum kernel's slow-path product
+// would otherwise push it to 129 and three waves.
+#ifndef SLAM_FUSED_WPE
+#define SLAM_FUSED_WPE 4
+#endif
+#if SLAM_FUSED_WPE > 0
 #define SLAM_FUSED_ATTR __attribute__((amdgpu_waves_per_eu(SLAM_FUSED_WPE)))
 #else
 #define SLAM_FUSED_ATTR

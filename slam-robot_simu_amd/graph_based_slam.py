@@ -66,6 +66,12 @@ def _row(h_bfr, h_aft):
             h_aft.getTime(), h_aft.getRobotPoseId(), oa.getDist(), oa.getDir(), oa.getOrient()]
 
 
+def _rec_row(r):
+    """slam_graph_edge record -> setPairObs row (the form _row builds)."""
+    return [int(r["time_bfr"]), int(r["pose_bfr"]), *r["obs_bfr"].tolist(),
+            int(r["time_aft"]), int(r["pose_aft"]), *r["obs_aft"].tolist()]
+
+
 class TrajectoryEstimator(object):
     """Pose-graph estimator (GPU linearise / assemble / solve)."""
 
@@ -130,19 +136,34 @@ class TrajectoryEstimator(object):
         rows = [[h.getTime(), h.getRobotPoseId(), h.getObs().getLandMarkId(),
                  h.getObs().getDist(), h.getObs().getDir(), h.getObs().getOrient()] for h in halves]
         paired = pair_halves(rows, n_landmarks, device=self._device)     # on the device
-        edges = np.concatenate([edge_array(self._rows), paired]) if self._rows else paired
+
+        def times_of(edges):
+            return np.unique(np.concatenate([edges["time_bfr"], edges["time_aft"]])).tolist()
+
+        pending = edge_array(self._rows) if len(self._rows) else None
+        first = np.concatenate([pending, paired]) if pending is not None else paired
         seen = set(self._times)
-        for t in np.unique(np.concatenate([edges["time_bfr"], edges["time_aft"]])).tolist():
+        for t in times_of(first) if len(first) else []:
             if t not in seen:
                 self._times.append(t)
-        self._rows = edges
         if len(self._times) * 3 <= 3:
-            self._rows, self._lm_ids, self._times = [], [], []
+            # updateEstPose's leng <= 3 branch (:469): nothing solved, and the
+            # pairs of this iteration stay pending (the reference clears only
+            # inside the branch, :509-512); the loop ends (delta_sum = 0)
+            self._rows = [_rec_row(r) for r in first]
             return np.zeros((1, 4))
-        times = sorted(self._times)
         self._upload_poses()
-        self._dev.set_edges(self._rows)
-        st = self._dev.optimize(DELTA_SUM_TH, max_iter)
-        self._write_back(times)
+        # iteration 1 (:697-706): pairs set before this call -- linearised at
+        # their setPairObs time, i.e. at these same poses -- plus this pairing
+        self._dev.set_edges(first)
+        st = [self._dev.update()]
+        self._write_back(sorted(self._times))
         self._rows, self._lm_ids, self._times = [], [], []
-        return st
+        # later iterations: only the re-paired edges, re-linearised each time;
+        # an iteration with is_calc = 0 returns delta_sum = 0 and ends the loop
+        if DELTA_SUM_TH <= st[0][1] and max_iter > 1 and len(paired):
+            if pending is not None:
+                self._dev.set_edges(paired)
+            st += list(self._dev.optimize(DELTA_SUM_TH, max_iter - 1))
+            self._write_back(times_of(paired))
+        return np.array(st, dtype=np.float64).reshape(-1, 4)

@@ -19,6 +19,7 @@ SLAM_ERR_ARG = -1
 SLAM_ERR_HIP = -2
 SLAM_ERR_INDEX = -3
 SLAM_ERR_STATE = -4
+SLAM_ERR_SOLVE = -5
 SLAM_ERR_COMM = -6
 
 MOTION = {"linear": 0, "velocity": 1}
@@ -91,6 +92,8 @@ SIGNATURES = {
     "slam_pf_set_graphs": (C.c_int, [_P, C.c_int32]),
     "slam_pf_set_scan_merged": (C.c_int, [_P, C.c_int32]),
     "slam_pf_set_stream": (C.c_int, [_P, _P, C.c_int32]),
+    "slam_motion_velocity": (C.c_int, [_D, C.c_int64, _D, C.c_double, C.c_double, _D, _D,
+                                       C.c_int]),
     "slam_pf_create_shard": (C.c_int, [C.POINTER(PFConfig), C.c_int64, C.c_int64, C.c_int64,
                                        C.c_int32, _D, C.c_int, C.POINTER(_P)]),
     "slam_pf_shard_sizes": (C.c_int, [_P, _I64]),
@@ -121,6 +124,7 @@ SIGNATURES = {
     "slam_ekfslam_set_state": (C.c_int, [_P, _D, _D]),
     "slam_ekfslam_init_diag": (C.c_int, [_P, _D, _D]),
     "slam_ekfslam_get_state": (C.c_int, [_P, _D, _D]),
+    "slam_ekfslam_get_rows": (C.c_int, [_P, C.c_int64, _I64, _D]),
     "slam_ekfslam_predict": (C.c_int, [_P, _D]),
     "slam_ekfslam_update": (C.c_int, [_P, C.c_int32, _I64, _D]),
     "slam_ekfslam_step": (C.c_int, [_P, _D, C.c_int32, _I64, _D]),
@@ -159,7 +163,10 @@ def load():
         raise ImportError(f"{LIB_PATH} not found: build it with `make -C slam-robot_simu_amd` "
                           "(there is no CPU fallback)")
     lib = C.CDLL(LIB_PATH)
+    variant = "SLAM_HIP_LIB" in os.environ      # development variant: may predate entry points
     for name, (res, args) in SIGNATURES.items():
+        if variant and not hasattr(lib, name):
+            continue
         f = getattr(lib, name)
         f.restype = res
         f.argtypes = args

@@ -153,6 +153,15 @@ class DeviceEKFSLAM:
         check(self._lib.slam_ekfslam_get_state(self._h, dptr(mu), dptr(P)), "slam_ekfslam_get_state")
         return (mu, P) if with_cov else mu
 
+    def get_rows(self, rows):
+        """Rows of the symmetric covariance (k x n) without copying all of P."""
+        rows = np.ascontiguousarray(rows, dtype=np.int64).ravel()
+        out = np.empty((rows.size, self.n))
+        check(self._lib.slam_ekfslam_get_rows(self._h, int(rows.size),
+                                              rows.ctypes.data_as(C.POINTER(C.c_int64)), dptr(out)),
+              "slam_ekfslam_get_rows")
+        return out
+
     def predict(self, control):
         check(self._lib.slam_ekfslam_predict(self._h, dptr(_f64(control, (2,)))),
               "slam_ekfslam_predict")

@@ -228,6 +228,10 @@ class ShardedFilter:
     def __init__(self, shards, ranks, comm, n_global):
         self.shards, self.ranks, self.comm = list(shards), list(ranks), comm
         self.world = comm.world
+        if isinstance(comm, LocalComm):
+            # LocalComm stacks its inputs in list order: shards[i] must be rank i
+            if self.ranks != list(range(self.world)):
+                raise ValueError("LocalComm needs every shard, in rank order (ranks == 0..world-1)")
         self.n_global = int(n_global)
         n = self.shards[0].n
         assert all(s.n == n for s in self.shards) and n * self.world == self.n_global, \

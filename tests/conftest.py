@@ -44,3 +44,29 @@ def stage_weights(tag, n, wseed):
 
 def rle_decode(vals, counts):
     return np.repeat(vals.astype(np.int64), counts)
+
+
+DBL_MIN = np.finfo(np.float64).tiny
+
+
+def weights_match(w, ref, rtol=1e-12, floor=DBL_MIN):
+    """SURVEY 8(a) A6 bar for likelihood weights: identical zero sets, <= rtol
+    relative on weights >= floor, and within 2 units of 2^-1074 below it (the
+    subnormal grid both sides round onto).  A multi-step trajectory passes a
+    larger floor with the absolute bound rtol * floor below it: weights that
+    went through the subnormal range in an earlier step carry that step's
+    precision loss -- the reference's own arithmetic.  Returns the worst
+    relative error seen."""
+    w, ref = np.asarray(w), np.asarray(ref)
+    zw, zr = w == 0, ref == 0
+    assert np.array_equal(zw, zr), f"zero sets differ at {np.flatnonzero(zw != zr)[:8]}"
+    nz = ~zr
+    normal = nz & (np.abs(ref) >= floor)
+    rel = np.abs(w[normal] - ref[normal]) / np.abs(ref[normal])
+    worst = float(rel.max()) if rel.size else 0.0
+    assert worst <= rtol, f"max relative weight error {worst:.3g} > {rtol}"
+    sub = nz & ~normal
+    if sub.any():
+        atol = 2 * 2.0 ** -1074 if floor <= DBL_MIN else rtol * floor
+        assert np.all(np.abs(w[sub] - ref[sub]) <= atol)
+    return worst

@@ -30,7 +30,7 @@ def test_bench_json_contract():
     assert d["unit"] == "particle-observation updates/s" and d["value"] > 1e10
     assert abs(d["value"] - 2 ** 20 * 100 / (d["ms_per_step"] / 1e3)) <= 1e-6 * d["value"]
     rf = d["roofline"]
-    assert rf["bound"] in ("hbm", "mfma") and 0 < rf["frac"] <= 1
+    assert rf["bound"] == "valu_fp64" and 0 < rf["frac"] <= 1
     assert abs(rf["frac"] - rf["achieved"] / rf["peak"]) < 1e-12
     assert d["config"]["particles_per_gpu"] == 2 ** 20 and d["config"]["landmarks"] == 100
 

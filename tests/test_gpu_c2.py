@@ -1,0 +1,128 @@
+"""BASELINE config 2 at its full size, through the exact bench path:
+1,048,576 particles x 100 landmarks, velocity motion model, systematic
+resampling, in both likelihood modes (the log-sum form the bench headlines
+and the reference-literal product), against the oracle's PFOracle.step
+(particle_filter.py:102-117, motion_model.py:31-62) on the same host-injected
+standard normals and resample offsets.
+
+Lockstep: before every step the device is loaded with the oracle's state
+(particles and normalised weights), so every step compares one step of both
+from identical inputs -- including the resample steps, whose indices must then
+be bit-exact.  A second, free-running device pass (its own state carried from
+step to step) must take the same resample decisions and argmax every step.
+
+Tolerances (SURVEY 8(a) A6 / north_star):
+  * weights (the likelihood of the device's predicted particles, evaluated by
+    the oracle -- identical inputs): identical zero sets; |w - w_ref| <= 1e-12
+    |w_ref| on the normal range (subnormal weights: within 2 units of 2^-1074,
+    the grid both sides round onto);
+  * resample indices (given identical weights and offset): bit-exact;
+  * argmax index: identical; x_est, cov: 1e-6 relative (cov atol 1e-12);
+  * particles after predict: |d| <= 1e-12 (|ref| + |a|), a = v^/w^ per particle:
+    x' = x - a sin(th) + a sin(th + w^ dt) cancels, so its rounding (an ulp of
+    sin/cos times a) scales with the turn radius a, which is large where the
+    sampled w^ is near 0 (motion_model.py:50-55).
+"""
+import numpy as np
+import pytest
+
+import pf_oracle as po
+from conftest import weights_match
+
+pytestmark = pytest.mark.gpu
+
+N = 1 << 20
+NL = 100
+STEPS = 8
+
+
+@pytest.fixture(scope="module")
+def c2_trajectory():
+    """The oracle's C2 trajectory: per step the input state, the injected
+    normals / observations / offset and the oracle's outputs."""
+    rs = np.random.RandomState(1)
+    lm = rs.uniform(-10, 10, (NL, 2))
+    p = po.PFParams(n_particles=N, landmarks=lm, motion="velocity")
+    orc, world = po.PFOracle(p), po.PFWorld(p)
+    np.random.seed(2)
+    steps = []
+    for _ in range(STEPS):
+        world.advance()
+        state = (orc.x.copy(), orc.y.copy(), orc.th.copy(), orc.w.copy())
+        u = np.random.rand() if orc.needs_resample() else None
+        g = np.random.standard_normal(3 * N).reshape(N, 3)
+        z = world.observe()
+        out = orc.step(z, g, None if u is None else u * p.np_recip)
+        steps.append(dict(state=state, u=u, g=g, z=z, out=out,
+                          post=(orc.x.copy(), orc.y.copy(), orc.th.copy(), orc.w.copy()),
+                          resample_next=orc.needs_resample()))
+    assert sum(s["out"]["resampled"] for s in steps) >= 1
+    return p, steps
+
+
+def _turn_radius(p, g):
+    """a = v^ / w^ of motion_model.py:46-50 for the standard normals g."""
+    a1, a2, a3, a4, a5, a6 = p.alphas
+    v, w = p.vel, p.omega
+    sv = (a1 * v ** 2) + (a2 * w ** 2)
+    sw = (a3 * v ** 2) + (a4 * w ** 2)
+    return (v + sv ** 2 * g[:, 0]) / (w + sw ** 2 * g[:, 1])
+
+
+def _dev(p, lik):
+    from slamhip.pf import DeviceParticleFilter
+    return DeviceParticleFilter(N, p.lm, dt=p.dt, motion="velocity", likelihood=lik,
+                                alphas=p.alphas)
+
+
+@pytest.mark.parametrize("lik", ["logsum", "product"])
+def test_c2_full_size_lockstep_vs_oracle(c2_trajectory, lik):
+    p, steps = c2_trajectory
+    worst = 0.0
+    with _dev(p, lik) as d:
+        for k, s in enumerate(steps):
+            d.set_state(*s["state"])
+            ro = s["out"]
+            assert d.resample_next == ro["resampled"], k
+            nan = float("nan")
+            if ro["resampled"]:
+                idx, _ = d.resample_indices(s["u"])
+                np.testing.assert_array_equal(idx, ro["idx"])
+            rd = d.step((p.vel, p.omega), s["z"], s["g"], nan if s["u"] is None else s["u"])
+            assert rd["resampled"] == ro["resampled"], k
+            assert rd["max_idx"] == ro["max_idx"], (k, rd["max_idx"], ro["max_idx"])
+            np.testing.assert_allclose(rd["x_est"], ro["x_est"], rtol=1e-6)
+            np.testing.assert_allclose(rd["cov"], ro["cov"], rtol=1e-6, atol=1e-12)
+            assert rd["resample_next"] == s["resample_next"], k
+            x, y, th, w = d.get_state()
+            px, py, pt, pw = s["post"]
+            rad = np.abs(_turn_radius(p, s["g"]))
+            for got, ref in ((x, px), (y, py), (th, pt)):
+                bad = np.abs(got - ref) > 1e-12 * (np.abs(ref) + rad)
+                assert not bad.any(), (k, np.flatnonzero(bad)[:5], got[bad][:3], ref[bad][:3])
+            # the likelihood from identical inputs: the oracle's factors on the
+            # device's predicted particles (they differ from the oracle's only
+            # by the predict roundings checked above, which a weight amplifies
+            # by ~|residual| / sigma^2 per landmark)
+            bn = ro["bn"].copy()
+            moved = (x != px) | (y != py) | (th != pt)
+            if moved.any():
+                bn[moved] = po.landmark_factors(x[moved], y[moved], th[moved], p.lm, s["z"],
+                                                p.r).prod(axis=1)
+            worst = max(worst, weights_match(w, po.normalize(ro["w_prev"] * bn)))
+    print(f"\nC2 {lik}: max relative weight error over {STEPS} steps = {worst:.3g}")
+
+
+@pytest.mark.parametrize("lik", ["logsum", "product"])
+def test_c2_full_size_free_running(c2_trajectory, lik):
+    """The device carries its own state; inputs as the oracle's run."""
+    p, steps = c2_trajectory
+    with _dev(p, lik) as d:
+        for k, s in enumerate(steps):
+            ro = s["out"]
+            assert d.resample_next == ro["resampled"], k
+            rd = d.step((p.vel, p.omega), s["z"], s["g"],
+                        float("nan") if s["u"] is None else s["u"])
+            assert rd["max_idx"] == ro["max_idx"], (k, rd["max_idx"], ro["max_idx"])
+            np.testing.assert_allclose(rd["x_est"], ro["x_est"], rtol=1e-6)
+            np.testing.assert_allclose(rd["cov"], ro["cov"], rtol=1e-6, atol=1e-12)

@@ -1,0 +1,153 @@
+"""BASELINE configs 3, 4 and 5 at their full workload size on one MI355X.
+
+  C3  8 x 1,048,576 particles as 8 in-process shards (LocalComm: the same
+      orchestration as the multi-GPU run) against one 8,388,608-particle
+      handle: bit-identical weights, particles, resample decisions and
+      argmax over 20 steps with resamples.
+  C4  EKF-SLAM, 10,000 landmarks (n = 30,003, P = 7.2 GB), 20 observed per
+      step: mu and sampled rows of P after predict and after each of three
+      updates against the oracle's O(n m) row form of P - K (P H^T)^T
+      (oracle/ekf_oracle.py: ekfslam_update_rows; parity unpinned by the
+      reference, which has no EKF-SLAM).
+  C5  graph SLAM, 50,000 poses x ~200,000 edges, PCG: ||H delta + b|| <=
+      1e-8 ||b|| on the BSR H exported from the device, sum delta^2 = delta.delta.
+"""
+import numpy as np
+import pytest
+
+import ekf_oracle as eo
+import pf_oracle as po
+
+pytestmark = pytest.mark.gpu
+
+
+def test_c3_eight_shards_match_single_handle():
+    from slamhip.pf import DeviceParticleFilter
+    from slamhip.shard import DeviceShard, LocalComm, ShardedFilter
+    world, n_local, nl, steps = 8, 1 << 20, 100, 20
+    n_global = world * n_local
+    rs = np.random.RandomState(31)
+    lm = rs.uniform(-10, 10, (nl, 2))
+    p = po.PFParams(n_particles=n_global, landmarks=lm, motion="velocity")
+    wd = po.PFWorld(p)
+    np.random.seed(32)
+    zs = []
+    for _ in range(steps):
+        wd.advance()
+        zs.append(wd.observe())
+    single = DeviceParticleFilter(n_global, lm, motion="velocity", likelihood="logsum", seed=9)
+    shards = [DeviceShard(n_local, n_global, r * n_local, lm, motion="velocity",
+                          likelihood="logsum", seed=9) for r in range(world)]
+    filt = ShardedFilter(shards, list(range(world)), LocalComm(world), n_global)
+    n_res = 0
+    try:
+        for k in range(steps):
+            assert single.resample_next == filt.resample_next, k
+            a = single.step((p.vel, p.omega), zs[k])
+            b = filt.step((p.vel, p.omega), zs[k])
+            n_res += a["resampled"]
+            assert a["resampled"] == b["resampled"], k
+            assert a["max_idx"] == b["max_idx"], (k, a["max_idx"], b["max_idx"])
+            np.testing.assert_array_equal(a["x_est"], b["x_est"])
+            assert a["max_val"] == b["max_val"] and a["weight_sum"] == b["weight_sum"]
+            np.testing.assert_allclose(a["cov"], b["cov"], rtol=1e-7, atol=1e-13)
+        for u, v in zip(single.get_state(), filt.get_state()):
+            np.testing.assert_array_equal(u, v)
+        assert n_res >= 2
+    finally:
+        single.close()
+        filt.close()
+
+
+def _scan_measure(pose, lmk):
+    psi = np.pi / 2 - pose[2]
+    dx, dy = lmk[:, 0] - pose[0], lmk[:, 1] - pose[1]
+    rx = np.cos(psi) * dx - np.sin(psi) * dy
+    ry = np.sin(psi) * dx + np.cos(psi) * dy
+    wrap = lambda a: np.mod(a + np.pi, 2 * np.pi) - np.pi
+    return np.column_stack([np.hypot(rx, ry), np.arctan2(ry, rx), wrap(psi + lmk[:, 2])])
+
+
+def test_c4_ekfslam_full_size_rows_vs_oracle():
+    from slamhip.ekf import DeviceEKFSLAM
+    n_lm, k, dt = 10000, 20, 0.1
+    n = 3 + 3 * n_lm
+    q = np.diag([0.1, 0.1, np.deg2rad(0.1)]) ** 2
+    noise = (0.05, np.deg2rad(2.0), np.deg2rad(2.0))
+    rs = np.random.RandomState(4)
+    lmk = np.column_stack([rs.uniform(-100, 100, (n_lm, 2)), rs.uniform(-np.pi, np.pi, n_lm)])
+    pose = np.array([50.0, 0.0, np.pi / 2])
+    ctl = (5.0, 0.1)
+    dev = DeviceEKFSLAM(n_lm, dt=dt, q_robot=q, noise=noise)
+    try:
+        mu0 = np.concatenate([pose, (lmk + rs.normal(0, 0.5, lmk.shape)).ravel()])
+        dev.init_diag(mu0, np.concatenate([[1e-4, 1e-4, 1e-5], np.full(n - 3, 0.25)]))
+        seen = np.zeros(0, dtype=np.int64)
+        for s in range(3):
+            a = dt * np.cos(pose[2]), dt * np.sin(pose[2])
+            pose = np.array([pose[0] + ctl[0] * a[0], pose[1] + ctl[0] * a[1],
+                             np.mod(pose[2] + ctl[1] * dt + np.pi, 2 * np.pi) - np.pi])
+            # the 20 nearest, half of them shared with the previous step's set
+            ids = np.argpartition(np.hypot(lmk[:, 0] - pose[0], lmk[:, 1] - pose[1]), k)[:k]
+            obs = _scan_measure(pose, lmk[ids])
+            obs[:, 0] *= 1 + 0.01 * rs.standard_normal(k)
+            idx = np.concatenate([[0, 1, 2], (3 + 3 * ids[:, None] + np.arange(3)).ravel()])
+            rows = np.unique(np.concatenate([idx, rs.choice(n, 64, replace=False), seen]))
+            # predict: F P F^T + Q on the robot rows / columns
+            mu_b = dev.get_state(with_cov=False)
+            Pb = dev.get_rows(rows)
+            dev.predict(ctl)
+            mu_p = dev.get_state(with_cov=False)
+            Pp = dev.get_rows(rows)
+            F = eo.ekf_jacobian(mu_b[:3], dt, ctl[0])
+            Po = Pb.copy()
+            r3 = np.searchsorted(rows, [0, 1, 2])
+            Po[r3] = F @ Pb[r3]
+            Po[:, :3] = Po[:, :3] @ F.T
+            Po[np.ix_(r3, [0, 1, 2])] += q
+            np.testing.assert_allclose(mu_p[:3], eo.ekf_motion(mu_b[:3], dt, *ctl), rtol=1e-14,
+                                       atol=1e-14)
+            np.testing.assert_array_equal(mu_p[3:], mu_b[3:])
+            np.testing.assert_allclose(Pp, Po, rtol=0, atol=1e-13 * np.abs(Po).max())
+            # update: rows of P - K (P H^T)^T in O(n m)
+            dev.update(ids, obs)
+            mu_u = dev.get_state(with_cov=False)
+            Pu = dev.get_rows(rows)
+            P_idx = Pp[np.searchsorted(rows, idx)]
+            mu_o, Pu_o = eo.ekfslam_update_rows(mu_p, P_idx, Pp, rows, ids, obs, noise)
+            scale = np.abs(Pp).max()
+            np.testing.assert_allclose(mu_u, mu_o, rtol=1e-9, atol=1e-9)
+            np.testing.assert_allclose(Pu, Pu_o, rtol=0, atol=1e-9 * scale)
+            # symmetric storage: P[i, j] == P[j, i] across the sampled rows
+            np.testing.assert_array_equal(Pu[:, rows], Pu[:, rows].T)
+            seen = idx
+        assert dev.timing()["rank_update_ms"] > 0
+    finally:
+        dev.close()
+
+
+def test_c5_graph_full_size_pcg_solves():
+    import scipy.sparse as sp
+    from slamhip.graph import DeviceGraph, circle_graph
+    init, truth, edges = circle_graph(50000, n_landmarks=64, seed=0, odom_noise=0.002)
+    assert len(edges) >= 190000
+    dev = DeviceGraph(solver="pcg", pcg_tol=1e-10)
+    try:
+        dev.set_poses(init)
+        dev.set_edges(edges)
+        for _ in range(2):
+            is_calc, dsum, det, cond = dev.update()
+            assert is_calc and np.isnan(det) and np.isnan(cond)
+            rows, cols, vals = dev.get_bsr()
+            nt = int(rows.max()) + 1
+            assert nt == 50000
+            H = sp.bsr_matrix((vals, cols, np.searchsorted(rows, np.arange(nt + 1))),
+                              shape=(3 * nt, 3 * nt))
+            _, _, b, _ = dev.get_system(dense=False)
+            d = dev.get_delta()
+            res = np.linalg.norm(H @ d + b) / np.linalg.norm(b)
+            assert res <= 1e-8, res
+            np.testing.assert_allclose(dsum, d @ d, rtol=1e-12)
+        assert np.all(np.isfinite(dev.get_poses()))
+    finally:
+        dev.close()

@@ -4,25 +4,22 @@ the reference-generated golden fixtures.  Runs on the GPU box (-m gpu).
 Tolerances (stated per test):
   * bit-exact: resampling indices given identical weights and offset, np.sum
     order, linear-model prediction noise addition;
-  * weights: |w - w_ref| <= 1e-11 |w_ref| + 1e-280 (GPU exp/sin/cos differ from
-    NumPy's by <= 1 ulp; weights below 1e-280 are underflow territory where the
-    reference's own sequential product has already lost precision);
+  * one likelihood step from identical inputs (both modes): identical zero sets
+    and <= 1e-12 relative on the non-zero weights (SURVEY 8(a) A6;
+    conftest.weights_match);
+  * multi-step trajectories (weights carried over steps, ulp differences of
+    exp/sin/cos compound): identical zero sets, 1e-9 relative above 1e-290 and
+    1e-299 absolute below (weights that passed through the subnormal range);
   * pose / covariance: 1e-6 relative (north_star), with identical max_idx.
 """
 import numpy as np
 import pytest
 
-from conftest import golden, heavy_weights, rle_decode, stage_weights
+from conftest import golden, heavy_weights, rle_decode, stage_weights, weights_match
 
 import pf_oracle as po
 
 pytestmark = pytest.mark.gpu
-
-
-def _close_w(a, b, rtol=1e-11, atol=1e-280):
-    a, b = np.asarray(a), np.asarray(b)
-    bad = np.abs(a - b) > rtol * np.abs(b) + atol
-    assert not bad.any(), f"{bad.sum()} weights differ; first at {np.argmax(bad)}: {a[bad][:3]} vs {b[bad][:3]}"
 
 
 @pytest.fixture(scope="module")
@@ -66,7 +63,8 @@ def test_likelihood_stage(slamhip_pf, tag, lik):
         d.set_state(px[0], px[1], px[2], pw)
         out = d.update(g[f"lik_{tag}_z"])
         _, _, _, w = d.get_state()
-    _close_w(w, ref)
+    worst = weights_match(w, ref, rtol=1e-12)
+    print(f"likelihood {tag} {lik}: max relative weight error {worst:.3g}")
     assert out["max_idx"] == int(np.argmax(ref))
 
 
@@ -121,7 +119,7 @@ def test_c1_end_to_end_vs_reference(lik):
         if k in keep:
             j = keep[k]
             np.testing.assert_allclose(px, g["px_keep"][j], rtol=1e-6, atol=1e-9)
-            _close_w(pf.weights, g["pw_keep"][j], rtol=1e-9, atol=1e-250)
+            weights_match(pf.weights, g["pw_keep"][j], rtol=1e-9, floor=1e-290)
     np.testing.assert_array_equal(res, g["resampled"])
     np.testing.assert_array_equal(max_idx, g["max_idx"])
     np.testing.assert_allclose(x_est, g["x_est"], rtol=1e-6, atol=1e-9)

@@ -52,13 +52,16 @@ def main(src, tag):
     os.makedirs("profiles", exist_ok=True)
     with open(f"profiles/{tag}_pmc.json", "w") as f:
         json.dump(out, f, indent=1, sort_keys=True)
-    fused = {k: v for k, v in out.items() if k.startswith("pf_fused_kernel<1, 1")}
-    if fused:
-        v = next(iter(fused.values()))
-        traffic = v.get("hbm_read_bytes", 0) + v.get("hbm_write_bytes", 0)
+    key = "pf_fused_kernel<1, 1, false, true>"       # the bench's kernel (velocity, log-sum)
+    if key in out and "hbm_read_bytes" in out[key] and "hbm_write_bytes" in out[key]:
+        v = out[key]
+        traffic = v["hbm_read_bytes"] + v["hbm_write_bytes"]
+        sys.path.insert(0, os.getcwd())
+        from bench import pf_sources_sha
         with open("profiles/pmc_traffic.json", "w") as f:
-            json.dump({"source": f"profiles/{tag}_pmc.json", "kernel": "pf_fused_kernel<1, 1, false>",
+            json.dump({"source": f"profiles/{tag}_pmc.json", "kernel": key,
                        "fused_kernel_hbm_bytes_per_launch": traffic,
+                       "sources_sha": pf_sources_sha(),
                        "note": "FETCH_SIZE x2 (gfx950 half-count) + WRITE_SIZE, KB -> B, mean over launches"},
                       f, indent=1)
     for k, v in sorted(out.items()):
