@@ -142,6 +142,19 @@ int slam_motion_velocity(const double* params, int64_t n, const double* poses, d
                          const double* normals, double* out, int device);
 
 /* ====================================================================
+ * RCCL communicator (one process per GPU).  RCCL is loaded at run time
+ * (dlopen librccl.so.1); slam_comm_unique_id on one rank, the 128 bytes
+ * broadcast by the caller's bootstrap, slam_comm_create on every rank.
+ * ==================================================================== */
+typedef struct slam_comm slam_comm;
+int slam_comm_unique_id(uint8_t* id_out /* 128 bytes */);
+int slam_comm_create(const uint8_t* id, int32_t world, int32_t rank, int device, slam_comm** out);
+int slam_comm_destroy(slam_comm* comm);
+int slam_comm_info(slam_comm* comm, int32_t* world, int32_t* rank);
+/* recv (host, world * bytes) <- send (host, bytes) of every rank (bootstrap data) */
+int slam_comm_all_gather_host(slam_comm* comm, const void* send, void* recv, int64_t bytes);
+
+/* ====================================================================
  * Sharded particle filter (BASELINE config 3): one handle per GPU holds
  * particles [gbase, gbase + n_local) of a filter of n_global particles.
  * The caller runs the phases in order and exchanges the small device
@@ -173,6 +186,41 @@ int slam_pf_shard_normalize(slam_pf* h, const double* d_all_partials, int64_t np
                             void* d_record);
 int slam_pf_shard_finish(slam_pf* h, const void* d_all_records, int32_t world,
                          slam_pf_result* res);
+
+/* ====================================================================
+ * Sharded particle filter, device-resident step (BASELINE config 3).
+ * One filter of n_global particles split into contiguous shards; a
+ * slam_dist groups the shards this process holds -- all of them (LOCAL:
+ * several shards on one GPU, phases enqueued shard by shard on one stream) or
+ * one (one process per GPU).  Exchanges are peer-memory pushes into every
+ * rank's exchange region (fine-grained HBM, opened by the peers through IPC
+ * handles) with device-side signalling; every kernel gates on the device
+ * resample flag, so a step needs no host decision and slam_dist_run replays
+ * K steps per hipGraph.  Results are identical on every rank and bit-identical
+ * to one handle holding all particles (particle_filter.py:102-117).
+ * ==================================================================== */
+typedef struct slam_dist slam_dist;
+/* the standard split: rank r holds [gbase, gbase + n_local) */
+int slam_dist_shard_range(int64_t n_global, int32_t world, int32_t rank, int64_t* gbase,
+                          int64_t* n_local);
+/* a shard handle for slam_dist (device RNG; every shard but the last holds a
+ * multiple of 8192 particles) */
+int slam_pf_create_dist_shard(const slam_pf_config* cfg, int64_t n_local, int64_t n_global,
+                              int64_t gbase, int32_t n_landmarks, const double* landmarks, int device,
+                              slam_pf** out);
+/* shards: the held shards in rank order (n_held == world: LOCAL, ranks 0..world-1;
+ * n_held == 1: rank rank0, connect before stepping).  The shards must outlive it. */
+int slam_dist_create(slam_pf** shards, int32_t n_held, int32_t world, int32_t rank0, slam_dist** out);
+int slam_dist_destroy(slam_dist* d);
+int slam_dist_handle_size(int64_t* bytes);
+int slam_dist_export(slam_dist* d, void* blob);                 /* n_held x handle size */
+int slam_dist_connect(slam_dist* d, const void* all_blobs);     /* world x handle size, rank order */
+int slam_dist_connect_comm(slam_dist* d, slam_comm* comm);      /* export + RCCL all-gather + connect */
+/* one step from host inputs (observations staged in slot 0, device RNG) */
+int slam_dist_step(slam_dist* d, const double* control, const double* z, slam_pf_result* res);
+int slam_dist_load_observations(slam_dist* d, int32_t n_steps, const double* z_all);
+int slam_dist_run(slam_dist* d, int32_t first_step, int32_t n_steps, const double* controls,
+                  slam_pf_result* results);
 
 /* ====================================================================
  * EKF localisation -- replaces ExtendedKalmanFilter

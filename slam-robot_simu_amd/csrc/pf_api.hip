@@ -11,6 +11,7 @@
 
 #include "pf_kernels.inl"
 #include "pf_shard.inl"
+#include "pf_dist.inl"
 
 namespace slam {
 
@@ -604,6 +605,15 @@ int stage_inputs(slam_pf* h, const double* control, const double* z, const doubl
 }  // namespace
 
 #include "pf_shard_api.inl"
+#include "pf_dist_api.inl"
+
+#ifdef SLAM_PROBE_COUNT_SLOW
+extern "C" int slam_probe_slow_count(unsigned long long* out) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_probe_slow), 16) != hipSuccess) return -1;
+    unsigned long long z[2] = {0, 0};
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_probe_slow), z, 16) == hipSuccess ? 0 : -1;
+}
+#endif
 
 #ifdef SLAM_PROBE
 extern "C" int slam_probe_read(unsigned long long* out, int count) {

@@ -1,0 +1,433 @@
+// pf_dist_api.inl -- C-ABI of the sharded particle filter's device-resident
+// step (included by pf_api.hip; kernels in pf_dist.inl).
+//
+// A slam_dist groups the shards this process holds: all of them (LOCAL: tests,
+// or several shards on one GPU -- one shared stream, kernels enqueued phase by
+// phase across the shards) or one (one process per GPU).  Each held shard owns
+// an exchange region in fine-grained device memory; in the one-per-process form
+// the regions are exported with hipIpcGetMemHandle, gathered by the caller's
+// bootstrap (slam_comm_all_gather_host over RCCL, or any other channel) and
+// opened by every peer.
+
+struct slam_dist {
+    int world = 1, rank0 = 0, nloc = 1;
+    bool local = false;
+    int device = 0;
+    std::vector<slam_pf*> sh;                 // held shards, rank order
+    DistLayout L;
+    std::vector<char*> xbuf;                  // exchange region of each held shard
+    std::vector<DistPeers> peers;             // per held shard
+    std::vector<DistScratch*> scr;
+    std::vector<SpecialIn*> spec_g;
+    std::vector<SpecialOut*> spec_go;
+    std::vector<int64_t*> hi;
+    std::vector<int32_t*> bsel, bsel_off;
+    std::vector<unsigned*> tk;                // 4 ticket blocks per held shard
+    std::vector<void*> dallocs;
+    std::vector<void*> opened;                // IPC mappings of peer regions
+    hipStream_t stream = nullptr;             // LOCAL: the shared stream
+    bool connected = false;
+    hipGraphExec_t graph[2] = {nullptr, nullptr};     // kGraphSteps steps per parity
+    hipGraphExec_t graph1[2] = {nullptr, nullptr};    // one step per parity
+};
+
+namespace {
+
+int dist_alloc(slam_dist* d, void** p, size_t bytes) {
+    SLAM_HIP_TRY(hipMalloc(p, bytes ? bytes : 8));
+    d->dallocs.push_back(*p);
+    return SLAM_OK;
+}
+
+void dist_drop_graphs(slam_dist* d) {
+    for (auto* gs : {d->graph, d->graph1})
+        for (int k = 0; k < 2; ++k)
+            if (gs[k]) {
+                (void)hipGraphExecDestroy(gs[k]);
+                gs[k] = nullptr;
+            }
+}
+
+// every phase of one step, phase-major across the held shards
+int dist_enqueue_step(slam_dist* d) {
+    const int m = d->nloc;
+    for (int i = 0; i < m; ++i) {                         // exact cumsum: classify
+        slam_pf* h = d->sh[i];
+        const double delta = 4.0 * (double)h->n_global * 0x1p-53 + 0x1p-45;
+        scan_classify_kernel<<<h->nb_scan, kScanThreads, 0, h->stream>>>(
+            h->w_un, h->n, h->boff, &d->scr[i]->base_off, h->c, h->kincl, h->fexcl, h->bk, h->bf,
+            h->boffk, h->bofff, h->ktot, h->nspec, delta, h->gbase, h->tk + 2 * kTicketWords,
+            h->flags, 0, h->s_cur, h->pc.np_recip, kPartPer);
+    }
+    for (int i = 0; i < m; ++i) {                         // emit + push specials
+        slam_pf* h = d->sh[i];
+        dist_emit_push_kernel<<<h->nb_scan, kScanThreads, 0, h->stream>>>(
+            h->w_un, h->s_cur, h->pc.np_recip, h->n, h->c, h->kincl, h->fexcl, h->boffk, h->bofff,
+            h->spec_in, h->gbase, h->nspec, h->ktot, d->tk[i], h->flags, d->peers[i], step_io(h));
+    }
+    for (int i = 0; i < m; ++i) {                         // fold (waits for the specials)
+        slam_pf* h = d->sh[i];
+        dist_fold_kernel<<<1, 256, 0, h->stream>>>(d->spec_g[i], d->spec_go[i], h->n_global,
+                                                   h->flags, d->scr[i], d->peers[i], step_io(h),
+                                                   h->pc.rstep, h->pc.np_recip, h->cfg.seed);
+    }
+    for (int i = 0; i < m; ++i) {                         // expand + hi + counts
+        slam_pf* h = d->sh[i];
+        dist_expand_hi_kernel<<<h->nb_scan, kScanThreads, 0, h->stream>>>(
+            h->n, h->kincl, h->fexcl, h->boffk, h->bofff, d->spec_go[i], h->c, d->hi[i], d->bsel[i],
+            d->bsel_off[i], d->tk[i] + kTicketWords, h->flags, d->scr[i], d->peers[i], step_io(h),
+            h->n_global, h->pc.rstep, h->pc.np_recip, h->cfg.seed);
+    }
+    for (int i = 0; i < m; ++i) {                         // pack + push items
+        slam_pf* h = d->sh[i];
+        const int c = h->cur;
+        dist_pack_push_kernel<<<h->nb_scan, kScanThreads, 0, h->stream>>>(
+            h->n, h->x[c], h->y[c], h->th[c], d->hi[i], d->bsel_off[i], d->tk[i] + 2 * kTicketWords,
+            h->flags, d->scr[i], d->peers[i], step_io(h));
+    }
+    for (int i = 0; i < m; ++i) {                         // unpack (waits for the items)
+        slam_pf* h = d->sh[i];
+        const int c = h->cur;
+        dist_unpack_kernel<<<grid_for(h->n, 256), 256, 0, h->stream>>>(
+            h->n, h->x[c], h->y[c], h->th[c], d->tk[i] + 3 * kTicketWords, h->flags, d->peers[i],
+            step_io(h));
+    }
+    SLAM_HIP_TRY(hipGetLastError());
+    int rc;
+    for (int i = 0; i < m; ++i)                           // predict + likelihood
+        if ((rc = launch_fused(d->sh[i], d->sh[i]->cfg.motion, false))) return rc;
+    for (int i = 0; i < m; ++i) {                         // record + push
+        slam_pf* h = d->sh[i];
+        const int c = h->cur;
+        dist_record_push_kernel<<<1, kFinThreads, 0, h->stream>>>(
+            h->n, h->dp, h->w_un, h->tail_leaves, h->tail_ops, h->n_tail_leaves, h->n_tail_ops,
+            h->x[c], h->y[c], h->th[c], d->peers[i], step_io(h));
+    }
+    for (int i = 0; i < m; ++i) {                         // global finalize (waits for the records)
+        slam_pf* h = d->sh[i];
+        dist_finalize_kernel<<<1, kFinThreads, 0, h->stream>>>(
+            h->n, h->dp, h->s_cur, h->refp, h->flags, h->cfg.ess_threshold, step_io(h),
+            h->pc.np_recip, h->boff, d->scr[i], d->peers[i]);
+    }
+    SLAM_HIP_TRY(hipGetLastError());
+    return SLAM_OK;
+}
+
+int dist_sync_results(slam_dist* d, int32_t first, int32_t count, slam_pf_result* out) {
+    for (int i = 0; i < d->nloc; ++i) SLAM_HIP_TRY(hipStreamSynchronize(d->sh[i]->stream));
+    int rc = sync_results(d->sh[0], first, count, out);
+    for (int i = 0; i < count; ++i) {
+        const int32_t st = d->sh[0]->res_host[i].status;
+        if (st & kDistStWait) rc = fail(SLAM_ERR_COMM, "sharded step: a peer did not publish in time");
+        if (st & kDistStItems) rc = fail(SLAM_ERR_COMM, "sharded resample: exchange inconsistent");
+    }
+    for (int i = 1; i < d->nloc; ++i) d->sh[i]->resample_next = d->sh[0]->resample_next;
+    return rc;
+}
+
+}  // namespace
+
+extern "C" {
+
+int slam_pf_create_dist_shard(const slam_pf_config* cfg, int64_t n_local, int64_t n_global,
+                              int64_t gbase, int32_t n_landmarks, const double* landmarks, int device,
+                              slam_pf** out) {
+    SLAM_ARG_CHECK(n_local % kSumChunk == 0 || gbase + n_local == n_global,
+                   "slam_pf_create_dist_shard: every shard but the last must hold a multiple of "
+                   "8192 particles (np.sum buffer alignment)");
+    SLAM_ARG_CHECK(n_local <= (int64_t)2048 * kSumChunk, "slam_pf_create_dist_shard: n_local > 2^24");
+    return create_impl(cfg, n_local, n_global, gbase, n_landmarks, landmarks, device, out, true);
+}
+
+// the standard split of N particles over `world` ranks: rank r holds
+// [gbase, gbase + n_local); every shard but the last is a whole number of
+// 8192-element np.sum buffers
+int slam_dist_shard_range(int64_t n_global, int32_t world, int32_t rank, int64_t* gbase,
+                          int64_t* n_local) {
+    SLAM_ARG_CHECK(gbase && n_local && world >= 1 && rank >= 0 && rank < world && n_global >= world,
+                   "slam_dist_shard_range: bad arguments");
+    int64_t nf = (n_global + world - 1) / world;
+    nf = (nf + kSumChunk - 1) / kSumChunk * kSumChunk;
+    const int64_t g = std::min<int64_t>((int64_t)rank * nf, n_global);
+    *gbase = g;
+    *n_local = std::min<int64_t>(nf, n_global - g);
+    return SLAM_OK;
+}
+
+int slam_dist_create(slam_pf** shards, int32_t n_held, int32_t world, int32_t rank0, slam_dist** out) {
+    SLAM_ARG_CHECK(shards && out && n_held >= 1 && world >= 1 && world <= kDistMaxWorld &&
+                       rank0 >= 0 && rank0 + n_held <= world,
+                   "slam_dist_create: bad arguments");
+    SLAM_ARG_CHECK(n_held == 1 || n_held == world,
+                   "slam_dist_create: hold one shard (one process per GPU) or all of them (LOCAL)");
+    *out = nullptr;
+    const int64_t N = shards[0]->n_global;
+    for (int i = 0; i < n_held; ++i) {
+        SLAM_ARG_CHECK(shards[i] && shards[i]->deferred && shards[i]->n_global == N,
+                       "slam_dist_create: shards must come from slam_pf_create_dist_shard, same filter");
+        if (n_held > 1)
+            SLAM_ARG_CHECK(shards[i]->device == shards[0]->device &&
+                               (i == 0 ? shards[i]->gbase == 0
+                                       : shards[i]->gbase == shards[i - 1]->gbase + shards[i - 1]->n),
+                           "slam_dist_create: LOCAL shards must share one device and be contiguous");
+    }
+    if (n_held == world)
+        SLAM_ARG_CHECK(shards[n_held - 1]->gbase + shards[n_held - 1]->n == N,
+                       "slam_dist_create: the shards do not cover the filter");
+    slam_dist* d = new slam_dist();
+    d->world = world;
+    d->rank0 = rank0;
+    d->nloc = n_held;
+    d->local = (n_held == world);
+    d->device = shards[0]->device;
+    d->sh.assign(shards, shards + n_held);
+    SLAM_HIP_TRY(hipSetDevice(d->device));
+    auto bail = [&](int rc) {
+        slam_dist_destroy(d);
+        return rc;
+    };
+    // the largest shard sets the slot sizes (shards are equal but the last)
+    int64_t nmax = 0;
+    for (auto* h : d->sh) nmax = std::max(nmax, h->n);
+    if (!d->local) nmax = std::max<int64_t>(nmax, (N + world - 1) / world);
+    const int64_t nch = (nmax + kSumChunk - 1) / kSumChunk;
+    DistLayout& L = d->L;
+    L.rec_stride = ((int64_t)sizeof(DistRec) + 8 * nch + 255) / 256 * 256;
+    L.cap_spec = nmax;
+    L.cap_item = nmax;
+    int64_t off = 0;
+    auto take = [&](int64_t bytes) {
+        const int64_t o = off;
+        off += (bytes + 4095) / 4096 * 4096;
+        return o;
+    };
+    L.flags = take(3 * kDistMaxWorld * 8);
+    L.g1 = take(2 * world * L.rec_stride);
+    L.spec_hdr = take(16 * world);
+    L.spec = take((int64_t)sizeof(SpecialIn) * L.cap_spec * world);
+    L.item_hdr = take(16 * world);
+    L.item = take((int64_t)sizeof(ShardItem) * L.cap_item * world);
+    L.total = off;
+    int rc;
+    if (d->local) {
+        hipError_t e = hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking);
+        if (e != hipSuccess) return bail(fail(SLAM_ERR_HIP, "slam_dist_create: stream creation failed"));
+    }
+    for (int i = 0; i < n_held; ++i) {
+        slam_pf* h = d->sh[i];
+        if (d->local && (rc = slam_pf_set_stream(h, d->stream, 1))) return bail(rc);
+        void* xb = nullptr;
+        if (hipExtMallocWithFlags(&xb, (size_t)L.total, hipDeviceMallocFinegrained) != hipSuccess)
+            return bail(fail(SLAM_ERR_HIP, "slam_dist_create: fine-grained exchange region allocation failed"));
+        d->xbuf.push_back((char*)xb);
+        SLAM_HIP_TRY(hipMemset(xb, 0, (size_t)L.flags + 3 * kDistMaxWorld * 8));
+        void *p1, *p2, *p3, *p4, *p5, *p6, *p7;
+        const int32_t nbs = h->nb_scan;
+        if ((rc = dist_alloc(d, &p1, sizeof(DistScratch))) ||
+            (rc = dist_alloc(d, &p2, sizeof(SpecialIn) * (size_t)std::max<int64_t>(N, 1))) ||
+            (rc = dist_alloc(d, &p3, sizeof(SpecialOut) * (size_t)std::max<int64_t>(N, 1))) ||
+            (rc = dist_alloc(d, &p4, sizeof(int64_t) * (size_t)h->n)) ||
+            (rc = dist_alloc(d, &p5, sizeof(int32_t) * (size_t)nbs)) ||
+            (rc = dist_alloc(d, &p6, sizeof(int32_t) * (size_t)nbs)) ||
+            (rc = dist_alloc(d, &p7, sizeof(unsigned) * 4 * kTicketWords)))
+            return bail(rc);
+        SLAM_HIP_TRY(hipMemset(p1, 0, sizeof(DistScratch)));
+        SLAM_HIP_TRY(hipMemset(p7, 0, sizeof(unsigned) * 4 * kTicketWords));
+        d->scr.push_back((DistScratch*)p1);
+        d->spec_g.push_back((SpecialIn*)p2);
+        d->spec_go.push_back((SpecialOut*)p3);
+        d->hi.push_back((int64_t*)p4);
+        d->bsel.push_back((int32_t*)p5);
+        d->bsel_off.push_back((int32_t*)p6);
+        d->tk.push_back((unsigned*)p7);
+        DistPeers P{};
+        P.world = world;
+        P.rank = rank0 + i;
+        P.L = L;
+        d->peers.push_back(P);
+    }
+    // shard bases.  LOCAL: the handles'.  One shard per process: the standard
+    // split, n_full = ceil(N / world) rounded up to whole np.sum buffers, the
+    // last rank taking the rest (slam_dist_shard_range)
+    int64_t gb[kDistMaxWorld + 1];
+    if (d->local) {
+        for (int q = 0; q < world; ++q) gb[q] = d->sh[q]->gbase;
+    } else {
+        int64_t nf = 0;
+        slam_dist_shard_range(N, world, 0, &gb[0], &nf);
+        for (int q = 0; q < world; ++q) slam_dist_shard_range(N, world, q, &gb[q], &nf);
+        int64_t g0 = 0, nl = 0;
+        slam_dist_shard_range(N, world, rank0, &g0, &nl);
+        if (d->sh[0]->gbase != g0 || d->sh[0]->n != nl)
+            return bail(fail(SLAM_ERR_ARG, "slam_dist_create: shard is not slam_dist_shard_range's for its rank"));
+    }
+    gb[world] = N;
+    for (auto& P : d->peers)
+        for (int q = 0; q <= world; ++q) P.gb[q] = gb[q];
+    SLAM_HIP_TRY(hipDeviceSynchronize());
+    if (d->local) {
+        for (auto& P : d->peers)
+            for (int q = 0; q < world; ++q) P.base[q] = d->xbuf[q];
+        d->connected = true;
+    }
+    *out = d;
+    return SLAM_OK;
+}
+
+int slam_dist_handle_size(int64_t* bytes) {
+    SLAM_ARG_CHECK(bytes, "slam_dist_handle_size: NULL argument");
+    *bytes = (int64_t)sizeof(hipIpcMemHandle_t);
+    return SLAM_OK;
+}
+
+// IPC handles of the held shards' exchange regions (n_held x handle size)
+int slam_dist_export(slam_dist* d, void* blob) {
+    SLAM_ARG_CHECK(d && blob, "slam_dist_export: NULL argument");
+    SLAM_HIP_TRY(hipSetDevice(d->device));
+    for (int i = 0; i < d->nloc; ++i) {
+        hipIpcMemHandle_t hd;
+        SLAM_HIP_TRY(hipIpcGetMemHandle(&hd, d->xbuf[i]));
+        std::memcpy((char*)blob + i * sizeof(hd), &hd, sizeof(hd));
+    }
+    return SLAM_OK;
+}
+
+// every rank's handle (world x handle size, rank order): open the peers'
+int slam_dist_connect(slam_dist* d, const void* all_blobs) {
+    SLAM_ARG_CHECK(d && all_blobs, "slam_dist_connect: NULL argument");
+    if (d->connected) return SLAM_OK;
+    SLAM_HIP_TRY(hipSetDevice(d->device));
+    std::vector<char*> base(d->world, nullptr);
+    for (int q = 0; q < d->world; ++q) {
+        if (q >= d->rank0 && q < d->rank0 + d->nloc) {
+            base[q] = d->xbuf[q - d->rank0];
+            continue;
+        }
+        hipIpcMemHandle_t hd;
+        std::memcpy(&hd, (const char*)all_blobs + q * sizeof(hd), sizeof(hd));
+        void* p = nullptr;
+        const hipError_t e = hipIpcOpenMemHandle(&p, hd, hipIpcMemLazyEnablePeerAccess);
+        if (e != hipSuccess)
+            return fail(SLAM_ERR_COMM, std::string("hipIpcOpenMemHandle (peer exchange region): ") +
+                                           hipGetErrorString(e));
+        d->opened.push_back(p);
+        base[q] = (char*)p;
+    }
+    for (auto& P : d->peers)
+        for (int q = 0; q < d->world; ++q) P.base[q] = base[q];
+    d->connected = true;
+    return SLAM_OK;
+}
+
+// one-call bootstrap over an RCCL communicator (rank = comm rank)
+int slam_dist_connect_comm(slam_dist* d, slam_comm* comm) {
+    SLAM_ARG_CHECK(d && comm && d->nloc == 1, "slam_dist_connect_comm: one held shard per process");
+    int32_t w = 0, r = 0;
+    int rc = slam_comm_info(comm, &w, &r);
+    if (rc) return rc;
+    SLAM_ARG_CHECK(w == d->world && r == d->rank0, "slam_dist_connect_comm: communicator rank mismatch");
+    const size_t hs = sizeof(hipIpcMemHandle_t);
+    std::vector<char> mine(hs), all(hs * w);
+    if ((rc = slam_dist_export(d, mine.data()))) return rc;
+    if ((rc = slam_comm_all_gather_host(comm, mine.data(), all.data(), (int64_t)hs))) return rc;
+    return slam_dist_connect(d, all.data());
+}
+
+int slam_dist_destroy(slam_dist* d) {
+    if (!d) return SLAM_OK;
+    (void)hipSetDevice(d->device);
+    if (d->stream) (void)hipStreamSynchronize(d->stream);
+    for (auto* h : d->sh)
+        if (h && h->stream) (void)hipStreamSynchronize(h->stream);
+    dist_drop_graphs(d);
+    for (void* p : d->opened) (void)hipIpcCloseMemHandle(p);
+    for (char* p : d->xbuf) (void)hipFree(p);
+    for (void* p : d->dallocs) (void)hipFree(p);
+    // LOCAL: the shards keep running on private streams again
+    if (d->local)
+        for (auto* h : d->sh)
+            if (h) (void)slam_pf_set_stream(h, nullptr, 0);
+    if (d->stream) (void)hipStreamDestroy(d->stream);
+    delete d;
+    return SLAM_OK;
+}
+
+// One step of every held shard (device RNG noise and resample offset; the
+// observations of this step staged in slot 0).  res: the global result
+// (identical on every rank).
+int slam_dist_step(slam_dist* d, const double* control, const double* z, slam_pf_result* res) {
+    SLAM_ARG_CHECK(d && control && d->connected, "slam_dist_step: bad argument or not connected");
+    SLAM_HIP_TRY(hipSetDevice(d->device));
+    int rc;
+    for (auto* h : d->sh)
+        if ((rc = stage_inputs(h, control, z, nullptr, std::nan("")))) return rc;
+    if ((rc = dist_enqueue_step(d))) return rc;
+    for (auto* h : d->sh) h->stepno++;
+    return dist_sync_results(d, 0, 1, res);
+}
+
+int slam_dist_load_observations(slam_dist* d, int32_t n_steps, const double* z_all) {
+    SLAM_ARG_CHECK(d, "slam_dist_load_observations: NULL handle");
+    dist_drop_graphs(d);
+    for (auto* h : d->sh) {
+        const int rc = slam_pf_load_observations(h, n_steps, z_all);
+        if (rc) return rc;
+    }
+    return SLAM_OK;
+}
+
+// n_steps device-resident steps from loaded observations, replayed as
+// captured hipGraphs (kGraphSteps per graph); results of the first held shard.
+int slam_dist_run(slam_dist* d, int32_t first_step, int32_t n_steps, const double* controls,
+                  slam_pf_result* results) {
+    SLAM_ARG_CHECK(d && controls && n_steps > 0 && d->connected, "slam_dist_run: bad argument");
+    SLAM_HIP_TRY(hipSetDevice(d->device));
+    for (auto* h : d->sh) {
+        SLAM_ARG_CHECK(first_step >= 0 && first_step + n_steps <= h->z_steps,
+                       "slam_dist_run: steps outside the loaded observations");
+        SLAM_HIP_TRY(hipMemcpyAsync(h->ctl + 2 * first_step, controls, 2 * n_steps * sizeof(double),
+                                    hipMemcpyHostToDevice, h->stream));
+        const int rc = set_ctr(h, first_step);
+        if (rc) return rc;
+    }
+    const bool graphs = d->sh[0]->use_graph;
+    hipStream_t s = d->sh[0]->stream;          // LOCAL: the shared stream; else the shard's
+    auto capture = [&](hipGraphExec_t& ge, int steps) -> int {
+        std::vector<int> cur0;
+        for (auto* h : d->sh) cur0.push_back(h->cur);
+        hipGraph_t g;
+        SLAM_HIP_TRY(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+        int rc2 = SLAM_OK;
+        for (int k = 0; k < steps && rc2 == SLAM_OK; ++k) rc2 = dist_enqueue_step(d);
+        const hipError_t e = hipStreamEndCapture(s, &g);
+        for (int i = 0; i < d->nloc; ++i) d->sh[i]->cur = cur0[i];
+        if (rc2) return rc2;
+        if (e != hipSuccess) return fail(SLAM_ERR_HIP, "slam_dist_run: hipStreamEndCapture failed");
+        SLAM_HIP_TRY(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
+        (void)hipGraphDestroy(g);
+        return SLAM_OK;
+    };
+    int rc;
+    int32_t k = 0;
+    while (k < n_steps) {
+        const int par = d->sh[0]->cur;
+        if (graphs) {
+            const bool multi = n_steps - k >= kGraphSteps;
+            hipGraphExec_t& ge = multi ? d->graph[par] : d->graph1[par];
+            if (!ge && (rc = capture(ge, multi ? kGraphSteps : 1))) return rc;
+            SLAM_HIP_TRY(hipGraphLaunch(ge, s));
+            const int done = multi ? kGraphSteps : 1;
+            if (done & 1)
+                for (auto* h : d->sh) h->cur = 1 - h->cur;
+            k += done;
+            for (auto* h : d->sh) h->stepno += done;
+        } else {
+            if ((rc = dist_enqueue_step(d))) return rc;
+            ++k;
+            for (auto* h : d->sh) h->stepno++;
+        }
+    }
+    return dist_sync_results(d, first_step, n_steps, results);
+}
+
+}  // extern "C"

@@ -21,6 +21,10 @@ __device__ unsigned long long g_probe[32];
 
 namespace slam {
 
+#ifdef SLAM_PROBE_COUNT_SLOW
+__device__ unsigned long long g_probe_slow[2];   // slow particles, blocks with any (probe builds)
+#endif
+
 // ====================================================================
 // wave / block helpers (wave = 64 lanes)
 // ====================================================================
@@ -419,28 +423,70 @@ __device__ __forceinline__ double ref_q(const double xn, const double yn, const 
     return q;
 }
 
-__device__ __forceinline__ double logsum_slow(const double xn, const double yn, const double sp,
-                                              const double cp, const double* __restrict__ lm,
-                                              const double* __restrict__ z, const LikConst& lc) {
+// double-double a + b (TwoSum of the high parts, low parts added, renormalised)
+__device__ __forceinline__ void dd_add(double& ah, double& al, const double bh, const double bl) {
+    const double t = ah + bh;
+    const double bb = t - ah;
+    const double e = ((ah - (t - bb)) + (bh - bb)) + (al + bl);
+    ah = t + e;
+    al = e - (ah - t);
+}
+
+// One slow particle per WAVE (every lane passes the same particle): the log
+// prefix of 64 landmarks at a time -- one ref_q per lane, a double-double
+// inclusive wave scan plus the carry of the previous chunks -- then the first
+// landmark j0 whose prefix leaves the normal range by ballot, and the exact
+// tail from j0 (uniform across the wave).  A lane-serial walk of 100 landmarks
+// is a ~10 us dependency chain; this one is a few hundred issue slots.
+// inlined: a call costs the fused kernel 176 B of scratch and ~10 us per launch
+#ifdef SLAM_SLOW_NOINLINE
+#define SLAM_SLOW_ATTR __noinline__
+#else
+#define SLAM_SLOW_ATTR __forceinline__
+#endif
+__device__ SLAM_SLOW_ATTR double logsum_slow(const double xn, const double yn, const double sp,
+                                           const double cp, const double* __restrict__ lm,
+                                           const double* __restrict__ z, const LikConst& lc) {
     const int nl = lc.nl;
-    double hi = 0.0, lo = 0.0, s_prev = 0.0;
+    const int lane = threadIdx.x & 63;
+    double ch = 0.0, cl = 0.0;               // sum of q over the landmarks before this chunk
+    double s_prev = 0.0;                     // log prefix before j0 (0: empty product = 1)
     int j0 = nl;
-    for (int j = 0; j < nl; ++j) {
-        const double q = ref_q(xn, yn, sp, cp, lm[2 * j], lm[2 * j + 1], z[2 * j], z[2 * j + 1], lc);
-        const double t = hi + q;                         // TwoSum(hi, q)
-        const double bb = t - hi;
-        lo = lo + ((hi - (t - bb)) + (q - bb));
-        hi = t;
-        const double sq = hi + lo;
-        const double s = lc.has_rho ? fma(-sq, lc.rd2, (double)(j + 1) * lc.neg_ln_den)
-                                    : fma(-0.5, sq, (double)(j + 1) * lc.neg_ln_den);
-        if (!(s >= lc.normal_min_l)) {                   // also NaN
-            j0 = j;
+    for (int base = 0; base < nl; base += 64) {
+        const int j = base + lane;
+        double h = (j < nl) ? ref_q(xn, yn, sp, cp, lm[2 * j], lm[2 * j + 1], z[2 * j],
+                                     z[2 * j + 1], lc)
+                            : 0.0;
+        double l = 0.0;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {   // inclusive scan, lower lanes on the left
+            const double oh = __shfl_up(h, d, 64), ol = __shfl_up(l, d, 64);
+            if (lane >= d) {
+                double th = oh, tl = ol;
+                dd_add(th, tl, h, l);
+                h = th;
+                l = tl;
+            }
+        }
+        double th = ch, tl = cl;
+        dd_add(th, tl, h, l);                // + the previous chunks
+        const double sq = th + tl;
+        const double sj = lc.has_rho ? fma(-sq, lc.rd2, (double)(j + 1) * lc.neg_ln_den)
+                                     : fma(-0.5, sq, (double)(j + 1) * lc.neg_ln_den);
+        const unsigned long long below = __ballot(j < nl && !(sj >= lc.normal_min_l));
+        if (below) {
+            const int f = __ffsll((long long)below) - 1;     // first lane below
+            const double sp_lane = __shfl(sj, f > 0 ? f - 1 : 0, 64);
+            j0 = base + f;
+            if (f > 0) s_prev = sp_lane;                     // else the previous chunk's last
             break;
         }
-        s_prev = s;
+        const int last = (nl - base < 64 ? nl - base : 64) - 1;
+        s_prev = __shfl(sj, last, 64);
+        ch = __shfl(th, 63, 64);
+        cl = __shfl(tl, 63, 64);
     }
-    double acc = exp_lean(s_prev);                       // s_prev = 0 -> exactly 1 (j0 = 0)
+    double acc = exp_lean(s_prev);           // s_prev = 0 -> exactly 1 (j0 = 0)
     for (int j = j0; j < nl; ++j) {
         acc = acc * ref_factor(xn, yn, sp, cp, lm[2 * j], lm[2 * j + 1], z[2 * j], z[2 * j + 1], lc);
         if (acc == 0.0) break;
@@ -542,10 +588,10 @@ __device__ __forceinline__ void likelihood_lanes(const double* xn, const double*
 #ifdef SLAM_PROBE_NO_SLOW                                  // timing probe only: not exact
     any_slow = 0;
 #endif
-    // The few slow particles of the block (bench steady state: ~0.1% of them,
-    // in ~15% of the waves on some steps) are compacted through LDS and taken
-    // one per lane, so a block runs one slow walk in parallel instead of one
-    // per wave and particle slot.  Block-uniform: every lane reaches the barriers.
+    // The few slow particles of the block (bench workload: ~1,500 of 2^20 on
+    // every third step, in half of the blocks; ~100 on the step after) are
+    // compacted through LDS and taken one per wave.  Block-uniform: every lane
+    // reaches the barriers.
     if (__syncthreads_or(any_slow)) {
         constexpr int kMax = 256 * P;
         __shared__ int s_nslow;
@@ -567,8 +613,17 @@ __device__ __forceinline__ void likelihood_lanes(const double* xn, const double*
         }
         __syncthreads();
         const int ns = s_nslow;
-        for (int t = threadIdx.x; t < ns; t += blockDim.x)
-            s_bn[t] = logsum_slow(s_pt[0][t], s_pt[1][t], s_pt[2][t], s_pt[3][t], lm, z, lc);
+#ifdef SLAM_PROBE_COUNT_SLOW                               // probe builds only
+        if (threadIdx.x == 0) {
+            atomicAdd(&g_probe_slow[0], (unsigned long long)ns);
+            atomicAdd(&g_probe_slow[1], 1ull);
+        }
+#endif
+        // one slow particle per wave, all 64 lanes on it (wave-uniform loop)
+        for (int t = (int)(threadIdx.x >> 6); t < ns; t += (int)(blockDim.x >> 6)) {
+            const double r = logsum_slow(s_pt[0][t], s_pt[1][t], s_pt[2][t], s_pt[3][t], lm, z, lc);
+            if ((threadIdx.x & 63) == 0) s_bn[t] = r;
+        }
         __syncthreads();
 #pragma unroll
         for (int k = 0; k < P; ++k)

@@ -94,6 +94,23 @@ SIGNATURES = {
     "slam_pf_set_stream": (C.c_int, [_P, _P, C.c_int32]),
     "slam_motion_velocity": (C.c_int, [_D, C.c_int64, _D, C.c_double, C.c_double, _D, _D,
                                        C.c_int]),
+    "slam_comm_unique_id": (C.c_int, [C.c_char_p]),
+    "slam_comm_create": (C.c_int, [C.c_char_p, C.c_int32, C.c_int32, C.c_int, C.POINTER(_P)]),
+    "slam_comm_destroy": (C.c_int, [_P]),
+    "slam_comm_info": (C.c_int, [_P, _I32, _I32]),
+    "slam_comm_all_gather_host": (C.c_int, [_P, _P, _P, C.c_int64]),
+    "slam_dist_shard_range": (C.c_int, [C.c_int64, C.c_int32, C.c_int32, _I64, _I64]),
+    "slam_pf_create_dist_shard": (C.c_int, [C.POINTER(PFConfig), C.c_int64, C.c_int64, C.c_int64,
+                                            C.c_int32, _D, C.c_int, C.POINTER(_P)]),
+    "slam_dist_create": (C.c_int, [C.POINTER(_P), C.c_int32, C.c_int32, C.c_int32, C.POINTER(_P)]),
+    "slam_dist_destroy": (C.c_int, [_P]),
+    "slam_dist_handle_size": (C.c_int, [_I64]),
+    "slam_dist_export": (C.c_int, [_P, _P]),
+    "slam_dist_connect": (C.c_int, [_P, _P]),
+    "slam_dist_connect_comm": (C.c_int, [_P, _P]),
+    "slam_dist_step": (C.c_int, [_P, _D, _D, C.POINTER(PFResult)]),
+    "slam_dist_load_observations": (C.c_int, [_P, C.c_int32, _D]),
+    "slam_dist_run": (C.c_int, [_P, C.c_int32, C.c_int32, _D, C.POINTER(PFResult)]),
     "slam_pf_create_shard": (C.c_int, [C.POINTER(PFConfig), C.c_int64, C.c_int64, C.c_int64,
                                        C.c_int32, _D, C.c_int, C.POINTER(_P)]),
     "slam_pf_shard_sizes": (C.c_int, [_P, _I64]),

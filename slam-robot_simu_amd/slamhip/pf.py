@@ -28,6 +28,24 @@ def numpy_noise_factor(q):
     return np.sqrt(s)[:, None] * v
 
 
+def make_config(n_global, *, dt=0.1, q=None, r=None, x0=(10.0, 0.0, np.pi / 2), motion="linear",
+                likelihood="product", alphas=(0.1,) * 6, ess_threshold=None, seed=0):
+    """slam_pf_config from particle_filter.py:21-84's constants (keyword overrides)."""
+    q = np.diag([0.03, 0.03, np.deg2rad(2.0)]) ** 2 if q is None else np.asarray(q, float)
+    r = np.diag([0.3, 0.3]) ** 2 if r is None else np.asarray(r, float)
+    cfg = PFConfig()
+    cfg.dt = float(dt)
+    cfg.ess_threshold = n_global / 100.0 if ess_threshold is None else float(ess_threshold)
+    cfg.r_cov[:] = [float(v) for v in r.ravel()]
+    cfg.q_factor[:] = [float(v) for v in numpy_noise_factor(q).ravel()]
+    cfg.alphas[:] = [float(v) for v in alphas]
+    cfg.x0[:] = [float(v) for v in x0]
+    cfg.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
+    cfg.motion = _lib.MOTION[motion]
+    cfg.likelihood = _lib.LIKELIHOOD[likelihood]
+    return cfg
+
+
 class DeviceParticleFilter:
     """Particles on one GPU.  Parameters mirror particle_filter.py:21-84."""
 
@@ -38,18 +56,8 @@ class DeviceParticleFilter:
         self.n = int(n_particles)
         self.lm = _f64(landmarks).reshape(-1, 2)
         self.nl = self.lm.shape[0]
-        q = np.diag([0.03, 0.03, np.deg2rad(2.0)]) ** 2 if q is None else np.asarray(q, float)
-        r = np.diag([0.3, 0.3]) ** 2 if r is None else np.asarray(r, float)
-        cfg = PFConfig()
-        cfg.dt = float(dt)
-        cfg.ess_threshold = self.n / 100.0 if ess_threshold is None else float(ess_threshold)
-        cfg.r_cov[:] = [float(v) for v in r.ravel()]
-        cfg.q_factor[:] = [float(v) for v in numpy_noise_factor(q).ravel()]
-        cfg.alphas[:] = [float(v) for v in alphas]
-        cfg.x0[:] = [float(v) for v in x0]
-        cfg.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
-        cfg.motion = _lib.MOTION[motion]
-        cfg.likelihood = _lib.LIKELIHOOD[likelihood]
+        cfg = make_config(self.n, dt=dt, q=q, r=r, x0=x0, motion=motion, likelihood=likelihood,
+                          alphas=alphas, ess_threshold=ess_threshold, seed=seed)
         self.motion = motion
         self.cfg = cfg
         h = C.c_void_p()

@@ -17,6 +17,20 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (runs on the GPU box)")
 
 
+@pytest.fixture(scope="session", autouse=True)
+def _torch_hip_first(request):
+    """When GPU tests run, bring up PyTorch's HIP runtime before libslam_hip
+    touches the device (the torch-based shard tests share the process)."""
+    if any(item.get_closest_marker("gpu") for item in request.session.items):
+        try:
+            import torch
+            if torch.cuda.is_available():
+                torch.cuda.init()
+        except Exception:
+            pass
+    yield
+
+
 def golden(name):
     return np.load(os.path.join(GOLDEN, name + ".npz"))
 

@@ -1,0 +1,180 @@
+"""The sharded particle filter's device-resident step (slam_dist_*, BASELINE
+config 3) against one handle holding all particles: bit-identical weights,
+particles, resample decisions, argmax, estimate and np.sum, step by step.
+
+  * LOCAL: every shard in this process on one GPU (the multi-GPU step's
+    kernels, exchanges and signalling, phase by phase on one stream);
+  * one rank per process: a 1-rank RCCL communicator (slam_comm_*) bootstraps
+    the exchange; two processes sharing the GPU exchange through IPC-opened
+    peer regions (the path of one process per GPU).
+"""
+import multiprocessing as mp
+import os
+import sys
+
+import numpy as np
+import pytest
+
+import pf_oracle as po
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def _world(n_global, nl, steps, seed):
+    rs = np.random.RandomState(seed)
+    lm = rs.uniform(-10, 10, (nl, 2))
+    p = po.PFParams(n_particles=n_global, landmarks=lm, motion="velocity")
+    wd = po.PFWorld(p)
+    np.random.seed(seed + 1)
+    zs = []
+    for _ in range(steps):
+        wd.advance()
+        zs.append(wd.observe())
+    return lm, np.array(zs), p
+
+
+def _same(a, b, k):
+    assert a["resampled"] == b["resampled"], k
+    assert a["max_idx"] == b["max_idx"], (k, a["max_idx"], b["max_idx"])
+    np.testing.assert_array_equal(a["x_est"], b["x_est"])
+    assert a["max_val"] == b["max_val"] and a["weight_sum"] == b["weight_sum"], k
+    np.testing.assert_allclose(a["cov"], b["cov"], rtol=1e-7, atol=1e-13)
+    assert abs(a["ess"] - b["ess"]) <= 1e-9 * a["ess"]
+    assert a["resample_next"] == b["resample_next"], k
+
+
+@pytest.mark.parametrize("world,n_global,nl,lik", [(3, 3 * 65536, 20, "logsum"),
+                                                  (2, 2 * 8192 + 1000, 5, "product"),
+                                                  (8, 8 << 20, 100, "logsum")])
+def test_dist_local_steps_match_single(world, n_global, nl, lik):
+    from slamhip.dist import DistFilter
+    from slamhip.pf import DeviceParticleFilter
+    steps = 24
+    lm, zs, p = _world(n_global, nl, steps, 40 + world)
+    single = DeviceParticleFilter(n_global, lm, motion="velocity", likelihood=lik, seed=21)
+    dist = DistFilter(n_global, lm, world=world, motion="velocity", likelihood=lik, seed=21)
+    n_res = 0
+    try:
+        for k in range(steps):
+            a = single.step((p.vel, p.omega), zs[k])
+            b = dist.step((p.vel, p.omega), zs[k])
+            _same(a, b, k)
+            n_res += a["resampled"]
+        for u, v in zip(single.get_state(), dist.get_state()):
+            np.testing.assert_array_equal(u, v)
+        assert n_res >= 2
+    finally:
+        dist.close()
+        single.close()
+
+
+def test_dist_local_graph_run_matches_single():
+    """The bench path: observations loaded once, steps replayed as hipGraphs."""
+    from slamhip.dist import DistFilter
+    from slamhip.pf import DeviceParticleFilter
+    world, n_global, nl, steps = 4, 4 << 18, 100, 20
+    lm, zs, p = _world(n_global, nl, steps, 7)
+    ctl = np.tile([p.vel, p.omega], (steps, 1))
+    single = DeviceParticleFilter(n_global, lm, motion="velocity", likelihood="logsum", seed=3)
+    dist = DistFilter(n_global, lm, world=world, motion="velocity", likelihood="logsum", seed=3)
+    try:
+        single.load_observations(zs)
+        dist.load_observations(zs)
+        ra = single.run(0, ctl[:4]) + single.run(4, ctl[4:])
+        rb = dist.run(0, ctl[:4]) + dist.run(4, ctl[4:])
+        for k, (a, b) in enumerate(zip(ra, rb)):
+            _same(a, b, k)
+        assert sum(r["resampled"] for r in ra) >= 2
+        for u, v in zip(single.get_state(), dist.get_state()):
+            np.testing.assert_array_equal(u, v)
+    finally:
+        dist.close()
+        single.close()
+
+
+def test_comm_one_rank_rccl():
+    """slam_comm over RCCL with one rank: the bootstrap all-gather, and a
+    one-rank DistFilter connected through it."""
+    from slamhip.dist import Comm, DistFilter
+    from slamhip.pf import DeviceParticleFilter
+    comm = Comm(Comm.unique_id(), 1, 0, 0)
+    try:
+        assert comm.all_gather_bytes(b"slam-hip") == [b"slam-hip"]
+        n, nl, steps = 3 * 8192, 20, 12
+        lm, zs, p = _world(n, nl, steps, 11)
+        single = DeviceParticleFilter(n, lm, motion="velocity", likelihood="logsum", seed=5)
+        dist = DistFilter(n, lm, world=1, rank=0, comm=comm, motion="velocity", likelihood="logsum",
+                          seed=5)
+        try:
+            for k in range(steps):
+                _same(single.step((p.vel, p.omega), zs[k]), dist.step((p.vel, p.omega), zs[k]), k)
+        finally:
+            dist.close()
+            single.close()
+    finally:
+        comm.close()
+
+
+def _rank_main(rank, world, n, lm, zs, ctl, q_out, q_in, conn):
+    sys.path.insert(0, os.path.join(os.path.dirname(HERE), "slam-robot_simu_amd"))
+    from slamhip.dist import DistFilter
+
+    def all_gather(mine):
+        conn.send((rank, mine))
+        return conn.recv()
+
+    try:
+        d = DistFilter(n, lm, world=world, rank=rank, all_gather=all_gather, motion="velocity",
+                       likelihood="logsum", seed=8)
+        d.load_observations(zs)
+        res = d.run(0, ctl)
+        st = d.get_state()
+        d.close()
+        q_out.put((rank, [(r["max_idx"], r["weight_sum"], r["resampled"]) for r in res], st))
+    except Exception as e:              # reported to the parent
+        q_out.put((rank, repr(e), None))
+
+
+def test_dist_two_processes_share_one_gpu():
+    """Two ranks, two processes, one GPU: the IPC path of one process per GPU
+    (exchange regions exported / opened, device-side signalling across
+    processes), replayed as hipGraphs; compared with one handle."""
+    from slamhip.pf import DeviceParticleFilter
+    world, n, nl, steps = 2, 2 * 65536, 50, 16
+    lm, zs, p = _world(n, nl, steps, 23)
+    ctl = np.tile([p.vel, p.omega], (steps, 1))
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    pipes = [ctx.Pipe() for _ in range(world)]
+    procs = [ctx.Process(target=_rank_main, args=(r, world, n, lm, zs, ctl, q, None, pipes[r][1]))
+             for r in range(world)]
+    for pr in procs:
+        pr.start()
+    try:
+        blobs = [None] * world
+        for r in range(world):
+            rr, b = pipes[r][0].recv()
+            blobs[rr] = b
+        for r in range(world):
+            pipes[r][0].send(blobs)
+        out = {}
+        for _ in range(world):
+            rank, res, st = q.get(timeout=240)
+            assert st is not None, res
+            out[rank] = (res, st)
+    finally:
+        for pr in procs:
+            pr.join(timeout=60)
+            if pr.is_alive():
+                pr.kill()
+    with DeviceParticleFilter(n, lm, motion="velocity", likelihood="logsum", seed=8) as single:
+        single.load_observations(zs)
+        ref = single.run(0, ctl)
+        xs = single.get_state()
+    for rank in range(world):
+        res, _ = out[rank]
+        assert [(r["max_idx"], r["weight_sum"], r["resampled"]) for r in ref] == res
+    for k in range(4):
+        np.testing.assert_array_equal(np.concatenate([out[0][1][k], out[1][1][k]]), xs[k])
