@@ -11,14 +11,15 @@ for every step are simulated on the host and uploaded BEFORE the timed region
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
 
-N > 1 is launched by torch.distributed.run (one process per GPU).  Each rank
-runs its own 1,048,576-particle filter (weak scaling).  --mode sharded makes the
-ranks one filter over N x 2^20 particles (slamhip.shard.ShardedFilter: RCCL
-all-gathers of weight partials / reduction records, all-to-all-v of resampled
-particles; host-driven phases, no step graph); --mode replicas (the default:
-the sharded path is validated on one GPU only -- in-process shards and a
-1-rank RCCL group) runs independent Monte-Carlo realisations with no
-data-path collective.
+N > 1 is launched by torch.distributed.run (one process per GPU) and runs
+--mode sharded by default: the ranks are ONE filter over N x 2^20 particles
+(BASELINE configs[2], weak scaling: 2^20 per GPU) through slamhip.dist --
+the device-resident step whose exchanges (exact-cumsum specials, resampled
+particles, per-rank reduction records) are pushes into peer memory over xGMI
+with device-side signalling, bootstrapped over an RCCL communicator; 8 steps
+per hipGraph, no host decision per step.  --mode replicas runs independent
+Monte-Carlo realisations (no data-path exchange; the N = 1 default).  At N = 1
+the line also carries "sharded1": the sharded step's kernels on one shard.
 """
 from __future__ import annotations
 
@@ -407,21 +408,31 @@ def main():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--likelihood", default="logsum", choices=["product", "logsum"])
-    ap.add_argument("--mode", default="replicas", choices=["replicas", "sharded"])
+    ap.add_argument("--mode", default=None, choices=["replicas", "sharded"],
+                    help="sharded (default for N > 1): one filter over N x 2^20 particles "
+                         "(BASELINE configs[2]); replicas (default for N = 1): independent filters")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-secondary", action="store_true",
                     help="skip the EKF / EKF-SLAM / graph-SLAM rows (rank 0, N = 1 only)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.mode is None:
+        args.mode = "sharded" if world > 1 else "replicas"
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    # SLAM_BENCH_SHARE_GPU=1 (tests on a one-GPU box): every rank on device 0,
+    # gloo for the harness, the exchange regions bootstrapped through gloo
+    # (RCCL refuses two ranks on one GPU)
+    share_gpu = os.environ.get("SLAM_BENCH_SHARE_GPU") == "1"
+    if share_gpu:
+        local_rank = 0
     dist = None
     if world > 1 or ("MASTER_ADDR" in os.environ and "RANK" in os.environ):   # torch.distributed.run
         import torch
         import torch.distributed as dist
         torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl" if torch.cuda.is_available() else "gloo")
+        dist.init_process_group("nccl" if torch.cuda.is_available() and not share_gpu else "gloo")
 
     from slamhip.pf import DeviceParticleFilter
     total_steps = args.warmup + 2 * args.steps
@@ -436,37 +447,44 @@ def main():
 
     def measure_sharded(likelihood):
         # one filter over world x 2^20 particles (BASELINE configs[2]): this
-        # rank's shard through slamhip.shard.ShardedFilter; the exchange is
-        # torch.distributed (RCCL over xGMI) at world > 1, in-process at 1.
-        # Direct launches per phase (the host drives the exchange each step).
-        from slamhip.shard import DeviceShard, LocalComm, ShardedFilter, TorchComm
+        # rank's shard through slamhip.dist.DistFilter -- the device-resident
+        # step (peer-memory exchanges over xGMI inside the step's kernels, no
+        # host decision, 8 steps per hipGraph); the exchange regions are
+        # bootstrapped over an RCCL communicator created by the library (the
+        # 128-byte RCCL id travels through torch.distributed once).  At
+        # world = 1 the single shard runs the same kernels in-process.
+        from slamhip.dist import Comm, DistFilter
         n_global = world * NP_PER_GPU
-        shard = DeviceShard(NP_PER_GPU, n_global, rank * NP_PER_GPU, lm, dt=dt, motion="velocity",
-                            likelihood=likelihood, seed=1234, device=local_rank)
-        comm = TorchComm() if dist is not None else LocalComm(1)
-        filt = ShardedFilter([shard], [rank], comm, n_global)
-        nan = float("nan")
-
-        def run(k0, k1):
-            return [filt.step(ctl[k], zs[k], None, nan) for k in range(k0, k1)]
-
-        run(0, args.warmup)
+        comm = None
+        kw = dict(dt=dt, motion="velocity", likelihood=likelihood, seed=1234, device=local_rank)
+        if dist is not None and world > 1 and share_gpu:
+            def all_gather(b):
+                out = [None] * world
+                dist.all_gather_object(out, b)
+                return out
+            filt = DistFilter(n_global, lm, world=world, rank=rank, all_gather=all_gather, **kw)
+        elif dist is not None and world > 1:
+            obj = [Comm.unique_id() if rank == 0 else None]
+            dist.broadcast_object_list(obj, src=0)
+            comm = Comm(obj[0], world, rank, local_rank)
+            filt = DistFilter(n_global, lm, world=world, rank=rank, comm=comm, **kw)
+        else:
+            filt = DistFilter(n_global, lm, world=1, **kw)
+        filt.load_observations(zs)
+        if args.warmup:
+            filt.run(0, ctl[:args.warmup], want_results=False)
         barrier_sync()
         t0 = time.perf_counter()
-        out = run(args.warmup, args.warmup + args.steps)
+        out = filt.run(args.warmup, ctl[args.warmup:args.warmup + args.steps])
         barrier_sync()
         elapsed = time.perf_counter() - t0
-        lib = shard.lib
-        import ctypes as C
-        lib.slam_pf_enable_timing(shard._h, 1)
-        run(args.warmup + args.steps, total_steps)
-        timing = {}
-        for k in range(4):
-            ms, cnt = C.c_double(0.0), C.c_int64(0)
-            lib.slam_pf_timing(shard._h, k, C.byref(ms), C.byref(cnt))
-            timing[k] = (ms.value, cnt.value)
-        lib.slam_pf_enable_timing(shard._h, 0)
+        filt.enable_timing(True)
+        filt.run(args.warmup + args.steps, ctl[args.warmup + args.steps:])
+        timing = {k: filt.timing(k) for k in range(4)}
+        filt.enable_timing(False)
         filt.close()
+        if comm is not None:
+            comm.close()
         return elapsed, out, timing
 
     def measure(likelihood):
@@ -500,7 +518,8 @@ def main():
 
     if dist is not None:
         import torch
-        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local_rank}")
+        t = torch.tensor([elapsed], dtype=torch.float64,
+                         device="cpu" if share_gpu else f"cuda:{local_rank}")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
@@ -523,8 +542,11 @@ def main():
         "dtype": "f64",
         "data": "synthetic (simulated circular trajectory, 100 landmarks ~ U(-10,10)^2, "
                 "on-device Philox noise)",
-        "config": {"workload": "PF C2: 1,048,576 particles/GPU x 100 landmarks, velocity "
-                               "motion model, systematic resample",
+        "config": {"workload": ("PF C2: 1,048,576 particles/GPU x 100 landmarks, velocity "
+                                "motion model, systematic resample") if args.mode == "replicas" else
+                               (f"PF C3 form: one filter of {world} x 1,048,576 particles sharded "
+                                "1M/GPU x 100 landmarks, velocity motion model, exact systematic "
+                                "resample across shards; global np.sum-order normalisation"),
                    "particles_per_gpu": NP_PER_GPU, "landmarks": NL,
                    "likelihood": args.likelihood, "parallelism": f"{args.mode}{world}"},
         "roofline": {"bound": "valu_fp64", "kernel": "pf_fused_kernel (predict+likelihood)",
@@ -546,6 +568,12 @@ def main():
         e2, _, t2 = measure("product")
         line["alt_modes"] = {"product": {"value": NP_PER_GPU * NL * args.steps / e2,
                                          "fused_avg_ms": t2[0][0] / max(t2[0][1], 1)}}
+    if world == 1 and args.mode == "replicas":
+        # the sharded step's kernels on one shard (its overhead over the single handle)
+        e3, _, t3 = measure_sharded(args.likelihood)
+        line["sharded1"] = {"ms_per_step": e3 * 1e3 / args.steps,
+                            "over_single": e3 / elapsed,
+                            "fused_avg_ms": t3[0][0] / max(t3[0][1], 1)}
     if rank == 0 and world == 1 and not args.no_secondary:
         line["secondary"] = secondary(local_rank, cpu=not args.no_cpu_baseline)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -390,7 +390,7 @@ int slam_dist_run(slam_dist* d, int32_t first_step, int32_t n_steps, const doubl
         const int rc = set_ctr(h, first_step);
         if (rc) return rc;
     }
-    const bool graphs = d->sh[0]->use_graph;
+    const bool graphs = d->sh[0]->use_graph && !d->sh[0]->timing;
     hipStream_t s = d->sh[0]->stream;          // LOCAL: the shared stream; else the shard's
     auto capture = [&](hipGraphExec_t& ge, int steps) -> int {
         std::vector<int> cur0;

@@ -150,6 +150,18 @@ class DistFilter:
         self.resample_next = bool(res[k - 1].resample_next)
         return [DeviceParticleFilter._res(r) for r in res] if want_results else None
 
+    def enable_timing(self, on=True):
+        """HIP events around the fused kernel of every held shard (disables graphs)."""
+        for h, _, _ in self._shards:
+            check(self._lib.slam_pf_enable_timing(h, int(bool(on))), "slam_pf_enable_timing")
+
+    def timing(self, kernel=0):
+        """(total ms, launches) of the first held shard (slam_pf_timing kernel ids)."""
+        ms, cnt = C.c_double(0.0), C.c_int64(0)
+        check(self._lib.slam_pf_timing(self._shards[0][0], int(kernel), C.byref(ms), C.byref(cnt)),
+              "slam_pf_timing")
+        return ms.value, cnt.value
+
     def get_state(self):
         """Concatenated state of the held shards (x, y, th, w)."""
         parts = []

@@ -59,3 +59,22 @@ def test_bench_sharded_mode(launcher):
     assert d["config"]["parallelism"] == "sharded1"
     assert d["n_gpus"] == 1 and d["steps"] == 6 and d["value"] > 1e9
     assert d["resample_steps"] >= 0 and d["roofline"]["avg_launch_ms"] > 0
+
+
+def test_bench_sharded_two_ranks_share_one_gpu():
+    """bench.py's N > 1 path (the default --mode sharded) with two ranks on the
+    one GPU of the test box: IPC-opened exchange regions across processes, the
+    timed hipGraph replays, max-over-ranks timing, one JSON line from rank 0."""
+    args = [os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "8", "--warmup", "2",
+            "--no-secondary", "--no-cpu-baseline"]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", "29541"] + args
+    env = dict(os.environ, SLAM_BENCH_SHARE_GPU="1")
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["config"]["parallelism"] == "sharded2"
+    assert d["value"] > 1e10 and d["resample_steps"] >= 1
+    assert abs(d["value"] - 2 * 2 ** 20 * 100 / (d["ms_per_step"] / 1e3)) <= 1e-6 * d["value"]
