@@ -181,8 +181,7 @@ def cpu_baseline_vectorised(n_per_proc=1 << 15, steps=6):
                       f"process {busy:.1f} s (pool wall {wall:.1f} s incl. start-up)"}
 
 
-PF_SOURCES = ("pf_kernels.inl", "pf_kernels.hpp", "pf_finalize.inl", "fastmath.hpp", "common.hpp",
-              "pf_api.hip")
+PF_SOURCES = ("pf_kernels.inl", "pf_kernels.hpp", "fastmath.hpp", "common.hpp")
 
 
 def pf_sources_sha():

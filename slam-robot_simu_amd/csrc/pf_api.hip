@@ -5,6 +5,7 @@
 // resident in HBM.
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <limits>
 #include <vector>
@@ -87,6 +88,9 @@ struct slam_pf {
     int32_t cap = 0;                // steps the StepIO arrays hold
     double* ctl = nullptr;
     double* z_all = nullptr;
+    double* zc = nullptr;                 // [cap][kClosedWords] closed-form log-sum sums
+    std::vector<double> lm_host;          // landmarks (closed-form sums)
+    std::vector<double> z_host;           // the loaded batch's observations (closed-form sums)
     double* ofs = nullptr;
     slam_pf_result* res_dev = nullptr;
     slam_pf_result* res_host = nullptr;   // pinned
@@ -148,7 +152,9 @@ int make_lik_const(slam_pf* h) {
     lc.rsxsy = 1.0 / lc.sxsy;
     lc.rd2 = 1.0 / lc.d2;
     lc.iso = (lc.sx2 == lc.sy2 && !lc.has_rho) ? 1 : 0;
-    lc.pad = 0;
+    // closed-form log-sum (iso, NL > 0); SLAM_PF_CLOSED=0 keeps the landmark loop (diagnostic)
+    const char* ce = std::getenv("SLAM_PF_CLOSED");
+    lc.closed = (lc.iso && h->nl > 0 && !(ce && ce[0] == '0')) ? 1 : 0;
     // Log-sum fast-path bound.  A factor is at most 1/den (q >= 0), so the log of
     // the reference's partial product after landmark k is at least
     // L - (NL - k) max(0, -ln den).  L >= ln(DBL_MIN) + NL max(0, -ln den) + 1
@@ -180,6 +186,7 @@ StepIO step_io(slam_pf* h) {
     StepIO io;
     io.ctl = h->ctl;
     io.z = h->z_all;
+    io.zc = h->zc;
     io.ofs = h->ofs;
     io.res = h->res_dev;
     io.ctr = h->ctr;
@@ -228,6 +235,7 @@ int ensure_steps(slam_pf* h, int32_t steps) {
     drop_graphs(h);
     release(h, h->ctl);
     release(h, h->z_all);
+    release(h, h->zc);
     release(h, h->ofs);
     release(h, h->res_dev);
     if (h->res_host) (void)hipHostFree(h->res_host);
@@ -235,6 +243,7 @@ int ensure_steps(slam_pf* h, int32_t steps) {
     int rc;
     const size_t nlz = 2 * (size_t)std::max<int32_t>(h->nl, 1);
     if ((rc = dalloc(h, &h->ctl, 2 * (size_t)steps)) || (rc = dalloc(h, &h->z_all, nlz * steps)) ||
+        (rc = dalloc(h, &h->zc, (size_t)kClosedWords * steps)) ||
         (rc = dalloc(h, &h->ofs, (size_t)steps)) || (rc = dalloc(h, &h->res_dev, (size_t)steps)))
         return rc;
     SLAM_HIP_TRY(hipHostMalloc((void**)&h->res_host, sizeof(slam_pf_result) * steps));
@@ -563,8 +572,10 @@ int create_impl(const slam_pf_config* cfg, int64_t n_local, int64_t n_global, in
     SLAM_HIP_TRY(hipMemset(h->flags, 0, kFlagWords * sizeof(int32_t)));
     SLAM_HIP_TRY(hipMemset(h->tk, 0, 4 * kTicketWords * sizeof(unsigned)));
     SLAM_HIP_TRY(hipMemset(h->ctr, 0, 4 * sizeof(int32_t)));
-    if (n_landmarks > 0)
+    if (n_landmarks > 0) {
         SLAM_HIP_TRY(hipMemcpy(h->lm, landmarks, 2 * n_landmarks * sizeof(double), hipMemcpyHostToDevice));
+        h->lm_host.assign(landmarks, landmarks + 2 * (size_t)n_landmarks);
+    }
     *out = h;
     return SLAM_OK;
 }
@@ -586,12 +597,68 @@ int set_s_one(slam_pf* h) {
     return SLAM_OK;
 }
 
+// Closed-form log-sum sums of one step (likelihood_lanes, iso): S_ll = sum |l|^2,
+// S_l = sum l, S_zz = sum |z|^2, S_z = sum z, D = sum z.l, E = sum (z_y l_x - z_x l_y),
+// each a double-double (hi, lo) -- exact products, compensated sums.
+struct HostDD {
+    double h = 0.0, l = 0.0;
+    void add(const double bh, const double bl = 0.0) {
+        const double t = h + bh;
+        const double bb = t - h;
+        const double e = ((h - (t - bb)) + (bh - bb)) + (l + bl);
+        h = t + e;
+        l = e - (h - t);
+    }
+    void add_prod(const double a, const double b) {
+        const double p = a * b;
+        add(p, std::fma(a, b, -p));
+    }
+};
+
+void closed_sums(const double* lm, const double* z, const int32_t nl, double* out) {
+    HostDD Sll, Slx, Sly, Szz, Szx, Szy, D, E;
+    for (int32_t j = 0; j < nl; ++j) {
+        const double lx = lm[2 * j], ly = lm[2 * j + 1], zx = z[2 * j], zy = z[2 * j + 1];
+        Sll.add_prod(lx, lx);
+        Sll.add_prod(ly, ly);
+        Slx.add(lx);
+        Sly.add(ly);
+        Szz.add_prod(zx, zx);
+        Szz.add_prod(zy, zy);
+        Szx.add(zx);
+        Szy.add(zy);
+        D.add_prod(zx, lx);
+        D.add_prod(zy, ly);
+        E.add_prod(zy, lx);
+        E.add_prod(-zx, ly);
+    }
+    const HostDD* v[8] = {&Sll, &Slx, &Sly, &Szz, &Szx, &Szy, &D, &E};
+    for (int k = 0; k < 8; ++k) {
+        out[2 * k] = v[k]->h;
+        out[2 * k + 1] = v[k]->l;
+    }
+}
+
+// the closed-form sums of steps [0, n_steps) of z_host (or of one staged z) into zc
+int upload_closed(slam_pf* h, const double* z, const int32_t n_steps) {
+    if (!h->nl || !h->lc.iso) return SLAM_OK;
+    std::vector<double> zc((size_t)kClosedWords * n_steps);
+    for (int32_t t = 0; t < n_steps; ++t)
+        closed_sums(h->lm_host.data(), z + (size_t)t * 2 * h->nl, h->nl, zc.data() + (size_t)t * kClosedWords);
+    SLAM_HIP_TRY(hipMemcpyAsync(h->zc, zc.data(), zc.size() * sizeof(double), hipMemcpyHostToDevice,
+                                h->stream));
+    return SLAM_OK;
+}
+
 // stage one sync-mode step's inputs into StepIO slot 0
 int stage_inputs(slam_pf* h, const double* control, const double* z, const double* noise,
                  double u) {
-    if (h->nl && z)
+    if (h->nl && z) {
         SLAM_HIP_TRY(hipMemcpyAsync(h->z_all, z, 2 * h->nl * sizeof(double), hipMemcpyHostToDevice,
                                     h->stream));
+        const int rc = upload_closed(h, z, 1);
+        if (rc) return rc;
+    }
     SLAM_HIP_TRY(hipMemcpyAsync(h->ctl, control, 2 * sizeof(double), hipMemcpyHostToDevice, h->stream));
     h->sh.ofs_host = std::isnan(u) ? u : u * h->pc.np_recip;           // particle_filter.py:214
     SLAM_HIP_TRY(hipMemcpyAsync(h->ofs, &h->sh.ofs_host, sizeof(double), hipMemcpyHostToDevice, h->stream));
@@ -675,9 +742,16 @@ int slam_pf_set_stream(slam_pf* h, void* stream, int32_t external) {
 int slam_pf_set_landmarks(slam_pf* h, const double* landmarks) {
     SLAM_ARG_CHECK(h && (landmarks || h->nl == 0), "slam_pf_set_landmarks: NULL argument");
     SLAM_HIP_TRY(hipSetDevice(h->device));
-    if (h->nl)
+    if (h->nl) {
         SLAM_HIP_TRY(hipMemcpyAsync(h->lm, landmarks, 2 * h->nl * sizeof(double),
                                     hipMemcpyHostToDevice, h->stream));
+        h->lm_host.assign(landmarks, landmarks + 2 * (size_t)h->nl);
+        // the loaded batch's closed-form sums depend on the landmarks
+        if (h->z_steps > 0) {
+            const int rc = upload_closed(h, h->z_host.data(), h->z_steps);
+            if (rc) return rc;
+        }
+    }
     SLAM_HIP_TRY(hipStreamSynchronize(h->stream));
     return SLAM_OK;
 }
@@ -868,9 +942,12 @@ int slam_pf_load_observations(slam_pf* h, int32_t n_steps, const double* z_all) 
     SLAM_HIP_TRY(hipSetDevice(h->device));
     int rc = ensure_steps(h, n_steps);
     if (rc) return rc;
-    if (h->nl)
+    if (h->nl) {
         SLAM_HIP_TRY(hipMemcpyAsync(h->z_all, z_all, (size_t)n_steps * 2 * h->nl * sizeof(double),
                                     hipMemcpyHostToDevice, h->stream));
+        if (h->lc.iso) h->z_host.assign(z_all, z_all + (size_t)n_steps * 2 * h->nl);
+        if ((rc = upload_closed(h, z_all, n_steps))) return rc;
+    }
     std::vector<double> nan((size_t)n_steps, std::nan(""));
     SLAM_HIP_TRY(hipMemcpyAsync(h->ofs, nan.data(), n_steps * sizeof(double), hipMemcpyHostToDevice,
                                 h->stream));

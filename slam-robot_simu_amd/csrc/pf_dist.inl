@@ -86,7 +86,7 @@ struct DistScratch {
     double base_off;            // approximate cumsum before local element 0
     double c_left;              // exact cumsum just before local element 0 (-inf on rank 0)
     int64_t lo0;                // positions <= c_left
-    int64_t pad;
+    int64_t covered;            // positions covered by the received items (unpack; reset by its last block)
     int64_t dbase[kDistMaxWorld];   // per destination: selected sources before its range
     int64_t dcnt[kDistMaxWorld];    // per destination: items sent
 };
@@ -393,140 +393,237 @@ __global__ __launch_bounds__(kScanThreads) void dist_pack_push_kernel(
     dist_signal(P, kXItem, dist_epoch(io));
 }
 
-// wait for every rank's items; every local position takes the item whose range
-// covers it (items of rank q cover a contiguous stretch of positions, ranks in
-// order); the last block marks the resample done (flag 2: w = 1/NP)
+// wait for every rank's items and hand them to the fused kernel's resample
+// gather (the single-GPU expand pass's inverse map): item k (ranks in order,
+// each rank's items in position order) is stored at local index k of the
+// particle arrays -- the pre-resample particles were packed already -- with a
+// run mark (mark generation | k) at its first local position and the carry of
+// every fused block whose first position it covers.  Items never outnumber the
+// positions (disjoint, non-empty ranges), so k < n.  The last block checks that
+// the ranges tile the shard (status kDistStItems otherwise).  The resample flag
+// stays 1: the fused kernel gathers through the marks, at weight 1/NP.
 __global__ __launch_bounds__(256) void dist_unpack_kernel(
     const int64_t n, double* __restrict__ xs, double* __restrict__ ys, double* __restrict__ ts,
-    unsigned* __restrict__ counter, int32_t* __restrict__ flags, const DistPeers P, StepIO io) {
+    int64_t* __restrict__ mark, int32_t* __restrict__ carry, unsigned* __restrict__ counter,
+    int32_t* __restrict__ flags, DistScratch* __restrict__ scr, const DistPeers P, StepIO io) {
     if (!dist_resampling(flags) || flags[kFlagFallback]) return;
     dist_wait(P, kXItem, dist_epoch(io), flags);
-    __shared__ int64_t s_cnt[kDistMaxWorld], s_first[kDistMaxWorld];
+    __shared__ int64_t s_off[kDistMaxWorld + 1];
+    __shared__ unsigned long long s_cov;
     const char* mine = P.base[P.rank];
     const ShardItem* items = reinterpret_cast<const ShardItem*>(mine + P.L.item);
-    if ((int)threadIdx.x < P.world) {
-        const int q = threadIdx.x;
-        const int64_t cq = (int64_t)ld_sys(reinterpret_cast<const int64_t*>(mine + P.L.item_hdr) + 2 * q);
-        s_cnt[q] = cq;
-        s_first[q] = cq > 0 ? (int64_t)ld_sys(&items[(int64_t)q * P.L.cap_item].lo) : INT64_MAX;
+    if (threadIdx.x == 0) {
+        int64_t o = 0;
+        for (int q = 0; q < P.world; ++q) {
+            s_off[q] = o;
+            o += (int64_t)ld_sys(reinterpret_cast<const int64_t*>(mine + P.L.item_hdr) + 2 * q);
+        }
+        s_off[P.world] = o;
+        s_cov = 0;
     }
     __syncthreads();
-    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (p < n) {
-        const int64_t g = P.gb[P.rank] + p;
-        int q = -1;
-        for (int r = 0; r < P.world; ++r)
-            if (s_cnt[r] > 0 && s_first[r] <= g) q = r;
-        bool ok = q >= 0;
-        if (ok) {
-            const ShardItem* L = items + (int64_t)q * P.L.cap_item;
-            int64_t a = 0, b = s_cnt[q];                    // first item with hi > g
-            while (a < b) {
-                const int64_t m = (a + b) >> 1;
-                if ((int64_t)ld_sys(&L[m].hi) > g) b = m;
-                else a = m + 1;
-            }
-            ok = a < s_cnt[q] && (int64_t)ld_sys(&L[a].lo) <= g;
-            if (ok) {
-                xs[p] = ld_sys_d(&L[a].x);
-                ys[p] = ld_sys_d(&L[a].y);
-                ts[p] = ld_sys_d(&L[a].th);
-            }
+    const int64_t ntot = s_off[P.world] < n ? s_off[P.world] : n;
+    const int64_t gb = P.gb[P.rank];
+    const int64_t gen = (int64_t)(uint32_t)flags[kFlagMarkGen] << 32;
+    uint64_t cov = 0;
+    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < ntot;
+         k += (int64_t)gridDim.x * blockDim.x) {
+        int q = 0;
+        while (q + 1 < P.world && s_off[q + 1] <= k) ++q;
+        const ShardItem* it = items + (int64_t)q * P.L.cap_item + (k - s_off[q]);
+        const int64_t lo = (int64_t)ld_sys(&it->lo) - gb, hi = (int64_t)ld_sys(&it->hi) - gb;
+        const double x = ld_sys_d(&it->x), y = ld_sys_d(&it->y), th = ld_sys_d(&it->th);
+        if (!(lo >= 0 && lo < hi && hi <= n)) {
+            atomicOr(&flags[kFlagStatus], kDistStItems);
+            continue;
         }
-        if (!ok) atomicOr(&flags[kFlagStatus], kDistStItems);
+        xs[k] = x;
+        ys[k] = y;
+        ts[k] = th;
+        mark[lo] = gen | k;
+        for (int64_t b = (lo + kPartPer - 1) / kPartPer; b * kPartPer < hi; ++b) carry[b] = (int32_t)k;
+        cov += (uint64_t)(hi - lo);
     }
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) cov += __shfl_xor(cov, d, 64);
+    if ((threadIdx.x & 63) == 0 && cov) atomicAdd(&s_cov, (unsigned long long)cov);
+    __syncthreads();
+    if (threadIdx.x == 0 && s_cov) atomicAdd((unsigned long long*)&scr->covered, s_cov);
     if (!arrive_last(counter)) return;
-    if (threadIdx.x == 0) flags[kFlagResample] = 2;        // gathered: the fused kernel uses w = 1/NP
+    if (threadIdx.x == 0) {
+        const unsigned long long c = atomicExch((unsigned long long*)&scr->covered, 0ull);
+        if ((int64_t)c != n || s_off[P.world] > n) atomicOr(&flags[kFlagStatus], kDistStItems);
+    }
 }
 
 // ---------------------------------------------------------------- record
 // The shard's reduction record from the fused kernel's block partials,
-// pushed into every peer's G1 slot (parity = epoch & 1), then kXG1.
-// One workgroup of kFinThreads lanes.
-__global__ __launch_bounds__(kFinThreads) void dist_record_push_kernel(
-    const int64_t n, const DeferParts dp, const double* __restrict__ w_un,
-    const int32_t* __restrict__ tail_leaves, const int32_t* __restrict__ tail_ops,
-    const int32_t n_tail_leaves, const int32_t n_tail_ops, const double* __restrict__ xs,
-    const double* __restrict__ ys, const double* __restrict__ ts, const DistPeers P, StepIO io) {
-    __shared__ double sh[2048];
-    __shared__ double s_q[11][kFinThreads];
+// pushed into every peer's G1 slot (parity = epoch & 1), then kXG1.  One
+// workgroup of kFinThreads lanes, laid out like finalize_deferred_kernel:
+// every lane issues the loads of its blocks and leaves first; the sums are
+// wave butterflies (a fixed order); the tie-window candidates are the first
+// kDistWin blocks whose max is within 2^-48 of M, found in parallel (the
+// window then reads only those blocks).
+__device__ __forceinline__ void dist_record(const int64_t n, const DeferParts& dp,
+                                            const double* __restrict__ w_un,
+                                            const int32_t* __restrict__ tail_leaves,
+                                            const int32_t* __restrict__ tail_ops,
+                                            const int32_t n_tail_leaves, const int32_t n_tail_ops,
+                                            const double* __restrict__ xs,
+                                            const double* __restrict__ ys,
+                                            const double* __restrict__ ts, const DistPeers& P,
+                                            const uint64_t epoch, double* sh) {
+    __shared__ double s_red[12][kFinWaves];
     __shared__ double s_wm[kFinWaves];
-    __shared__ unsigned long long s_min;
+    __shared__ unsigned long long s_cand[kDistWin], s_mblk;
     __shared__ DistRec rec;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int64_t nb = (n + kPartPer - 1) / kPartPer;
     const int64_t nfull = n / kSumChunk;
     const int64_t nch = (n + kSumChunk - 1) / kSumChunk;
     const int64_t gbase = P.gb[P.rank];
-    double* chunks = sh;                                    // reused below (nch <= 2048)
-    // ---- np.sum buffer partials: 64 leaves per 8192-element buffer, perfect tree
-    for (int64_t c = tid; c < nfull; c += kFinThreads) {
-        const double* Lp = dp.leaf + 64 * c;
-        double a[32];
+    if (tid < kDistWin) s_cand[tid] = ~0ull;
+    if (tid == 0) s_mblk = ~0ull;
+    // ---- loads up front: this lane's blocks tid + kFinThreads k and its leaves
+    double pm[kFinRegBlocks], q[kFinRegBlocks][11];
+    bool has[kFinRegBlocks];
 #pragma unroll
-        for (int j = 0; j < 32; ++j) a[j] = Lp[2 * j] + Lp[2 * j + 1];
+    for (int k = 0; k < kFinRegBlocks; ++k) {
+        const int64_t b = tid + (int64_t)kFinThreads * k;
+        has[k] = b < nb;
+        const int64_t bb = has[k] ? b : 0;
+        pm[k] = dp.pmax[bb];
 #pragma unroll
-        for (int j = 0; j < 16; ++j) a[j] = a[2 * j] + a[2 * j + 1];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) a[j] = a[2 * j] + a[2 * j + 1];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) a[j] = a[2 * j] + a[2 * j + 1];
-        chunks[c] = (a[0] + a[1]) + (a[2] + a[3]);
+        for (int j = 0; j < 11; ++j) q[k][j] = dp.ps[j][bb];
     }
-    __syncthreads();
-    if (nch > nfull) {
-        __shared__ double tl[1024];
-        const double t = tail_chunk_sum(w_un + nfull * kSumChunk, tail_leaves, tail_ops, n_tail_leaves,
-                                        n_tail_ops, tl);
-        if (tid == 0) chunks[nfull] = t;
-    }
-    // ---- block maxima: M, the first block holding it
-    double m = -1.0;
-    for (int64_t b = tid; b < nb; b += kFinThreads) m = fmax(m, dp.pmax[b]);
+    const int part = tid & (kFinLeafLanes - 1);
+    double L[16];
+    {
+        const int64_t c = tid / kFinLeafLanes;
+        const double* Lp = dp.leaf + 64 * (c < nfull ? c : 0) + 16 * part;
 #pragma unroll
-    for (int d = 1; d < 64; d <<= 1) m = fmax(m, __shfl_xor(m, d, 64));
-    if (lane == 0) s_wm[wave] = m;
-    if (tid == 0) s_min = ~0ull;
+        for (int j = 0; j < 16; ++j) L[j] = Lp[j];
+    }
+    const int64_t bx0 = tid + (int64_t)kFinThreads * kFinRegBlocks;   // NP > 2^20 only
+    double mlane = -1.0;
+#pragma unroll
+    for (int k = 0; k < kFinRegBlocks; ++k)
+        if (has[k]) mlane = fmax(mlane, pm[k]);
+    for (int64_t b = bx0; b < nb; b += kFinThreads) mlane = fmax(mlane, dp.pmax[b]);
+    // lane sums scaled by the lane's max; T = sum of w_un (unscaled)
+    double acc[12];
+#pragma unroll
+    for (int j = 0; j < 12; ++j) acc[j] = 0.0;
+    {
+        const double rm = mlane > 0.0 ? 1.0 / mlane : 0.0;
+        auto add = [&](const double p, const double* qq) {
+            if (mlane > 0.0) {
+                const double r = p * rm;
+                acc[0] += r * qq[0];
+                acc[1] += (r * r) * qq[1];
+#pragma unroll
+                for (int j = 2; j < 11; ++j) acc[j] += r * qq[j];
+            }
+            acc[11] += p * qq[0];
+        };
+#pragma unroll
+        for (int k = 0; k < kFinRegBlocks; ++k)
+            if (has[k]) add(pm[k], q[k]);
+        for (int64_t b = bx0; b < nb; b += kFinThreads) {
+            double qq[11];
+#pragma unroll
+            for (int j = 0; j < 11; ++j) qq[j] = dp.ps[j][b];
+            add(dp.pmax[b], qq);
+        }
+    }
+    double mx = mlane;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) mx = fmax(mx, __shfl_xor(mx, d, 64));
+    if (lane == 0) s_wm[wave] = mx;
+    // ---- np.sum buffer partials: 4 lanes per 8192-element buffer, pairwise tree
+    for (int64_t c0 = 0; c0 < nfull; c0 += kFinBufPerRound) {
+        const int64_t c = c0 + tid / kFinLeafLanes;
+        double v = 0.0;
+        if (c < nfull) {
+            if (c0 > 0) {
+                const double* Lp = dp.leaf + 64 * c + 16 * part;
+#pragma unroll
+                for (int j = 0; j < 16; ++j) L[j] = Lp[j];
+            }
+            v = tree16(L);
+        }
+#pragma unroll
+        for (int d = 1; d < kFinLeafLanes; d <<= 1) {
+            const double o = __shfl_xor(v, d, 64);
+            v = (part & d) ? (o + v) : (v + o);              // left operand = lower lane
+        }
+        if (part == 0 && c < nfull) sh[c] = v;
+    }
     __syncthreads();
     double M = s_wm[0];
 #pragma unroll
     for (int w = 1; w < kFinWaves; ++w) M = fmax(M, s_wm[w]);
-    const double thr = M * (1.0 - 0x1p-48);                // tie window (2^-48 relative)
-    // ---- scaled sums over the blocks (lane-strided, then a fixed tree)
-    double acc[11];
+    const double thr = M * (1.0 - 0x1p-48);                 // tie window (2^-48 relative)
+    {
+        const double rl = (mlane > 0.0 && M > 0.0) ? mlane / M : 0.0;
+        acc[0] *= rl;
+        acc[1] *= rl * rl;
 #pragma unroll
-    for (int j = 0; j < 11; ++j) acc[j] = 0.0;
-    double T = 0.0;
-    unsigned long long first = ~0ull;
-    for (int64_t b = tid; b < nb; b += kFinThreads) {
-        const double pm = dp.pmax[b];
-        if (M > 0.0) {
-            const double r = pm / M;
-            acc[0] += r * dp.ps[0][b];
-            acc[1] += (r * r) * dp.ps[1][b];
+        for (int j = 2; j < 11; ++j) acc[j] *= rl;
+    }
 #pragma unroll
-            for (int j = 2; j < 11; ++j) acc[j] += r * dp.ps[j][b];
+    for (int j = 0; j < 12; ++j) {
+        double r = acc[j];
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const double o = __shfl_xor(r, d, 64);
+            r = (lane & d) ? (o + r) : (r + o);
         }
-        T += pm * dp.ps[0][b];
-        if (pm >= thr && first == ~0ull) first = (unsigned long long)b;
+        if (lane == 0) s_red[j][wave] = r;
     }
-    if (first != ~0ull) atomicMin(&s_min, first);
+    // first block holding M, and the first kDistWin candidate blocks (index order)
+    if (M > 0.0) {
+        unsigned long long mb = ~0ull;
 #pragma unroll
-    for (int j = 0; j < 11; ++j) s_q[j][tid] = acc[j];
-    __syncthreads();
-    if (tid < 11) {
-        double r = 0.0;
-        for (int k = 0; k < kFinThreads; ++k) r = r + s_q[tid][k];
-        rec.q[tid] = r;
+        for (int k = kFinRegBlocks - 1; k >= 0; --k)
+            if (has[k] && pm[k] == M) mb = (unsigned long long)(tid + (int64_t)kFinThreads * k);
+        for (int64_t b = bx0; b < nb && mb == ~0ull; b += kFinThreads)
+            if (dp.pmax[b] == M) mb = (unsigned long long)b;
+        if (mb != ~0ull) atomicMin(&s_mblk, mb);
+    }
+    unsigned long long prev = 0;                            // candidates must be >= prev
+    for (int r = 0; r < kDistWin; ++r) {
+        unsigned long long cb = ~0ull;
+        if (M > 0.0) {
+#pragma unroll
+            for (int k = kFinRegBlocks - 1; k >= 0; --k) {
+                const unsigned long long b = (unsigned long long)(tid + (int64_t)kFinThreads * k);
+                if (has[k] && pm[k] >= thr && b >= prev) cb = b;
+            }
+            for (int64_t b = bx0; b < nb && cb == ~0ull; b += kFinThreads)
+                if ((unsigned long long)b >= prev && dp.pmax[b] >= thr) cb = (unsigned long long)b;
+        }
+        if (cb != ~0ull) atomicMin(&s_cand[r], cb);
+        __syncthreads();
+        const unsigned long long got = s_cand[r];
+        if (got == ~0ull) break;                            // block-uniform
+        prev = got + 1;
     }
     __syncthreads();
-    // T: the same fixed tree through s_q[0]
-    s_q[0][tid] = T;
-    __syncthreads();
+    if (tid < 12) {
+        double r = s_red[tid][0];
+#pragma unroll
+        for (int w = 1; w < kFinWaves; ++w) r = r + s_red[tid][w];
+        if (tid < 11) rec.q[tid] = r;
+        else rec.T = r;
+    }
+    if (nch > nfull) {
+        __shared__ double tl[1024];
+        const double t = tail_chunk_sum(w_un + nfull * kSumChunk, tail_leaves, tail_ops, n_tail_leaves,
+                                        n_tail_ops, tl);
+        if (tid == 0) sh[nfull] = t;
+    }
     if (tid == 0) {
-        double r = 0.0;
-        for (int k = 0; k < kFinThreads; ++k) r = r + s_q[0][k];
-        rec.T = r;
         rec.M = M;
         rec.nchunk = nch;
         rec.x0[0] = xs[0];
@@ -536,11 +633,13 @@ __global__ __launch_bounds__(kFinThreads) void dist_record_push_kernel(
     }
     __syncthreads();
     // ---- tie window: the first kDistWin elements (index order) with w_un >= thr,
-    // scanning the blocks from the first candidate on (usually one element: M)
+    // from the candidate blocks (usually one element: M)
     if (M > 0.0 && wave == 0) {
         int64_t cnt = 0;
-        for (int64_t b = (int64_t)s_min; b < nb && cnt < kDistWin; ++b) {
-            if (dp.pmax[b] < thr) continue;
+        for (int r = 0; r < kDistWin && cnt < kDistWin; ++r) {
+            const unsigned long long cb = s_cand[r];
+            if (cb == ~0ull) break;
+            const int64_t b = (int64_t)cb;
             for (int e0 = 0; e0 < kPartPer && cnt < kDistWin; e0 += 64) {
                 const int64_t i = b * kPartPer + e0 + lane;
                 const double v = (i < n) ? w_un[i] : -1.0;
@@ -572,23 +671,22 @@ __global__ __launch_bounds__(kFinThreads) void dist_record_push_kernel(
                 for (int j = 0; j < 3; ++j) rec.xc[j] = rec.win[k].x[j];
                 break;
             }
-        for (int64_t b = 0; rec.idx < 0 && b < nb; ++b)
-            if (dp.pmax[b] == M) {
-                rec.idx = gbase + dp.pidx[b];
-                for (int j = 0; j < 3; ++j) rec.xc[j] = dp.pxe[j][b];
-            }
+        if (rec.idx < 0 && s_mblk != ~0ull) {
+            const int64_t b = (int64_t)s_mblk;
+            rec.idx = gbase + dp.pidx[b];
+            for (int j = 0; j < 3; ++j) rec.xc[j] = dp.pxe[j][b];
+        }
     }
     __syncthreads();
     // ---- push into every peer's slot (parity = epoch & 1)
-    const uint64_t epoch = dist_epoch(io);
     const int64_t words = (int64_t)sizeof(DistRec) / 8;
-    for (int q = 0; q < P.world; ++q) {
-        char* slot = P.base[q] + P.L.g1 + ((int64_t)(epoch & 1) * P.world + P.rank) * P.L.rec_stride;
+    for (int qq = 0; qq < P.world; ++qq) {
+        char* slot = P.base[qq] + P.L.g1 + ((int64_t)(epoch & 1) * P.world + P.rank) * P.L.rec_stride;
         uint64_t* dst = reinterpret_cast<uint64_t*>(slot);
         const uint64_t* src = reinterpret_cast<const uint64_t*>(&rec);
         for (int64_t k = tid; k < words; k += kFinThreads) dst[k] = src[k];
         double* dch = reinterpret_cast<double*>(slot + sizeof(DistRec));
-        for (int64_t c = tid; c < nch; c += kFinThreads) dch[c] = chunks[c];
+        for (int64_t c = tid; c < nch; c += kFinThreads) dch[c] = sh[c];
     }
     __syncthreads();
     dist_signal(P, kXG1, epoch);
@@ -597,38 +695,73 @@ __global__ __launch_bounds__(kFinThreads) void dist_record_push_kernel(
 // ---------------------------------------------------------------- finalize
 // Wait for every rank's record and form the step's global result -- the same
 // on every rank: s = np.sum in the reference's order (buffer partials, ranks in
-// order), the exact max and first argmax of w = w_un / s, ESS and covariance
-// from the scaled sums, the result record, the next step's resample flag and,
-// when it resamples, this rank's exact-cumsum base offsets.
-__global__ __launch_bounds__(kFinThreads) void dist_finalize_kernel(
-    const int64_t n, const DeferParts dp, double* __restrict__ s_cur, double* __restrict__ refp,
-    int32_t* __restrict__ flags, const double ess_th, StepIO io, const double np_recip,
-    double* __restrict__ boff, DistScratch* __restrict__ scr, const DistPeers P) {
+// order: staged through LDS, then one left-to-right chain), the exact max and
+// first argmax of w = w_un / s, ESS and covariance from the scaled sums, the
+// result record, the next step's resample flag and, when it resamples, this
+// rank's exact-cumsum base offsets.
+__device__ __forceinline__ void dist_finalize(const int64_t n, const DeferParts& dp,
+                                              double* __restrict__ s_cur, double* __restrict__ refp,
+                                              int32_t* __restrict__ flags, const double ess_th,
+                                              const StepIO& io, const double np_recip,
+                                              double* __restrict__ boff,
+                                              DistScratch* __restrict__ scr, const DistPeers& P,
+                                              const uint64_t epoch, double* sh) {
+    constexpr int kStage = 2048;                            // LDS doubles per staged round
     __shared__ double s_rq[kDistMaxWorld][11];
     __shared__ double s_M[kDistMaxWorld], s_T[kDistMaxWorld];
+    __shared__ int64_t s_nc[kDistMaxWorld + 1];
     __shared__ double s_s;
     __shared__ int32_t s_do_off;
     const int tid = threadIdx.x;
-    const uint64_t epoch = dist_epoch(io);
+    __shared__ DistRec s_rec[kDistMaxWorld];
     dist_wait(P, kXG1, epoch, flags);
     const char* g1 = P.base[P.rank] + P.L.g1 + (int64_t)(epoch & 1) * P.world * P.L.rec_stride;
     auto rec_of = [&](int q) { return reinterpret_cast<const DistRec*>(g1 + (int64_t)q * P.L.rec_stride); };
-    if (tid < P.world) {
-        const DistRec* r = rec_of(tid);
-        s_M[tid] = ld_sys_d(&r->M);
-        s_T[tid] = ld_sys_d(&r->T);
-        for (int j = 0; j < 11; ++j) s_rq[tid][j] = ld_sys_d(&r->q[j]);
+    {   // every rank's record into LDS (one parallel round of system-scope loads)
+        constexpr int kW = (int)(sizeof(DistRec) / 8);
+        for (int e = tid; e < P.world * kW; e += kFinThreads) {
+            const int q = e / kW, k = e - q * kW;
+            reinterpret_cast<uint64_t*>(&s_rec[q])[k] = ld_sys(reinterpret_cast<const uint64_t*>(rec_of(q)) + k);
+        }
     }
     __syncthreads();
-    if (tid == 0) {
-        // np.sum (particle_filter.py:234): buffer partials left to right, ranks in order
-        double s = 0.0;
+    if (tid < P.world) {
+        const DistRec& r = s_rec[tid];
+        s_M[tid] = r.M;
+        s_T[tid] = r.T;
+        s_nc[tid] = r.nchunk;
+        for (int j = 0; j < 11; ++j) s_rq[tid][j] = r.q[j];
+    }
+    __syncthreads();
+    if (tid == 0) {                                         // s_nc -> exclusive prefix
+        int64_t o = 0;
         for (int q = 0; q < P.world; ++q) {
-            const DistRec* r = rec_of(q);
-            const int64_t nc = (int64_t)ld_sys(&r->nchunk);
-            const double* ch = reinterpret_cast<const double*>(reinterpret_cast<const char*>(r) + sizeof(DistRec));
-            for (int64_t c = 0; c < nc; ++c) s = s + ld_sys_d(&ch[c]);
+            const int64_t c = s_nc[q];
+            s_nc[q] = o;
+            o += c;
         }
+        s_nc[P.world] = o;
+    }
+    __syncthreads();
+    // np.sum (particle_filter.py:234): buffer partials left to right, ranks in order
+    const int64_t ntot = s_nc[P.world];
+    double s = 0.0;
+    for (int64_t g0 = 0; g0 < ntot; g0 += kStage) {
+        const int64_t cnt = ntot - g0 < kStage ? ntot - g0 : kStage;
+        for (int64_t e = tid; e < cnt; e += kFinThreads) {
+            const int64_t g = g0 + e;
+            int q = 0;
+            while (q + 1 < P.world && s_nc[q + 1] <= g) ++q;
+            const double* ch = reinterpret_cast<const double*>(reinterpret_cast<const char*>(rec_of(q)) +
+                                                               sizeof(DistRec));
+            sh[e] = ld_sys_d(&ch[g - s_nc[q]]);
+        }
+        __syncthreads();
+        if (tid == 0)
+            for (int64_t k = 0; k < cnt; ++k) s = s + sh[k];
+        __syncthreads();
+    }
+    if (tid == 0) {
         s_s = s;
         double M = -1.0;
         for (int q = 0; q < P.world; ++q) M = fmax(M, s_M[q]);
@@ -642,16 +775,16 @@ __global__ __launch_bounds__(kFinThreads) void dist_finalize_kernel(
             // first rank whose max rounds to the maximum, then its first element that does
             int win = 0;
             while (win < P.world && !(s_M[win] > 0.0 && s_M[win] / s == mval)) ++win;
-            const DistRec* r = rec_of(win);
-            const int nw = (int)ld_sys(&r->nwin);
+            const DistRec& r = s_rec[win];
+            const int nw = (int)r.nwin;
             int k = 0;
-            while (k < nw && !(ld_sys_d(&r->win[k].v) / s == mval)) ++k;
+            while (k < nw && !(r.win[k].v / s == mval)) ++k;
             if (k < nw) {
-                tot.maxi = (int64_t)ld_sys(&r->win[k].idx);
-                for (int j = 0; j < 3; ++j) xe[j] = ld_sys_d(&r->win[k].x[j]);
+                tot.maxi = r.win[k].idx;
+                for (int j = 0; j < 3; ++j) xe[j] = r.win[k].x[j];
             } else {                                        // window exhausted: M's own element
-                tot.maxi = (int64_t)ld_sys(&r->idx);
-                for (int j = 0; j < 3; ++j) xe[j] = ld_sys_d(&r->xc[j]);
+                tot.maxi = r.idx;
+                for (int j = 0; j < 3; ++j) xe[j] = r.xc[j];
                 st |= kDistStTie;
             }
             tot.maxv = mval;
@@ -672,10 +805,9 @@ __global__ __launch_bounds__(kFinThreads) void dist_finalize_kernel(
             for (int j = 0; j < 6; ++j) tot.m2[j] = a[5 + j] * f;
         } else {
             // every weight NaN -> 1/NP (particle_filter.py:236): argmax 0
-            const DistRec* r0 = rec_of(0);
             tot.maxv = np_recip;
             tot.maxi = 0;
-            for (int j = 0; j < 3; ++j) xe[j] = ld_sys_d(&r0->x0[j]);
+            for (int j = 0; j < 3; ++j) xe[j] = s_rec[0].x0[j];
             tot.sw = 1.0;
             tot.sw2 = np_recip;                             // ESS = NP
             for (int j = 0; j < 3; ++j) tot.m1[j] = NAN;
@@ -715,6 +847,29 @@ __global__ __launch_bounds__(kFinThreads) void dist_finalize_kernel(
                 ex = ex + btot(b0 + k);
             }
         if (tid == 0) boff[nb] = total;
+    }
+}
+
+// RECORD / FINALIZE: one workgroup.  A process holding one shard runs both in
+// one launch (push, then wait for the peers); a process holding several
+// (LOCAL mode, one stream) launches every shard's record before any finalize.
+template <bool RECORD, bool FINALIZE>
+__global__ __launch_bounds__(kFinThreads) void dist_reduce_kernel(
+    const int64_t n, const DeferParts dp, const double* __restrict__ w_un,
+    const int32_t* __restrict__ tail_leaves, const int32_t* __restrict__ tail_ops,
+    const int32_t n_tail_leaves, const int32_t n_tail_ops, const double* __restrict__ xs,
+    const double* __restrict__ ys, const double* __restrict__ ts, double* __restrict__ s_cur,
+    double* __restrict__ refp, int32_t* __restrict__ flags, const double ess_th, StepIO io,
+    const double np_recip, double* __restrict__ boff, DistScratch* __restrict__ scr,
+    const DistPeers P) {
+    __shared__ double sh[2048];                             // buffer partials (nch <= 2048)
+    const uint64_t epoch = dist_epoch(io);
+    if (RECORD)
+        dist_record(n, dp, w_un, tail_leaves, tail_ops, n_tail_leaves, n_tail_ops, xs, ys, ts, P,
+                    epoch, sh);
+    if (FINALIZE) {
+        if (RECORD) __syncthreads();
+        dist_finalize(n, dp, s_cur, refp, flags, ess_th, io, np_recip, boff, scr, P, epoch, sh);
     }
 }
 

@@ -88,26 +88,27 @@ int dist_enqueue_step(slam_dist* d) {
     for (int i = 0; i < m; ++i) {                         // unpack (waits for the items)
         slam_pf* h = d->sh[i];
         const int c = h->cur;
-        dist_unpack_kernel<<<grid_for(h->n, 256), 256, 0, h->stream>>>(
-            h->n, h->x[c], h->y[c], h->th[c], d->tk[i] + 3 * kTicketWords, h->flags, d->peers[i],
-            step_io(h));
+        dist_unpack_kernel<<<std::min<unsigned>(grid_for(h->n, 256), 1024), 256, 0, h->stream>>>(
+            h->n, h->x[c], h->y[c], h->th[c], h->dp.mark, h->dp.carry, d->tk[i] + 3 * kTicketWords,
+            h->flags, d->scr[i], d->peers[i], step_io(h));
     }
     SLAM_HIP_TRY(hipGetLastError());
     int rc;
     for (int i = 0; i < m; ++i)                           // predict + likelihood
         if ((rc = launch_fused(d->sh[i], d->sh[i]->cfg.motion, false))) return rc;
-    for (int i = 0; i < m; ++i) {                         // record + push
+    auto reduce = [&](int i, auto kern) {
         slam_pf* h = d->sh[i];
         const int c = h->cur;
-        dist_record_push_kernel<<<1, kFinThreads, 0, h->stream>>>(
+        kern<<<1, kFinThreads, 0, h->stream>>>(
             h->n, h->dp, h->w_un, h->tail_leaves, h->tail_ops, h->n_tail_leaves, h->n_tail_ops,
-            h->x[c], h->y[c], h->th[c], d->peers[i], step_io(h));
-    }
-    for (int i = 0; i < m; ++i) {                         // global finalize (waits for the records)
-        slam_pf* h = d->sh[i];
-        dist_finalize_kernel<<<1, kFinThreads, 0, h->stream>>>(
-            h->n, h->dp, h->s_cur, h->refp, h->flags, h->cfg.ess_threshold, step_io(h),
-            h->pc.np_recip, h->boff, d->scr[i], d->peers[i]);
+            h->x[c], h->y[c], h->th[c], h->s_cur, h->refp, h->flags, h->cfg.ess_threshold,
+            step_io(h), h->pc.np_recip, h->boff, d->scr[i], d->peers[i]);
+    };
+    if (m == 1) {                                         // record + push, wait, global finalize
+        reduce(0, dist_reduce_kernel<true, true>);
+    } else {                                              // one stream: every record first
+        for (int i = 0; i < m; ++i) reduce(i, dist_reduce_kernel<true, false>);
+        for (int i = 0; i < m; ++i) reduce(i, dist_reduce_kernel<false, true>);
     }
     SLAM_HIP_TRY(hipGetLastError());
     return SLAM_OK;

@@ -5,6 +5,7 @@
 namespace slam {
 
 constexpr int kMotionNone = 2;     // internal: likelihood-only pass
+constexpr int kClosedWords = 16;   // S_ll, S_lx, S_ly, S_zz, S_zx, S_zy, D, E (hi, lo each)
 constexpr int kSumChunk = 8192;     // np.sum buffer size (particle_filter.py:234 order)
 constexpr int kScanBlock = 2048;    // elements per block of the exact-cumsum passes
 constexpr int kScanThreads = 256;
@@ -54,7 +55,7 @@ struct LikConst {
     int32_t has_rho;
     int32_t iso;            // sx2 == sy2 and rho == 0 (log-sum shortcut)
     int32_t nl;
-    int32_t pad;
+    int32_t closed;         // iso log-sum from the per-step landmark/observation sums (StepIO.zc)
 };
 
 struct PredictConst {
@@ -73,6 +74,7 @@ struct PredictConst {
 struct StepIO {
     const double* ctl;      // [cap][2] control (v, omega)
     const double* z;        // [cap][2*NL] robot-frame observations
+    const double* zc;       // [cap][kClosedWords] closed-form log-sum sums (double-double pairs)
     const double* ofs;      // [cap] host resample offset (NaN: device RNG)
     slam_pf_result* res;    // [cap] result records
     int32_t* ctr;           // [0] step within the batch, [1] global RNG step

@@ -383,6 +383,35 @@ __device__ __forceinline__ void predict_particle(const double x, const double y,
     }
 }
 
+// double-double values (closed-form log-sum): explicit fma, -ffp-contract=off
+struct dd_t {
+    double h, l;
+};
+__device__ __forceinline__ dd_t dd_two_prod(const double a, const double b) {
+    const double p = a * b;
+    return {p, fma(a, b, -p)};
+}
+__device__ __forceinline__ dd_t dd_renorm(const double p, const double e) {
+    const double r = p + e;
+    return {r, e - (r - p)};
+}
+__device__ __forceinline__ dd_t dd_add2(const dd_t a, const dd_t b) {
+    const double t = a.h + b.h;
+    const double bb = t - a.h;
+    return dd_renorm(t, ((a.h - (t - bb)) + (b.h - bb)) + (a.l + b.l));
+}
+__device__ __forceinline__ dd_t dd_mul_d(const dd_t a, const double b) {
+    const double p = a.h * b;
+    return dd_renorm(p, fma(a.h, b, -p) + a.l * b);
+}
+__device__ __forceinline__ dd_t dd_mul(const dd_t a, const dd_t b) {
+    const double p = a.h * b.h;
+    return dd_renorm(p, fma(a.h, b.h, -p) + (a.h * b.l + a.l * b.h));
+}
+__device__ __forceinline__ dd_t dd_scale(const dd_t a, const double p2) {   // p2 = +-2^k: exact
+    return {a.h * p2, a.l * p2};
+}
+
 // One landmark factor in the reference's rounding order
 // (particle_filter.py:187-191: mylib/transform.py:31-35 then mlab.bivariate_normal).
 __device__ __forceinline__ double ref_q(const double xn, const double yn, const double sp,
@@ -512,7 +541,8 @@ template <int LIK, int P>
 __device__ __forceinline__ void likelihood_lanes(const double* xn, const double* yn,
                                                  const double* sp, const double* cp,
                                                  const double* __restrict__ lm,
-                                                 const double* __restrict__ z, const LikConst& lc,
+                                                 const double* __restrict__ z,
+                                                 const double* __restrict__ zc, const LikConst& lc,
                                                  double* bn) {
     const int nl = lc.nl;
     if (LIK == SLAM_LIK_PRODUCT) {
@@ -530,7 +560,30 @@ __device__ __forceinline__ void likelihood_lanes(const double* xn, const double*
         return;
     }
     double L[P];
-    if (lc.iso) {
+    if (lc.closed) {
+        // sum_j |R(l_j - p) - z_j|^2 in closed form (iso: q_j = that / sx2):
+        //   k |l - p|^2 summed - 2 sum z.R(l - p) + sum |z|^2,  k = c^2 + s^2,
+        // from the step's landmark / observation sums, in double-double (the
+        // terms are ~1e4, the sum ~NL sx2: fp64 would lose ~1e-12 in L).  The
+        // exact value of the reference's sum: the difference to the reference
+        // is its own rounding (~1e-14 relative of the weight).
+        const dd_t Sll{zc[0], zc[1]}, Slx{zc[2], zc[3]}, Sly{zc[4], zc[5]}, Szz{zc[6], zc[7]};
+        const dd_t Szx{zc[8], zc[9]}, Szy{zc[10], zc[11]}, Dd{zc[12], zc[13]}, Ed{zc[14], zc[15]};
+        const double fnl = (double)nl;
+#pragma unroll
+        for (int k = 0; k < P; ++k) {
+            const double x = xn[k], y = yn[k], c = cp[k], sn = sp[k];
+            const dd_t r2 = dd_add2(dd_two_prod(x, x), dd_two_prod(y, y));          // |p|^2
+            const dd_t t1 = dd_add2(dd_mul_d(Slx, x), dd_mul_d(Sly, y));            // p . S_l
+            const dd_t p1 = dd_add2(dd_add2(Sll, dd_scale(t1, -2.0)), dd_mul_d(r2, fnl));
+            const dd_t kk = dd_add2(dd_two_prod(c, c), dd_two_prod(sn, sn));
+            const dd_t q1 = dd_add2(Dd, dd_scale(dd_add2(dd_mul_d(Szx, x), dd_mul_d(Szy, y)), -1.0));
+            const dd_t q2 = dd_add2(Ed, dd_scale(dd_add2(dd_mul_d(Szy, x), dd_mul_d(Szx, -y)), -1.0));
+            const dd_t rr = dd_add2(dd_mul_d(q1, c), dd_mul_d(q2, sn));
+            const dd_t acc = dd_add2(dd_add2(dd_mul(kk, p1), dd_scale(rr, -2.0)), Szz);
+            L[k] = nl ? fma(-0.5, acc.h * lc.rsx2, lc.neg_nl_ln_den) : lc.neg_nl_ln_den;
+        }
+    } else if (lc.iso) {
         double a[P][2];
 #pragma unroll
         for (int k = 0; k < P; ++k) a[k][0] = a[k][1] = 0.0;
@@ -848,7 +901,7 @@ __global__ __launch_bounds__(256) SLAM_FUSED_ATTR void pf_fused_kernel(
 
     // ---- likelihood and weight (particle_filter.py:170-198)
     double bn[P];
-    likelihood_lanes<LIK, P>(xv, yv, sp, cp, lm, zs, lc, bn);
+    likelihood_lanes<LIK, P>(xv, yv, sp, cp, lm, zs, io.zc + (size_t)st * kClosedWords, lc, bn);
     // previous weights: particle_filter.py:222 (a resampled step starts from
     // 1/NP) / :235-236 (deferred: w_un / s, NaN -> 1/NP)
     double wv[P];

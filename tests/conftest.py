@@ -69,18 +69,44 @@ def weights_match(w, ref, rtol=1e-12, floor=DBL_MIN):
     subnormal grid both sides round onto).  A multi-step trajectory passes a
     larger floor with the absolute bound rtol * floor below it: weights that
     went through the subnormal range in an earlier step carry that step's
-    precision loss -- the reference's own arithmetic.  Returns the worst
-    relative error seen."""
+    precision loss -- the reference's own arithmetic.  rtol may be per element
+    (see subnormal_dip_rtol).  Returns the worst relative error seen."""
     w, ref = np.asarray(w), np.asarray(ref)
     zw, zr = w == 0, ref == 0
     assert np.array_equal(zw, zr), f"zero sets differ at {np.flatnonzero(zw != zr)[:8]}"
     nz = ~zr
     normal = nz & (np.abs(ref) >= floor)
+    rt = np.broadcast_to(np.asarray(rtol, dtype=np.float64), ref.shape)
     rel = np.abs(w[normal] - ref[normal]) / np.abs(ref[normal])
     worst = float(rel.max()) if rel.size else 0.0
-    assert worst <= rtol, f"max relative weight error {worst:.3g} > {rtol}"
+    if rel.size and np.any(rel > rt[normal]):
+        i = int(np.argmax(rel / rt[normal]))
+        raise AssertionError(f"max relative weight error {rel[i]:.3g} > {rt[normal][i]:.3g} "
+                             f"(element {np.flatnonzero(normal)[i]})")
     sub = nz & ~normal
     if sub.any():
-        atol = 2 * 2.0 ** -1074 if floor <= DBL_MIN else rtol * floor
+        atol = 2 * 2.0 ** -1074 if floor <= DBL_MIN else rt[sub] * floor
+        # a per-element rtol above the bar (a subnormal dip) bounds these too
+        atol = np.maximum(atol, rt[sub] * np.abs(ref[sub]))
         assert np.all(np.abs(w[sub] - ref[sub]) <= atol)
     return worst
+
+
+def subnormal_dip_rtol(factors, rtol, w_prev=None):
+    """Per-particle weight tolerance for a sequential product (particle_filter.py:
+    192) whose partial products dip below DBL_MIN and climb back: from the dip
+    on the product carries the subnormal grid's absolute quantum, so one ulp of
+    difference in any factor there (exp within 1 ulp) moves the result by up to
+    ~2^-1074 / (smallest partial product) relative -- the reference's own
+    precision loss.  w_prev: the previous weights, whose product with the
+    likelihood (particle_filter.py:194, before normalising) is one more partial
+    product.  rtol elsewhere."""
+    cp = np.cumprod(factors, axis=1)
+    dip = cp.min(axis=1)
+    if w_prev is not None:
+        dip = np.minimum(dip, w_prev * cp[:, -1])
+    del cp
+    out = np.full(dip.shape, float(rtol))
+    low = (dip > 0) & (dip < DBL_MIN)
+    out[low] = np.maximum(rtol, 4 * 2.0 ** -1074 / dip[low])
+    return out

@@ -1,11 +1,11 @@
-#!/bin/bash
-# Development loop on the GPU box: parity tests, then the landmark sweep with
-# the fused kernel's VALU counts (tools/pmc_nl.sh).  Stops at the first failure.
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+# selected GPU test files, then the default bench line
+cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
-OUT=gpurun_out/${TAG:-quick}
-mkdir -p "$OUT"
-timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread ${PYTEST_ARGS:-} > "$OUT/pytest_gpu.log" 2>&1
-rc=$?; echo "pytest rc=$rc"; tail -15 "$OUT/pytest_gpu.log"
-if [ $rc != 0 ]; then exit $rc; fi
-TAG=${TAG:-quick}/nl bash tools/pmc_nl.sh
+out=gpurun_out/$1; shift
+mkdir -p $out
+timeout -k 10 600 python -u -m pytest "$@" -x -v -rA -s --timeout 300 --timeout-method thread > $out/pytest.log 2>&1
+rc=$?; echo "pytest rc=$rc"; grep -E "PASSED|FAILED|passed|failed|^E  " $out/pytest.log | tail -40
+[ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python bench.py --no-cpu-baseline --no-secondary > $out/bench.json 2> $out/bench.err
+rc=$?; echo "bench rc=$rc"; cat $out/bench.json
+exit $rc

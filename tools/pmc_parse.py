@@ -43,9 +43,16 @@ def main(src, tag):
             rec["hbm_write_bytes"] = d["WRITE_SIZE"] * 1024
         for k in ("SQ_WAVES", "SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS", "SQ_WAVE_CYCLES",
                   "SQ_BUSY_CYCLES", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY",
-                  "GRBM_GUI_ACTIVE", "SQ_INSTS_VMEM_RD", "SQ_INSTS_VMEM_WR"):
+                  "GRBM_GUI_ACTIVE", "SQ_INSTS_VMEM_RD", "SQ_INSTS_VMEM_WR",
+                  "SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_FMA_F64",
+                  "SQ_INSTS_VALU_TRANS_F64"):
             if k in d:
                 rec[k] = d[k]
+        f64 = ("SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_FMA_F64",
+               "SQ_INSTS_VALU_TRANS_F64")
+        if all(k in d for k in f64):
+            # executed fp64 flops per launch: 64 lanes x (add + mul + trans + 2 fma)
+            rec["fp64_flops"] = 64 * (d[f64[0]] + d[f64[1]] + d[f64[3]] + 2 * d[f64[2]])
         if "SQ_INSTS_VALU" in d and "SQ_WAVES" in d and d["SQ_WAVES"]:
             rec["valu_insts_per_wave"] = d["SQ_INSTS_VALU"] / d["SQ_WAVES"]
         out[short(name) + ("" if "<" not in name else name[name.index("<"):name.index(">") + 1])] = rec
@@ -56,12 +63,15 @@ def main(src, tag):
     if key in out and "hbm_read_bytes" in out[key] and "hbm_write_bytes" in out[key]:
         v = out[key]
         traffic = v["hbm_read_bytes"] + v["hbm_write_bytes"]
+        extra = {k: v[k] for k in ("fp64_flops", "SQ_INSTS_VALU", "SQ_WAVES", "avg_dur_us_profiled")
+                 if k in v}
         sys.path.insert(0, os.getcwd())
         from bench import pf_sources_sha
         with open("profiles/pmc_traffic.json", "w") as f:
             json.dump({"source": f"profiles/{tag}_pmc.json", "kernel": key,
                        "fused_kernel_hbm_bytes_per_launch": traffic,
                        "sources_sha": pf_sources_sha(),
+                       "fused_kernel": extra,
                        "note": "FETCH_SIZE x2 (gfx950 half-count) + WRITE_SIZE, KB -> B, mean over launches"},
                       f, indent=1)
     for k, v in sorted(out.items()):
