@@ -205,12 +205,12 @@ def load_pmc_traffic():
         with open(path) as f:
             d = json.load(f)
     except Exception:
-        return None, "no profiles/pmc_traffic.json"
+        return None, "no profiles/pmc_traffic.json", {}
     cur = pf_sources_sha()
     if d.get("sources_sha") != cur:
-        return None, f"stale: measured on sources {d.get('sources_sha')}, current {cur}"
+        return None, f"stale: measured on sources {d.get('sources_sha')}, current {cur}", {}
     return d.get("fused_kernel_hbm_bytes_per_launch"), \
-        f"rocprofv3 PMC ({d.get('source')}), sources {cur}"
+        f"rocprofv3 PMC ({d.get('source')}), sources {cur}", d.get("fused_kernel", {})
 
 
 # ----------------------------------------------------------- secondary rows
@@ -526,7 +526,7 @@ def main():
     value = updates / elapsed
     fused_avg_s = fused_ms / 1e3 / max(fused_n, 1)
     achieved_tf = FLOPS_PER_UPDATE[args.likelihood] * NP_PER_GPU * NL / fused_avg_s / 1e12
-    traffic, traffic_src = load_pmc_traffic()
+    traffic, traffic_src, pmc = load_pmc_traffic()
     line = {
         "metric": METRIC,
         "value": value,
@@ -553,8 +553,12 @@ def main():
                      "frac": achieved_tf / FP64_PEAK_TFLOPS, "traffic": traffic,
                      "traffic_source": traffic_src,
                      "note": "fp64-VALU bound (not HBM, not MFMA); peak = MI355X fp64 vector "
-                             "78.6 TF; "
-                             f"{FLOPS_PER_UPDATE[args.likelihood]} algorithmic flops/update (fma = 2, exp = div = 1)",
+                             "78.6 TF; achieved counts the reference algorithm's "
+                             f"{FLOPS_PER_UPDATE[args.likelihood]} flops per particle-landmark update "
+                             "(SURVEY 8(d); fma = 2, exp = div = 1)" +
+                             ("; the kernel evaluates the iso log-sum in closed form (O(NP + NL) per "
+                              "step, DESIGN 4.3): its executed fp64 work is executed_fp64_tflops"
+                              if args.likelihood == "logsum" else ""),
                      "avg_launch_ms": fused_avg_s * 1e3,
                      "hbm_gbs_algorithmic": BYTES_PER_PARTICLE * NP_PER_GPU / fused_avg_s / 1e9},
         "breakdown_ms_per_step": {"fused": fused_ms / max(fused_n, 1),
@@ -563,6 +567,14 @@ def main():
                                   "step_events": step_ms / max(step_n, 1)},
         "resample_steps": int(sum(o["resampled"] for o in out)),
     }
+    if pmc.get("fp64_flops") and args.likelihood == "logsum":
+        # executed fp64 flops (PMC SQ_INSTS_VALU_{ADD,MUL,FMA,TRANS}_F64 x 64 lanes, fma = 2)
+        # over this run's live launch time, and the VALU issue utilisation: every wave64
+        # VALU instruction occupies a 16-lane SIMD for 4 cycles (256 CUs x 4 SIMDs, 2.4 GHz)
+        rf = line["roofline"]
+        rf["executed_fp64_tflops"] = pmc["fp64_flops"] / fused_avg_s / 1e12
+        if pmc.get("SQ_INSTS_VALU"):
+            rf["valu_issue_frac"] = pmc["SQ_INSTS_VALU"] * 4 / (1024 * 2.4e9 * fused_avg_s)
     if world == 1 and args.likelihood != "product":
         e2, _, t2 = measure("product")
         line["alt_modes"] = {"product": {"value": NP_PER_GPU * NL * args.steps / e2,

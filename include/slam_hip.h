@@ -221,6 +221,9 @@ int slam_dist_step(slam_dist* d, const double* control, const double* z, slam_pf
 int slam_dist_load_observations(slam_dist* d, int32_t n_steps, const double* z_all);
 int slam_dist_run(slam_dist* d, int32_t first_step, int32_t n_steps, const double* controls,
                   slam_pf_result* results);
+/* resample exchange form: 1 = one launch (the default with one held shard whose
+ * scan grid is co-resident), 0 = five launches; on < 0 only reports */
+int slam_dist_set_merged(slam_dist* d, int32_t on, int32_t* active);
 
 /* ====================================================================
  * EKF localisation -- replaces ExtendedKalmanFilter

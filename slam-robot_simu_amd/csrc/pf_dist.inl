@@ -65,13 +65,21 @@ struct DistLayout {
     int64_t spec_hdr = 0;       // [world] {nspec, ktot}
     int64_t spec = 0;           // [world][cap_spec] SpecialIn
     int64_t item_hdr = 0;       // [world] {count, pad}
-    int64_t item = 0;           // [world][cap_item] ShardItem
+    int64_t item = 0;           // [world][cap_item] DistItem (own slot unused: self_items)
     int64_t total = 0;
     int64_t rec_stride = 0, cap_spec = 0, cap_item = 0;
 };
 
+// a resampled particle with its destination positions [lo, hi) (global), 48 B:
+// three 16-byte stores
+struct alignas(16) DistItem {
+    double x, y, th;
+    int64_t lo, hi, pad;
+};
+
 struct DistPeers {
     char* base[kDistMaxWorld];  // every rank's exchange region as mapped in this process
+    DistItem* self_items;       // items this rank sends itself (regular memory, cap_item)
     int64_t gb[kDistMaxWorld + 1];
     DistLayout L;
     int32_t world, rank;
@@ -87,6 +95,7 @@ struct DistScratch {
     double c_left;              // exact cumsum just before local element 0 (-inf on rank 0)
     int64_t lo0;                // positions <= c_left
     int64_t covered;            // positions covered by the received items (unpack; reset by its last block)
+    int32_t rel[2];             // dist_resample_merged_kernel: release tokens of phases A / B
     int64_t dbase[kDistMaxWorld];   // per destination: selected sources before its range
     int64_t dcnt[kDistMaxWorld];    // per destination: items sent
 };
@@ -95,12 +104,21 @@ __device__ __forceinline__ uint64_t* dist_flags(const DistPeers& P, const int q)
     return reinterpret_cast<uint64_t*>(P.base[q] + P.L.flags);
 }
 
-// publish `epoch` in flag word [kind][my rank] of every peer (after the data)
+// publish `epoch` in flag word [kind][my rank] of every peer (after the data).
+// One system-scope release per block: on gfx950 it writes back the L2, so
+// every lane's stores complete first (barrier), then lane 0 fences once and
+// stores the flags.  Data that other blocks stored earlier in the launch was
+// written with system-scope stores (dist_store_item) and had completed before
+// their tickets.
 __device__ __forceinline__ void dist_signal(const DistPeers& P, const int kind, const uint64_t epoch) {
-    __threadfence_system();
-    if ((int)threadIdx.x < P.world)
-        __hip_atomic_store(dist_flags(P, threadIdx.x) + kind * kDistMaxWorld + P.rank, epoch,
-                           __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __threadfence_system();
+        for (int q = 0; q < P.world; ++q)
+            __hip_atomic_store(dist_flags(P, q) + kind * kDistMaxWorld + P.rank, epoch,
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
 }
 
 // wait until every peer published `epoch` in my flag words [kind][q]
@@ -134,6 +152,30 @@ __device__ __forceinline__ S ld_sys_struct(const S* p) {
 #pragma unroll
     for (int k = 0; k < (int)(sizeof(S) / 8); ++k) d[k] = ld_sys(reinterpret_cast<const uint64_t*>(p) + k);
     return v;
+}
+
+typedef unsigned long long dist_u64x2 __attribute__((ext_vector_type(2)));
+
+// own items: three 16-byte stores to regular memory (read by a later launch on
+// this device); a peer's: system-scope stores into its exchange region, so
+// they have completed at system scope once the storing block's vmcnt drains
+// (before its ticket) -- no per-block L2 writeback
+__device__ __forceinline__ void dist_store_item(const DistPeers& P, const int d, const int64_t slot,
+                                                const double x, const double y, const double th,
+                                                const int64_t lo, const int64_t hi) {
+    if (d == P.rank) {
+        dist_u64x2* p = reinterpret_cast<dist_u64x2*>(P.self_items + slot);
+        p[0] = dist_u64x2{(unsigned long long)__double_as_longlong(x), (unsigned long long)__double_as_longlong(y)};
+        p[1] = dist_u64x2{(unsigned long long)__double_as_longlong(th), (unsigned long long)lo};
+        p[2] = dist_u64x2{(unsigned long long)hi, 0ull};
+        return;
+    }
+    uint64_t* p = reinterpret_cast<uint64_t*>(reinterpret_cast<DistItem*>(P.base[d] + P.L.item) +
+                                              (int64_t)P.rank * P.L.cap_item + slot);
+    const uint64_t v[5] = {(uint64_t)__double_as_longlong(x), (uint64_t)__double_as_longlong(y),
+                           (uint64_t)__double_as_longlong(th), (uint64_t)lo, (uint64_t)hi};
+#pragma unroll
+    for (int k = 0; k < 5; ++k) __hip_atomic_store(p + k, v[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 __device__ __forceinline__ uint64_t dist_epoch(const StepIO& io) { return (uint64_t)io.ctr[1] + 1; }
@@ -367,24 +409,19 @@ __global__ __launch_bounds__(kScanThreads) void dist_pack_push_kernel(
         if (i >= n) break;
         if (sel[k]) {
             const int64_t lo = prev, h = hv[k];
-            ShardItem it;
-            it.x = xs[i];
-            it.y = ys[i];
-            it.th = ts[i];
+            const double x = xs[i], y = ys[i], th = ts[i];
             for (int d = dist_owner(P, lo); d < P.world && P.gb[d] < h; ++d) {
                 const int64_t slot = ps - scr->dbase[d];
-                it.lo = lo > P.gb[d] ? lo : P.gb[d];
-                it.hi = h < P.gb[d + 1] ? h : P.gb[d + 1];
-                ShardItem* dst = reinterpret_cast<ShardItem*>(P.base[d] + P.L.item) +
-                                 (int64_t)P.rank * P.L.cap_item;
-                if (slot >= 0 && slot < P.L.cap_item) dst[slot] = it;
+                if (slot >= 0 && slot < P.L.cap_item)
+                    dist_store_item(P, d, slot, x, y, th, lo > P.gb[d] ? lo : P.gb[d],
+                                    h < P.gb[d + 1] ? h : P.gb[d + 1]);
                 else atomicOr(&flags[kFlagStatus], kDistStItems);
             }
             ++ps;
         }
         prev = hv[k];
     }
-    if (!arrive_last(counter)) return;
+    if (!arrive_last(counter)) return;                      // (drains this block's item stores)
     if ((int)threadIdx.x < P.world) {
         int64_t* hdr = reinterpret_cast<int64_t*>(P.base[threadIdx.x] + P.L.item_hdr) + 2 * P.rank;
         hdr[0] = scr->dcnt[threadIdx.x];
@@ -411,7 +448,7 @@ __global__ __launch_bounds__(256) void dist_unpack_kernel(
     __shared__ int64_t s_off[kDistMaxWorld + 1];
     __shared__ unsigned long long s_cov;
     const char* mine = P.base[P.rank];
-    const ShardItem* items = reinterpret_cast<const ShardItem*>(mine + P.L.item);
+    const DistItem* items = reinterpret_cast<const DistItem*>(mine + P.L.item);
     if (threadIdx.x == 0) {
         int64_t o = 0;
         for (int q = 0; q < P.world; ++q) {
@@ -430,9 +467,24 @@ __global__ __launch_bounds__(256) void dist_unpack_kernel(
          k += (int64_t)gridDim.x * blockDim.x) {
         int q = 0;
         while (q + 1 < P.world && s_off[q + 1] <= k) ++q;
-        const ShardItem* it = items + (int64_t)q * P.L.cap_item + (k - s_off[q]);
-        const int64_t lo = (int64_t)ld_sys(&it->lo) - gb, hi = (int64_t)ld_sys(&it->hi) - gb;
-        const double x = ld_sys_d(&it->x), y = ld_sys_d(&it->y), th = ld_sys_d(&it->th);
+        int64_t lo, hi;
+        double x, y, th;
+        if (q == P.rank) {                                  // own items: regular memory
+            const dist_u64x2* it = reinterpret_cast<const dist_u64x2*>(P.self_items + (k - s_off[q]));
+            const dist_u64x2 a = it[0], b = it[1], c = it[2];
+            x = __longlong_as_double((long long)a.x);
+            y = __longlong_as_double((long long)a.y);
+            th = __longlong_as_double((long long)b.x);
+            lo = (int64_t)b.y - gb;
+            hi = (int64_t)c.x - gb;
+        } else {
+            const DistItem* it = items + (int64_t)q * P.L.cap_item + (k - s_off[q]);
+            lo = (int64_t)ld_sys(&it->lo) - gb;
+            hi = (int64_t)ld_sys(&it->hi) - gb;
+            x = ld_sys_d(&it->x);
+            y = ld_sys_d(&it->y);
+            th = ld_sys_d(&it->th);
+        }
         if (!(lo >= 0 && lo < hi && hi <= n)) {
             atomicOr(&flags[kFlagStatus], kDistStItems);
             continue;
@@ -454,6 +506,393 @@ __global__ __launch_bounds__(256) void dist_unpack_kernel(
         const unsigned long long c = atomicExch((unsigned long long*)&scr->covered, 0ull);
         if ((int64_t)c != n || s_off[P.world] > n) atomicOr(&flags[kFlagStatus], kDistStItems);
     }
+}
+
+// ---------------------------------------------------------------- resample, one launch
+// The whole exchange side of a resample step in ONE launch (one shard per
+// process; the grid must be co-resident -- checked on the host -- because its
+// blocks wait for one another twice):
+//   A  every wave classifies its 512-element tile of w = w_un / s with the
+//      global approximate prefix (the lean exact cumsum's pass A) and stages its
+//      special elements; the last block scans the tile totals, pushes this
+//      rank's specials (global index, rank-local increment prefix) into every
+//      peer's slot, waits for every rank's, folds the global list in rank
+//      order (one wave, 63 specials per round) and releases the grid;
+//   B  every wave expands its tile's exact cumsum from the classification it
+//      kept in registers, counts the systematic positions at or below each
+//      c_j (a run [s_j, e_j) per selected source) and the block's selected
+//      sources, per destination rank too; the last block scans the counts and
+//      releases the grid again;
+//   C  every selected source is pushed, clipped to each destination's
+//      positions, into that destination's item slot for this rank; the last
+//      block publishes the counts and signals kXItem.
+// dist_unpack_kernel then hands the received items to the fused kernel.
+constexpr int kDistTokenWait = 1 << 22;
+
+// bounded wait of thread 0 for `token` in a write-through word; the block's
+// threads then all see the released data (agent-scope acquire)
+__device__ __forceinline__ bool dist_token_wait(const int32_t* word, const int32_t token,
+                                                int32_t* flags) {
+    __shared__ int s_go;
+    if (threadIdx.x == 0) {
+        int go = 0;
+        for (int it = 0; it < kDistTokenWait; ++it) {
+            if (ld_wt_i(word) == token) {
+                go = 1;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(2);
+        }
+        if (!go) atomicOr(&flags[kFlagStatus], kDistStWait);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        s_go = go;
+    }
+    __syncthreads();
+    return s_go != 0;
+}
+
+__device__ __forceinline__ void dist_token_release(int32_t* word, const int32_t token) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        st_wt_i(word, token);
+    }
+}
+
+// the global fold over every rank's specials (in this rank's exchange region),
+// by wave 0 of the calling block: lean_place_fold's 63-per-round walk.  Writes
+// every global SpecialOut; sets the fallback flag when a run check fails.
+__device__ void dist_fold_global(const DistPeers& P, const int64_t* s_off, const uint64_t* s_koff,
+                                 const int64_t M, const uint64_t ktot, const int64_t n_global,
+                                 SpecialOut* __restrict__ out, int32_t* __restrict__ flags) {
+    __shared__ int s_bad;
+    if (threadIdx.x == 0) {
+        s_bad = 0;
+        flags[kFlagNSpecial] = (int32_t)M;
+    }
+    __syncthreads();
+    const char* mine = P.base[P.rank];
+    if (threadIdx.x < 64) {
+        const int lane = threadIdx.x;
+        auto load_special = [&](const int64_t m, SpecialIn& e) {
+            int q = 0;
+            while (q + 1 < P.world && s_off[q + 1] <= m) ++q;
+            const SpecialIn* src = reinterpret_cast<const SpecialIn*>(mine + P.L.spec) + (int64_t)q * P.L.cap_spec;
+            e = ld_sys_struct(&src[m - s_off[q]]);
+            e.P += s_koff[q];
+        };
+        double s = 0.0;
+        bool bad = false;
+        for (int64_t t0 = 0; t0 < M; t0 += 63) {
+            const int64_t m = t0 + lane;
+            SpecialIn e{};
+            if (m < M) load_special(m, e);
+            int64_t nidx = __shfl_down((long long)e.idx, 1, 64);
+            uint64_t nP = (uint64_t)__shfl_down((long long)e.P, 1, 64);
+            if (m + 1 >= M) {
+                nidx = n_global;
+                nP = ktot;
+            }
+            const bool mine_l = (lane < 63) && (m < M);
+            const bool run = mine_l && (nidx - e.idx > 1);
+            const uint64_t K = nP - e.P;
+            const int E = e.E;
+            double lo = -__builtin_inf(), hi = __builtin_inf(), ku = 0.0;
+            if (run) {
+                lo = (E == -1022) ? 0.0 : ldexp(1.0, E);
+                hi = (E == -1022) ? 0x1p-1021 : ldexp(1.0, E + 1);
+                ku = (double)K * ldexp(1.0, E - 52);
+                if ((double)K >= 0x1p53) bad = true;
+            }
+            const double w = mine_l ? e.w : 0.0;
+            double cs = 0.0;
+            const int lim = (M - t0 < 63) ? (int)(M - t0) : 63;
+            for (int l = 0; l < lim; ++l) {
+                s = s + readlane_d(w, l);
+                if (lane == l) cs = s;
+                const double blo = readlane_d(lo, l), bhi = readlane_d(hi, l);
+                if (!(s >= blo) || !(s < bhi)) bad = true;
+                s = s + readlane_d(ku, l);
+                if (!(s < bhi)) bad = true;
+            }
+            if (mine_l) {
+                SpecialOut o;
+                o.cs = cs;
+                o.P = e.P;
+                o.E = e.E;
+                o.pad = 0;
+                st_wt_struct(&out[m], o);
+            }
+        }
+        if (__any(bad) && lane == 0) s_bad = 1;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        if (s_bad) flags[kFlagStatus] |= 2;
+        st_wt_i(&flags[kFlagFallback], s_bad ? 1 : 0);
+    }
+}
+
+__global__ __launch_bounds__(kScanThreads) void dist_resample_merged_kernel(
+    const double* __restrict__ w_un, const double* __restrict__ s_in, const double np_recip,
+    const int64_t n, const double* __restrict__ boff, const double delta,
+    SpecialIn* __restrict__ stage, uint64_t* __restrict__ bk, int32_t* __restrict__ bf,
+    uint64_t* __restrict__ boffk, int32_t* __restrict__ bofff, uint64_t* __restrict__ ktot_p,
+    int32_t* __restrict__ nspec_p, unsigned* __restrict__ tk, int32_t* __restrict__ flags,
+    SpecialOut* __restrict__ spec_go, DistScratch* __restrict__ scr,
+    int32_t* __restrict__ bsel, int32_t* __restrict__ bsel_off, int32_t* __restrict__ bdst,
+    const double* __restrict__ xs, const double* __restrict__ ys, const double* __restrict__ ts,
+    const DistPeers P, StepIO io, const PredictConst pc, const uint64_t seed, const int ntiles) {
+    if (!dist_resampling(flags)) return;
+    __shared__ int64_t s_off[kDistMaxWorld + 1];
+    __shared__ uint64_t s_koff[kDistMaxWorld + 1];
+    __shared__ int32_t s_cb[kDistMaxWorld], s_cc[kDistMaxWorld];
+    const uint64_t epoch = dist_epoch(io);
+    const int32_t tokA = ld_wt_i(&scr->rel[0]) + 1;        // read before this block arrives
+    const int32_t tokB = ld_wt_i(&scr->rel[1]) + 1;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int64_t tile = (int64_t)blockIdx.x * kTilesPerBlock + wave;
+    const bool active = tile < ntiles;
+    const int64_t gbase = P.gb[P.rank], n_global = P.gb[P.world];
+    if (blockIdx.x == 0) PROBE_AT(16);
+    // ---- A: classify + stage
+    TileScan tsc;
+    uint64_t ktile = 0, kofs, kblk;
+    int32_t ftile = 0, fofs, fblk;
+    if (active)
+        wave_tile_classify(w_un, *s_in, np_recip, n, tile, boff[tile] + scr->base_off, delta, tsc,
+                           ktile, ftile);
+    block_tile_offsets(ktile, ftile, kofs, fofs, kblk, fblk);
+    if (active) wave_tile_stage(tile, tsc, kofs, fofs, kblk, fblk, stage, bk, bf);
+    else if (threadIdx.x == 0) {
+        st_wt(&bk[blockIdx.x], kblk);
+        st_wt_i(&bf[blockIdx.x], fblk);
+    }
+    if (arrive_last(tk)) {
+        PROBE_AT(17);
+        __shared__ uint64_t shk[kScanThreads / 64 + 1];
+        __shared__ int32_t shf[kScanThreads / 64 + 1];
+        block_scan_array<uint64_t, kScanThreads>(bk, boffk, gridDim.x, ktot_p, shk, true);
+        __syncthreads();
+        block_scan_array<int32_t, kScanThreads>(bf, bofff, gridDim.x, nspec_p, shf, true);
+        __syncthreads();
+        const int32_t ns = ld_wt_i(nspec_p);
+        const uint64_t kt = ld_wt(ktot_p);
+        PROBE_AT(18);
+        // this rank's specials in order -> every peer's slot (tile by bofff search)
+        for (int32_t m = threadIdx.x; m < ns; m += blockDim.x) {
+            int lo = 0, hi = (int)gridDim.x - 1;
+            while (lo < hi) {
+                const int mid = (lo + hi + 1) >> 1;
+                if (ld_wt_i(&bofff[mid]) <= m) lo = mid;
+                else hi = mid - 1;
+            }
+            SpecialIn e = ld_wt_struct(&stage[(int64_t)lo * kScanBlock + (m - ld_wt_i(&bofff[lo]))]);
+            e.P += ld_wt(&boffk[lo]);
+            e.idx += gbase;
+            if (m < P.L.cap_spec)
+                for (int q = 0; q < P.world; ++q)
+                    reinterpret_cast<SpecialIn*>(P.base[q] + P.L.spec)[(int64_t)P.rank * P.L.cap_spec + m] = e;
+        }
+        if ((int)threadIdx.x < P.world) {
+            int64_t* hdr = reinterpret_cast<int64_t*>(P.base[threadIdx.x] + P.L.spec_hdr) + 2 * P.rank;
+            hdr[0] = ns < P.L.cap_spec ? ns : P.L.cap_spec;
+            hdr[1] = (int64_t)kt;
+        }
+        if (ns > P.L.cap_spec && threadIdx.x == 0) atomicOr(&flags[kFlagStatus], kDistStItems);
+        __syncthreads();
+        dist_signal(P, kXSpec, epoch);
+        PROBE_AT(19);
+        dist_wait(P, kXSpec, epoch, flags);
+        PROBE_AT(20);
+        if (threadIdx.x == 0) {
+            const char* mine = P.base[P.rank];
+            int64_t no = 0;
+            uint64_t ko = 0;
+            for (int q = 0; q < P.world; ++q) {
+                const int64_t* hdr = reinterpret_cast<const int64_t*>(mine + P.L.spec_hdr) + 2 * q;
+                s_off[q] = no;
+                s_koff[q] = ko;
+                no += (int64_t)ld_sys(hdr);
+                ko += ld_sys(hdr + 1);
+            }
+            s_off[P.world] = no;
+            s_koff[P.world] = ko;
+        }
+        __syncthreads();
+        dist_fold_global(P, s_off, s_koff, s_off[P.world], s_koff[P.world], n_global, spec_go, flags);
+        PROBE_AT(21);
+        if (threadIdx.x == 0) {
+            const int64_t sb = s_off[P.rank];
+            double cl = -INFINITY;
+            int64_t lo0 = 0;
+            if (P.rank > 0 && sb > 0) {
+                const SpecialOut p = ld_wt_struct(&spec_go[sb - 1]);
+                cl = p.cs + (double)(s_koff[P.rank] - p.P) * ldexp(1.0, p.E - 52);
+                const double ofs = resample_offset(io.ofs[io.ctr[0]], np_recip, seed, (uint32_t)io.ctr[1]);
+                lo0 = positions_upto(cl, n_global, pc.rstep, ofs);
+            }
+            scr->spec_base = (int32_t)sb;
+            scr->k_base = s_koff[P.rank];
+            scr->nspec_g = (int32_t)s_off[P.world];
+            scr->ktot_g = s_koff[P.world];
+            scr->c_left = cl;
+            scr->lo0 = lo0;
+        }
+        dist_token_release(&scr->rel[0], tokA);
+        PROBE_AT(22);
+    } else {
+        dist_token_wait(&scr->rel[0], tokA, flags);
+    }
+    __syncthreads();
+    if (ld_wt_i(&flags[kFlagFallback])) return;             // block-uniform
+    // ---- B: expand, positions, selected counts
+    if ((int)threadIdx.x < kDistMaxWorld) {
+        s_cb[threadIdx.x] = 0;
+        s_cc[threadIdx.x] = 0;
+    }
+    const double ofs = resample_offset(io.ofs[io.ctr[0]], np_recip, seed, (uint32_t)io.ctr[1]);
+    const int32_t sb = ld_wt_i(&scr->spec_base);
+    int64_t hv[kScanPer], lv[kScanPer];
+    int32_t cnt = 0;
+    if (active) {
+        const uint64_t kb = ld_wt(&scr->k_base);
+        const int64_t b = blockIdx.x;
+        const uint64_t bk0 = ld_wt(&boffk[b]) + kofs + kb;
+        const int32_t bf0 = ld_wt_i(&bofff[b]) + fofs + sb;
+        uint64_t kin = bk0 + tsc.kex;
+        int32_t m = bf0 + tsc.fex;
+        double out[kScanPer];
+        SpecialOut p = ld_wt_struct(&spec_go[m > 0 ? m - 1 : 0]);
+#pragma unroll
+        for (int k = 0; k < kScanPer; ++k) {
+            kin += tsc.kk[k];
+            if (tsc.ff[k]) {
+                p = ld_wt_struct(&spec_go[m]);
+                out[k] = p.cs;
+                ++m;
+            } else {
+                out[k] = p.cs + (double)(kin - p.P) * ldexp(1.0, p.E - 52);
+            }
+        }
+        double cprev = __shfl_up(out[kScanPer - 1], 1, 64);
+        if (lane == 0) {
+            if (tile == 0) {
+                cprev = ld_wt_d(&scr->c_left);
+            } else {
+                const SpecialOut q = ld_wt_struct(&spec_go[bf0 - 1]);
+                cprev = q.cs + (double)(bk0 - q.P) * ldexp(1.0, q.E - 52);
+            }
+        }
+        int64_t sj = positions_upto(cprev, n_global, pc.rstep, ofs);
+        const int64_t j0 = tile * kWaveTile + 8 * lane;
+#pragma unroll
+        for (int k = 0; k < kScanPer; ++k) {
+            const int64_t j = j0 + k;
+            int64_t ej = sj;
+            if (j < n) {
+                ej = positions_upto(out[k], n_global, pc.rstep, ofs);
+                if (gbase + j == n_global - 1) {
+                    if (ej < n_global) atomicOr(&flags[kFlagStatus], 1);   // IndexError in the reference
+                    ej = n_global;
+                }
+            }
+            lv[k] = sj;
+            hv[k] = ej;
+            cnt += (ej > sj) ? 1 : 0;
+            sj = ej;
+        }
+        // per destination: selected sources entirely before its positions / overlapping them
+        for (int d = 0; d < P.world; ++d) {
+            int32_t cb = 0, cc = 0;
+#pragma unroll
+            for (int k = 0; k < kScanPer; ++k) {
+                if (hv[k] > lv[k]) {
+                    if (hv[k] <= P.gb[d]) ++cb;
+                    else if (lv[k] < P.gb[d + 1]) ++cc;
+                }
+            }
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                cb += __shfl_xor(cb, o, 64);
+                cc += __shfl_xor(cc, o, 64);
+            }
+            if (lane == 0) {
+                if (cb) atomicAdd(&s_cb[d], cb);
+                if (cc) atomicAdd(&s_cc[d], cc);
+            }
+        }
+    }
+    __shared__ int32_t shs[kScanThreads / 64 + 1];
+    int32_t tot;
+    const int32_t cex = block_excl_scan<int32_t, kScanThreads>(cnt, shs, tot);   // (barriers publish s_cb / s_cc)
+    // the block's counts per destination (bdst[b][2 d + {0, 1}]): no contended atomics
+    if ((int)threadIdx.x < 2 * P.world) {
+        const int d = threadIdx.x >> 1;
+        st_wt_i(&bdst[(int64_t)blockIdx.x * 2 * kDistMaxWorld + threadIdx.x],
+                (threadIdx.x & 1) ? s_cc[d] : s_cb[d]);
+    }
+    if (threadIdx.x == 0) st_wt_i(&bsel[blockIdx.x], tot);
+    PROBE_MAX(23);
+    if (arrive_last(tk + kTicketWords)) {
+        __shared__ int32_t shs2[kScanThreads / 64 + 1];
+        block_scan_array<int32_t, kScanThreads>(bsel, bsel_off, gridDim.x, nullptr, shs2, true);
+        // dbase / dcnt: the per-destination counts summed over the blocks (a
+        // wave per destination pair, lanes striding over the blocks)
+        for (int e = wave; e < 2 * P.world; e += kScanThreads / 64) {
+            int64_t a = 0;
+            for (int b = lane; b < (int)gridDim.x; b += 64)
+                a += ld_wt_i(&bdst[(int64_t)b * 2 * kDistMaxWorld + e]);
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) a += __shfl_xor(a, o, 64);
+            if (lane == 0) st_wt((e & 1) ? (void*)&scr->dcnt[e >> 1] : (void*)&scr->dbase[e >> 1], (uint64_t)a);
+        }
+        dist_token_release(&scr->rel[1], tokB);
+        PROBE_AT(24);
+    } else {
+        dist_token_wait(&scr->rel[1], tokB, flags);
+    }
+    PROBE_MAX(14);
+    __shared__ int64_t s_dbase[kDistMaxWorld];
+    __shared__ int64_t s_ps0;
+    if ((int)threadIdx.x < P.world) s_dbase[threadIdx.x] = (int64_t)ld_wt(&scr->dbase[threadIdx.x]);
+    if (threadIdx.x == 0) s_ps0 = ld_wt_i(&bsel_off[blockIdx.x]);
+#ifdef SLAM_PROBE
+    if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0)
+        g_probe[15] = (unsigned long long)(ld_wt_i(&bsel_off[blockIdx.x]) + tot);
+#endif
+    __syncthreads();
+    PROBE_MAX(12);
+    // ---- C: items to every destination
+    if (active) {
+        int64_t ps = s_ps0 + cex;
+        const int64_t j0 = tile * kWaveTile + 8 * lane;
+#pragma unroll
+        for (int k = 0; k < kScanPer; ++k) {
+            if (hv[k] > lv[k]) {
+                const int64_t j = j0 + k, lo = lv[k], h = hv[k];
+                const double x = xs[j], y = ys[j], th = ts[j];
+                for (int d = dist_owner(P, lo); d < P.world && P.gb[d] < h; ++d) {
+                    const int64_t slot = ps - s_dbase[d];
+                    if (slot >= 0 && slot < P.L.cap_item)
+                        dist_store_item(P, d, slot, x, y, th, lo > P.gb[d] ? lo : P.gb[d],
+                                        h < P.gb[d + 1] ? h : P.gb[d + 1]);
+                    else atomicOr(&flags[kFlagStatus], kDistStItems);
+                }
+                ++ps;
+            }
+        }
+    }
+    PROBE_MAX(25);
+    if (!arrive_last(tk + 2 * kTicketWords)) return;       // (drains this block's item stores)
+    if ((int)threadIdx.x < P.world) {
+        int64_t* hdr = reinterpret_cast<int64_t*>(P.base[threadIdx.x] + P.L.item_hdr) + 2 * P.rank;
+        hdr[0] = (int64_t)ld_wt(&scr->dcnt[threadIdx.x]);
+    }
+    __syncthreads();
+    dist_signal(P, kXItem, epoch);
+    PROBE_AT(26);
 }
 
 // ---------------------------------------------------------------- record
@@ -560,6 +999,7 @@ __device__ __forceinline__ void dist_record(const int64_t n, const DeferParts& d
         if (part == 0 && c < nfull) sh[c] = v;
     }
     __syncthreads();
+    PROBE_AT(0);
     double M = s_wm[0];
 #pragma unroll
     for (int w = 1; w < kFinWaves; ++w) M = fmax(M, s_wm[w]);
@@ -591,6 +1031,7 @@ __device__ __forceinline__ void dist_record(const int64_t n, const DeferParts& d
             if (dp.pmax[b] == M) mb = (unsigned long long)b;
         if (mb != ~0ull) atomicMin(&s_mblk, mb);
     }
+    PROBE_AT(1);
     unsigned long long prev = 0;                            // candidates must be >= prev
     for (int r = 0; r < kDistWin; ++r) {
         unsigned long long cb = ~0ull;
@@ -610,6 +1051,7 @@ __device__ __forceinline__ void dist_record(const int64_t n, const DeferParts& d
         prev = got + 1;
     }
     __syncthreads();
+    PROBE_AT(2);
     if (tid < 12) {
         double r = s_red[tid][0];
 #pragma unroll
@@ -633,33 +1075,41 @@ __device__ __forceinline__ void dist_record(const int64_t n, const DeferParts& d
     }
     __syncthreads();
     // ---- tie window: the first kDistWin elements (index order) with w_un >= thr,
-    // from the candidate blocks (usually one element: M)
-    if (M > 0.0 && wave == 0) {
-        int64_t cnt = 0;
-        for (int r = 0; r < kDistWin && cnt < kDistWin; ++r) {
+    // from the candidate blocks (usually one element: M) -- one element per lane,
+    // a candidate block per round (block-uniform loop)
+    PROBE_AT(3);
+    static_assert(kFinThreads == kPartPer, "one lane per element of a fused block");
+    {
+        __shared__ int s_wh[kFinWaves];
+        int cnt = 0;
+        for (int r = 0; r < kDistWin && cnt < kDistWin && M > 0.0; ++r) {
             const unsigned long long cb = s_cand[r];
             if (cb == ~0ull) break;
-            const int64_t b = (int64_t)cb;
-            for (int e0 = 0; e0 < kPartPer && cnt < kDistWin; e0 += 64) {
-                const int64_t i = b * kPartPer + e0 + lane;
-                const double v = (i < n) ? w_un[i] : -1.0;
-                unsigned long long hit = __ballot(v >= thr);
-                while (hit && cnt < kDistWin) {
-                    const int l = __ffsll((long long)hit) - 1;
-                    hit &= hit - 1;
-                    if (lane == l) {
-                        DistWin& wv = rec.win[cnt];
-                        wv.idx = gbase + i;
-                        wv.v = v;
-                        wv.x[0] = xs[i];
-                        wv.x[1] = ys[i];
-                        wv.x[2] = ts[i];
-                    }
-                    ++cnt;
-                }
+            const int64_t i = (int64_t)cb * kPartPer + tid;
+            const double v = (i < n) ? w_un[i] : -1.0;
+            const bool hit = v >= thr;
+            const unsigned long long bal = __ballot(hit);
+            if (lane == 0) s_wh[wave] = __popcll(bal);
+            __syncthreads();
+            int before = 0, tot = 0;
+#pragma unroll
+            for (int w = 0; w < kFinWaves; ++w) {
+                before += (w < wave) ? s_wh[w] : 0;
+                tot += s_wh[w];
             }
+            const int rank = cnt + before + __popcll(bal & ((1ull << lane) - 1ull));
+            if (hit && rank < kDistWin) {
+                DistWin& wv = rec.win[rank];
+                wv.idx = gbase + i;
+                wv.v = v;
+                wv.x[0] = xs[i];
+                wv.x[1] = ys[i];
+                wv.x[2] = ts[i];
+            }
+            cnt += tot;
+            __syncthreads();                                // s_wh reused
         }
-        if (lane == 0) rec.nwin = cnt;
+        if (tid == 0) rec.nwin = cnt < kDistWin ? cnt : kDistWin;
     }
     __syncthreads();
     if (tid == 0) {
@@ -679,6 +1129,7 @@ __device__ __forceinline__ void dist_record(const int64_t n, const DeferParts& d
     }
     __syncthreads();
     // ---- push into every peer's slot (parity = epoch & 1)
+    PROBE_AT(28);
     const int64_t words = (int64_t)sizeof(DistRec) / 8;
     for (int qq = 0; qq < P.world; ++qq) {
         char* slot = P.base[qq] + P.L.g1 + ((int64_t)(epoch & 1) * P.world + P.rank) * P.L.rec_stride;
@@ -690,6 +1141,7 @@ __device__ __forceinline__ void dist_record(const int64_t n, const DeferParts& d
     }
     __syncthreads();
     dist_signal(P, kXG1, epoch);
+    PROBE_AT(29);
 }
 
 // ---------------------------------------------------------------- finalize
@@ -715,6 +1167,7 @@ __device__ __forceinline__ void dist_finalize(const int64_t n, const DeferParts&
     const int tid = threadIdx.x;
     __shared__ DistRec s_rec[kDistMaxWorld];
     dist_wait(P, kXG1, epoch, flags);
+    PROBE_AT(30);
     const char* g1 = P.base[P.rank] + P.L.g1 + (int64_t)(epoch & 1) * P.world * P.L.rec_stride;
     auto rec_of = [&](int q) { return reinterpret_cast<const DistRec*>(g1 + (int64_t)q * P.L.rec_stride); };
     {   // every rank's record into LDS (one parallel round of system-scope loads)
@@ -864,12 +1317,14 @@ __global__ __launch_bounds__(kFinThreads) void dist_reduce_kernel(
     const DistPeers P) {
     __shared__ double sh[2048];                             // buffer partials (nch <= 2048)
     const uint64_t epoch = dist_epoch(io);
+    PROBE_AT(27);
     if (RECORD)
         dist_record(n, dp, w_un, tail_leaves, tail_ops, n_tail_leaves, n_tail_ops, xs, ys, ts, P,
                     epoch, sh);
     if (FINALIZE) {
         if (RECORD) __syncthreads();
         dist_finalize(n, dp, s_cur, refp, flags, ess_th, io, np_recip, boff, scr, P, epoch, sh);
+        PROBE_AT(31);
     }
 }
 

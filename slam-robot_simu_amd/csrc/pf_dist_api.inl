@@ -22,11 +22,14 @@ struct slam_dist {
     std::vector<SpecialOut*> spec_go;
     std::vector<int64_t*> hi;
     std::vector<int32_t*> bsel, bsel_off;
+    std::vector<int32_t*> bdst;               // [nb_scan][2 kDistMaxWorld] per-block destination counts
     std::vector<unsigned*> tk;                // 4 ticket blocks per held shard
     std::vector<void*> dallocs;
     std::vector<void*> opened;                // IPC mappings of peer regions
     hipStream_t stream = nullptr;             // LOCAL: the shared stream
     bool connected = false;
+    bool merged = false;                      // one-launch resample exchange (one held shard, co-resident grid)
+    bool merged_ok = false;
     hipGraphExec_t graph[2] = {nullptr, nullptr};     // kGraphSteps steps per parity
     hipGraphExec_t graph1[2] = {nullptr, nullptr};    // one step per parity
 };
@@ -51,7 +54,17 @@ void dist_drop_graphs(slam_dist* d) {
 // every phase of one step, phase-major across the held shards
 int dist_enqueue_step(slam_dist* d) {
     const int m = d->nloc;
-    for (int i = 0; i < m; ++i) {                         // exact cumsum: classify
+    if (d->merged) {                                      // the resample exchange in one launch
+        slam_pf* h = d->sh[0];
+        const double delta = 4.0 * (double)h->n_global * 0x1p-53 + 0x1p-45;
+        const int c = h->cur;
+        dist_resample_merged_kernel<<<h->nb_scan, kScanThreads, 0, h->stream>>>(
+            h->w_un, h->s_cur, h->pc.np_recip, h->n, h->boff, delta, h->stage, h->bk, h->bf,
+            h->boffk, h->bofff, h->ktot, h->nspec, d->tk[0], h->flags, d->spec_go[0], d->scr[0],
+            d->bsel[0], d->bsel_off[0], d->bdst[0], h->x[c], h->y[c], h->th[c], d->peers[0],
+            step_io(h), h->pc, h->cfg.seed, h->nb_part);
+    }
+    for (int i = 0; i < m && !d->merged; ++i) {           // exact cumsum: classify
         slam_pf* h = d->sh[i];
         const double delta = 4.0 * (double)h->n_global * 0x1p-53 + 0x1p-45;
         scan_classify_kernel<<<h->nb_scan, kScanThreads, 0, h->stream>>>(
@@ -59,26 +72,26 @@ int dist_enqueue_step(slam_dist* d) {
             h->boffk, h->bofff, h->ktot, h->nspec, delta, h->gbase, h->tk + 2 * kTicketWords,
             h->flags, 0, h->s_cur, h->pc.np_recip, kPartPer);
     }
-    for (int i = 0; i < m; ++i) {                         // emit + push specials
+    for (int i = 0; i < m && !d->merged; ++i) {           // emit + push specials
         slam_pf* h = d->sh[i];
         dist_emit_push_kernel<<<h->nb_scan, kScanThreads, 0, h->stream>>>(
             h->w_un, h->s_cur, h->pc.np_recip, h->n, h->c, h->kincl, h->fexcl, h->boffk, h->bofff,
             h->spec_in, h->gbase, h->nspec, h->ktot, d->tk[i], h->flags, d->peers[i], step_io(h));
     }
-    for (int i = 0; i < m; ++i) {                         // fold (waits for the specials)
+    for (int i = 0; i < m && !d->merged; ++i) {           // fold (waits for the specials)
         slam_pf* h = d->sh[i];
         dist_fold_kernel<<<1, 256, 0, h->stream>>>(d->spec_g[i], d->spec_go[i], h->n_global,
                                                    h->flags, d->scr[i], d->peers[i], step_io(h),
                                                    h->pc.rstep, h->pc.np_recip, h->cfg.seed);
     }
-    for (int i = 0; i < m; ++i) {                         // expand + hi + counts
+    for (int i = 0; i < m && !d->merged; ++i) {           // expand + hi + counts
         slam_pf* h = d->sh[i];
         dist_expand_hi_kernel<<<h->nb_scan, kScanThreads, 0, h->stream>>>(
             h->n, h->kincl, h->fexcl, h->boffk, h->bofff, d->spec_go[i], h->c, d->hi[i], d->bsel[i],
             d->bsel_off[i], d->tk[i] + kTicketWords, h->flags, d->scr[i], d->peers[i], step_io(h),
             h->n_global, h->pc.rstep, h->pc.np_recip, h->cfg.seed);
     }
-    for (int i = 0; i < m; ++i) {                         // pack + push items
+    for (int i = 0; i < m && !d->merged; ++i) {           // pack + push items
         slam_pf* h = d->sh[i];
         const int c = h->cur;
         dist_pack_push_kernel<<<h->nb_scan, kScanThreads, 0, h->stream>>>(
@@ -207,7 +220,7 @@ int slam_dist_create(slam_pf** shards, int32_t n_held, int32_t world, int32_t ra
     L.spec_hdr = take(16 * world);
     L.spec = take((int64_t)sizeof(SpecialIn) * L.cap_spec * world);
     L.item_hdr = take(16 * world);
-    L.item = take((int64_t)sizeof(ShardItem) * L.cap_item * world);
+    L.item = take((int64_t)sizeof(DistItem) * L.cap_item * world);
     L.total = off;
     int rc;
     if (d->local) {
@@ -222,7 +235,7 @@ int slam_dist_create(slam_pf** shards, int32_t n_held, int32_t world, int32_t ra
             return bail(fail(SLAM_ERR_HIP, "slam_dist_create: fine-grained exchange region allocation failed"));
         d->xbuf.push_back((char*)xb);
         SLAM_HIP_TRY(hipMemset(xb, 0, (size_t)L.flags + 3 * kDistMaxWorld * 8));
-        void *p1, *p2, *p3, *p4, *p5, *p6, *p7;
+        void *p1, *p2, *p3, *p4, *p5, *p6, *p7, *p8, *p9;
         const int32_t nbs = h->nb_scan;
         if ((rc = dist_alloc(d, &p1, sizeof(DistScratch))) ||
             (rc = dist_alloc(d, &p2, sizeof(SpecialIn) * (size_t)std::max<int64_t>(N, 1))) ||
@@ -230,7 +243,9 @@ int slam_dist_create(slam_pf** shards, int32_t n_held, int32_t world, int32_t ra
             (rc = dist_alloc(d, &p4, sizeof(int64_t) * (size_t)h->n)) ||
             (rc = dist_alloc(d, &p5, sizeof(int32_t) * (size_t)nbs)) ||
             (rc = dist_alloc(d, &p6, sizeof(int32_t) * (size_t)nbs)) ||
-            (rc = dist_alloc(d, &p7, sizeof(unsigned) * 4 * kTicketWords)))
+            (rc = dist_alloc(d, &p7, sizeof(unsigned) * 4 * kTicketWords)) ||
+            (rc = dist_alloc(d, &p8, sizeof(DistItem) * (size_t)L.cap_item)) ||
+            (rc = dist_alloc(d, &p9, sizeof(int32_t) * 2 * kDistMaxWorld * (size_t)nbs)))
             return bail(rc);
         SLAM_HIP_TRY(hipMemset(p1, 0, sizeof(DistScratch)));
         SLAM_HIP_TRY(hipMemset(p7, 0, sizeof(unsigned) * 4 * kTicketWords));
@@ -241,10 +256,12 @@ int slam_dist_create(slam_pf** shards, int32_t n_held, int32_t world, int32_t ra
         d->bsel.push_back((int32_t*)p5);
         d->bsel_off.push_back((int32_t*)p6);
         d->tk.push_back((unsigned*)p7);
+        d->bdst.push_back((int32_t*)p9);
         DistPeers P{};
         P.world = world;
         P.rank = rank0 + i;
         P.L = L;
+        P.self_items = (DistItem*)p8;
         d->peers.push_back(P);
     }
     // shard bases.  LOCAL: the handles'.  One shard per process: the standard
@@ -263,6 +280,19 @@ int slam_dist_create(slam_pf** shards, int32_t n_held, int32_t world, int32_t ra
             return bail(fail(SLAM_ERR_ARG, "slam_dist_create: shard is not slam_dist_shard_range's for its rank"));
     }
     gb[world] = N;
+    {
+        // one held shard: the resample exchange in one launch when its grid is
+        // co-resident (its blocks wait for the last one twice); SLAM_DIST_MERGED=0
+        // keeps the five-launch form
+        int per_cu = 0, cus = 0;
+        const char* ev = std::getenv("SLAM_DIST_MERGED");
+        if (n_held == 1 && !(ev && ev[0] == '0') &&
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, dist_resample_merged_kernel,
+                                                         kScanThreads, 0) == hipSuccess &&
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, d->device) == hipSuccess)
+            d->merged_ok = (int64_t)d->sh[0]->nb_scan <= (int64_t)per_cu * cus / 2;
+        d->merged = d->merged_ok;
+    }
     for (auto& P : d->peers)
         for (int q = 0; q <= world; ++q) P.gb[q] = gb[q];
     SLAM_HIP_TRY(hipDeviceSynchronize());
@@ -356,6 +386,19 @@ int slam_dist_destroy(slam_dist* d) {
 // One step of every held shard (device RNG noise and resample offset; the
 // observations of this step staged in slot 0).  res: the global result
 // (identical on every rank).
+// one-launch (1) or five-launch (0) resample exchange; reports the form in use
+int slam_dist_set_merged(slam_dist* d, int32_t on, int32_t* active) {
+    SLAM_ARG_CHECK(d, "slam_dist_set_merged: NULL handle");
+    if (on >= 0) {
+        SLAM_ARG_CHECK(!on || d->merged_ok,
+                       "slam_dist_set_merged: needs one held shard with a co-resident scan grid");
+        if (d->merged != (on != 0)) dist_drop_graphs(d);
+        d->merged = on != 0;
+    }
+    if (active) *active = d->merged ? 1 : 0;
+    return SLAM_OK;
+}
+
 int slam_dist_step(slam_dist* d, const double* control, const double* z, slam_pf_result* res) {
     SLAM_ARG_CHECK(d && control && d->connected, "slam_dist_step: bad argument or not connected");
     SLAM_HIP_TRY(hipSetDevice(d->device));

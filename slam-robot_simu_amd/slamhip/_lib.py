@@ -111,6 +111,7 @@ SIGNATURES = {
     "slam_dist_step": (C.c_int, [_P, _D, _D, C.POINTER(PFResult)]),
     "slam_dist_load_observations": (C.c_int, [_P, C.c_int32, _D]),
     "slam_dist_run": (C.c_int, [_P, C.c_int32, C.c_int32, _D, C.POINTER(PFResult)]),
+    "slam_dist_set_merged": (C.c_int, [_P, C.c_int32, C.POINTER(C.c_int32)]),
     "slam_pf_create_shard": (C.c_int, [C.POINTER(PFConfig), C.c_int64, C.c_int64, C.c_int64,
                                        C.c_int32, _D, C.c_int, C.POINTER(_P)]),
     "slam_pf_shard_sizes": (C.c_int, [_P, _I64]),

@@ -150,6 +150,14 @@ class DistFilter:
         self.resample_next = bool(res[k - 1].resample_next)
         return [DeviceParticleFilter._res(r) for r in res] if want_results else None
 
+    def set_merged(self, on=None):
+        """Resample exchange in one launch (True) or five (False); None only
+        reports.  Returns the form in use."""
+        act = C.c_int32(0)
+        check(self._lib.slam_dist_set_merged(self._d, -1 if on is None else int(bool(on)),
+                                             C.byref(act)), "slam_dist_set_merged")
+        return bool(act.value)
+
     def enable_timing(self, on=True):
         """HIP events around the fused kernel of every held shard (disables graphs)."""
         for h, _, _ in self._shards:

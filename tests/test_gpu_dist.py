@@ -94,6 +94,35 @@ def test_dist_local_graph_run_matches_single():
         single.close()
 
 
+@pytest.mark.parametrize("merged", [True, False])
+def test_dist_one_shard_resample_forms_match_single(merged):
+    """One held shard (the bench's N = 1 sharded form, and one process per GPU):
+    the resample exchange in one launch (dist_resample_merged_kernel) and in
+    five, against one handle -- at the bench size, replayed as hipGraphs."""
+    from slamhip.dist import DistFilter
+    from slamhip.pf import DeviceParticleFilter
+    n, nl, steps = 1 << 20, 100, 20
+    lm, zs, p = _world(n, nl, steps, 17)
+    ctl = np.tile([p.vel, p.omega], (steps, 1))
+    single = DeviceParticleFilter(n, lm, motion="velocity", likelihood="logsum", seed=13)
+    dist = DistFilter(n, lm, world=1, motion="velocity", likelihood="logsum", seed=13)
+    try:
+        assert dist.set_merged(None)                 # the default where the grid fits
+        assert dist.set_merged(merged) == merged
+        single.load_observations(zs)
+        dist.load_observations(zs)
+        ra = single.run(0, ctl[:3]) + single.run(3, ctl[3:])
+        rb = dist.run(0, ctl[:3]) + dist.run(3, ctl[3:])
+        for k, (a, b) in enumerate(zip(ra, rb)):
+            _same(a, b, k)
+        assert sum(r["resampled"] for r in ra) >= 3
+        for u, v in zip(single.get_state(), dist.get_state()):
+            np.testing.assert_array_equal(u, v)
+    finally:
+        dist.close()
+        single.close()
+
+
 def test_comm_one_rank_rccl():
     """slam_comm over RCCL with one rank: the bootstrap all-gather, and a
     one-rank DistFilter connected through it."""
@@ -129,10 +158,11 @@ def _rank_main(rank, world, n, lm, zs, ctl, q_out, q_in, conn):
         d = DistFilter(n, lm, world=world, rank=rank, all_gather=all_gather, motion="velocity",
                        likelihood="logsum", seed=8)
         d.load_observations(zs)
+        merged = d.set_merged(None)
         res = d.run(0, ctl)
         st = d.get_state()
         d.close()
-        q_out.put((rank, [(r["max_idx"], r["weight_sum"], r["resampled"]) for r in res], st))
+        q_out.put((rank, [(r["max_idx"], r["weight_sum"], r["resampled"]) for r in res], st + (merged,)))
     except Exception as e:              # reported to the parent
         q_out.put((rank, repr(e), None))
 
@@ -174,7 +204,8 @@ def test_dist_two_processes_share_one_gpu():
         ref = single.run(0, ctl)
         xs = single.get_state()
     for rank in range(world):
-        res, _ = out[rank]
+        res, st = out[rank]
+        assert st[4], "one shard per process: the one-launch resample exchange"
         assert [(r["max_idx"], r["weight_sum"], r["resampled"]) for r in ref] == res
     for k in range(4):
         np.testing.assert_array_equal(np.concatenate([out[0][1][k], out[1][1][k]]), xs[k])

@@ -55,7 +55,7 @@ def main(src, tag):
             rec["fp64_flops"] = 64 * (d[f64[0]] + d[f64[1]] + d[f64[3]] + 2 * d[f64[2]])
         if "SQ_INSTS_VALU" in d and "SQ_WAVES" in d and d["SQ_WAVES"]:
             rec["valu_insts_per_wave"] = d["SQ_INSTS_VALU"] / d["SQ_WAVES"]
-        out[short(name) + ("" if "<" not in name else name[name.index("<"):name.index(">") + 1])] = rec
+        out[short(name)] = rec
     os.makedirs("profiles", exist_ok=True)
     with open(f"profiles/{tag}_pmc.json", "w") as f:
         json.dump(out, f, indent=1, sort_keys=True)
