@@ -3,15 +3,19 @@
 // TrajectoryEstimator (graph_based_slam.py:330-581) -> slam_graph_*.  The
 // block structure of H and the per-block accumulation plan (which edge parts
 // land in which 3x3 block, in the reference's edge order) are built on the
-// host once per edge set; every Gauss-Newton iteration then runs entirely on
-// the device: linearise -> assemble -> solve -> pose update.
+// device once per edge set (graph_build.inl: radix sorts, uniques, binary
+// searches; SLAM_GRAPH_HOST_BUILD=1 builds the same arrays on the host, for
+// the tests); every Gauss-Newton iteration then runs entirely on the device:
+// linearise -> assemble -> solve -> pose update.
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <limits>
 #include <vector>
 
 #include "graph_kernels.inl"
+#include "graph_build.inl"
 
 using namespace slam;
 
@@ -19,7 +23,10 @@ struct slam_graph {
     slam_graph_config cfg;
     int device = 0;
     hipStream_t stream = nullptr;
-    std::vector<void*> allocs;     // per edge-set / per pose-set buffers
+    std::vector<void*> allocs;     // dense-path buffers (per edge set, small systems only)
+    void* arena = nullptr;         // structure + solver buffers of the edge set (grow-only)
+    size_t arena_bytes = 0;
+    int64_t dense_n = 0;           // unknowns the dense buffers were sized for
     // poses
     int64_t T = 0;
     double* poses = nullptr;
@@ -79,7 +86,202 @@ int upload(slam_graph* h, T* dst, const std::vector<T>& src) {
 
 unsigned nblk(int64_t n, int t = 256) { return (unsigned)((n + t - 1) / t); }
 
-int build_structure(slam_graph* h, int64_t E, const slam_graph_edge* ed) {
+// carve 256-byte aligned arrays out of one allocation
+struct Carver {
+    char* base;
+    size_t off = 0;
+    template <typename T>
+    T* take(int64_t count) {
+        T* p = reinterpret_cast<T*>(base ? base + off : nullptr);
+        off += ((size_t)std::max<int64_t>(count, 1) * sizeof(T) + 255) / 256 * 256;
+        return p;
+    }
+};
+
+// the edge set's device arrays, sized by the upper bounds nt <= min(2E, T) and
+// slots <= 2E + nt (carve twice: sizes, then pointers); one allocation reused
+// while it is large enough
+struct BuildScratch {
+    int64_t *tl, *tl_s, *keys, *keys_s, *ukeys, *rb, *ra, *sl, *sl_s, *cval, *bkey, *bkey_s, *bval;
+    int64_t* cnt;                  // [0] nt, [1] slots
+    void* tmp;
+    size_t tmp_bytes;
+};
+
+int carve_edge_set(slam_graph* h, int64_t E, int64_t nt_ub, size_t tmp_bytes, BuildScratch* bs) {
+    const int64_t K = 2 * E + nt_ub;
+    const int64_t n = 3 * nt_ub;
+    for (int pass = 0; pass < 2; ++pass) {
+        Carver c{pass ? (char*)h->arena : nullptr};
+        h->edges = c.take<slam_graph_edge>(E);
+        h->blocks = c.take<double>(42 * E);
+        h->times = c.take<int64_t>(nt_ub);
+        h->srow = c.take<int64_t>(K);
+        h->scol = c.take<int64_t>(K);
+        h->rptr = c.take<int64_t>(nt_ub + 1);
+        h->cptr = c.take<int64_t>(K + 1);
+        h->clist = c.take<int64_t>(4 * E);
+        h->bptr = c.take<int64_t>(nt_ub + 1);
+        h->blist = c.take<int64_t>(2 * E);
+        h->dslot = c.take<int64_t>(nt_ub);
+        h->val = c.take<double>(9 * K);
+        h->b = c.take<double>(n);
+        h->delta = c.take<double>(n);
+        h->dsum = c.take<double>(1);
+        h->minv = c.take<double>(9 * nt_ub);
+        h->r = c.take<double>(n);
+        h->z = c.take<double>(n);
+        h->p = c.take<double>(n);
+        h->q = c.take<double>(n);
+        h->part = c.take<double>(3 * (int64_t)nblk(n, kPcgThreads) + 3);
+        h->st = c.take<PcgState>(1);
+        h->luout = c.take<double>(8);
+        if (bs) {
+            bs->tl = c.take<int64_t>(2 * E);
+            bs->tl_s = c.take<int64_t>(2 * E);
+            bs->keys = c.take<int64_t>(K);
+            bs->keys_s = c.take<int64_t>(K);
+            bs->ukeys = c.take<int64_t>(K);
+            bs->rb = c.take<int64_t>(E);
+            bs->ra = c.take<int64_t>(E);
+            bs->sl = c.take<int64_t>(4 * E);
+            bs->sl_s = c.take<int64_t>(4 * E);
+            bs->cval = c.take<int64_t>(4 * E);
+            bs->bkey = c.take<int64_t>(2 * E);
+            bs->bkey_s = c.take<int64_t>(2 * E);
+            bs->bval = c.take<int64_t>(2 * E);
+            bs->cnt = c.take<int64_t>(2);
+            bs->tmp = c.take<char>((int64_t)tmp_bytes);
+            bs->tmp_bytes = tmp_bytes;
+        }
+        if (pass == 0 && c.off > h->arena_bytes) {
+            if (h->arena) SLAM_HIP_TRY(hipFree(h->arena));
+            h->arena = nullptr;
+            h->arena_bytes = 0;
+            SLAM_HIP_TRY(hipMalloc(&h->arena, c.off + c.off / 4));
+            h->arena_bytes = c.off + c.off / 4;
+        }
+    }
+    return SLAM_OK;
+}
+
+// dense-path buffers (n = 3 nt <= kGraphDenseMax), grow-only
+int dense_buffers(slam_graph* h, int64_t n) {
+    if (n > kGraphDenseMax) return SLAM_OK;
+    if (n <= h->dense_n && h->A) return SLAM_OK;
+    free_list(h->allocs);
+    GTRY(galloc(h, &h->A, n * n));
+    GTRY(galloc(h, &h->LU, n * n));
+    GTRY(galloc(h, &h->S, n * n));
+    GTRY(galloc(h, &h->V, n * (n + 1)));
+    GTRY(galloc(h, &h->lan, 3 * n + 8));
+    GTRY(galloc(h, &h->piv, n));
+    h->dense_n = n;
+    return SLAM_OK;
+}
+
+int finish_structure(slam_graph* h, int64_t E, int64_t nt, int64_t ns) {
+    h->E = E;
+    h->pcg_last_iters = 0;
+    h->nt = nt;
+    h->n_slots = ns;
+    const int64_t n = 3 * nt;
+    if (n <= kGraphDenseMax) {
+        GTRY(dense_buffers(h, n));
+    } else {
+        free_list(h->allocs);
+        h->A = h->LU = h->S = h->V = h->lan = nullptr;
+        h->piv = nullptr;
+        h->dense_n = 0;
+    }
+    return SLAM_OK;
+}
+
+// the structure on the device (graph_build.inl)
+int build_structure_device(slam_graph* h, int64_t E, const slam_graph_edge* ed) {
+    const int64_t nt_ub = std::min<int64_t>(2 * E, h->T);
+    const int64_t K = 2 * E + nt_ub;
+    const int tbits = bits_for((uint64_t)h->T);
+    const int sbits = bits_for((uint64_t)K);
+    hipStream_t s = h->stream;
+    // temporary storage of the largest rocPRIM call
+    size_t tb = 0, t1 = 0;
+    int64_t* np = nullptr;
+    auto q = [&](hipError_t e) { return e == hipSuccess; };
+    if (!q(rocprim::radix_sort_keys(nullptr, t1, np, np, (size_t)(2 * E), 0, tbits, s))) goto qfail;
+    tb = std::max(tb, t1);
+    if (!q(rocprim::unique(nullptr, t1, np, np, np, (size_t)(2 * E), rocprim::equal_to<int64_t>(), s)))
+        goto qfail;
+    tb = std::max(tb, t1);
+    if (!q(rocprim::radix_sort_keys(nullptr, t1, np, np, (size_t)K, 0, 64, s))) goto qfail;
+    tb = std::max(tb, t1);
+    if (!q(rocprim::unique(nullptr, t1, np, np, np, (size_t)K, rocprim::equal_to<int64_t>(), s))) goto qfail;
+    tb = std::max(tb, t1);
+    if (!q(rocprim::radix_sort_pairs(nullptr, t1, np, np, np, np, (size_t)(4 * E), 0, sbits, s)))
+        goto qfail;
+    tb = std::max(tb, t1);
+    if (!q(rocprim::radix_sort_pairs(nullptr, t1, np, np, np, np, (size_t)(2 * E), 0, tbits, s)))
+        goto qfail;
+    tb = std::max(tb, t1);
+    {
+        BuildScratch bs{};
+        GTRY(carve_edge_set(h, E, nt_ub, tb, &bs));
+        SLAM_HIP_TRY(hipMemcpyAsync(h->edges, ed, E * sizeof(slam_graph_edge), hipMemcpyHostToDevice, s));
+        // distinct times (:457-467 order)
+        hipLaunchKernelGGL(gb_times_kernel, dim3(nblk(E)), dim3(256), 0, s, E, h->edges, bs.tl);
+        size_t t = bs.tmp_bytes;
+        if (!q(rocprim::radix_sort_keys(bs.tmp, t, bs.tl, bs.tl_s, (size_t)(2 * E), 0, tbits, s))) goto rfail;
+        t = bs.tmp_bytes;
+        if (!q(rocprim::unique(bs.tmp, t, bs.tl_s, h->times, bs.cnt, (size_t)(2 * E),
+                               rocprim::equal_to<int64_t>(), s)))
+            goto rfail;
+        // slots of H: unique sorted keys r nt + c
+        hipLaunchKernelGGL(gb_keys_kernel, dim3(nblk(std::max(E, nt_ub))), dim3(256), 0, s, E, h->edges,
+                           h->times, bs.cnt, nt_ub, bs.rb, bs.ra, bs.keys, bs.bkey, bs.bval);
+        t = bs.tmp_bytes;
+        if (!q(rocprim::radix_sort_keys(bs.tmp, t, bs.keys, bs.keys_s, (size_t)K, 0, 64, s))) goto rfail;
+        t = bs.tmp_bytes;
+        if (!q(rocprim::unique(bs.tmp, t, bs.keys_s, bs.ukeys, bs.cnt + 1, (size_t)K,
+                               rocprim::equal_to<int64_t>(), s)))
+            goto rfail;
+        hipLaunchKernelGGL(gb_count_kernel, dim3(1), dim3(1), 0, s, bs.ukeys, bs.cnt + 1);
+        hipLaunchKernelGGL(gb_slots_kernel, dim3(nblk(std::max(K, nt_ub + 1))), dim3(256), 0, s, bs.ukeys,
+                           bs.cnt + 1, bs.cnt, nt_ub + 1, h->srow, h->scol, h->dslot, h->rptr);
+        // H plan: edge parts grouped by slot, edge order kept (stable sort)
+        hipLaunchKernelGGL(gb_parts_kernel, dim3(nblk(4 * E)), dim3(256), 0, s, E, bs.rb, bs.ra, bs.cnt,
+                           bs.ukeys, bs.cnt + 1, bs.sl, bs.cval);
+        t = bs.tmp_bytes;
+        if (!q(rocprim::radix_sort_pairs(bs.tmp, t, bs.sl, bs.sl_s, bs.cval, h->clist, (size_t)(4 * E), 0,
+                                         sbits, s)))
+            goto rfail;
+        hipLaunchKernelGGL(gb_offsets_kernel, dim3(nblk(K + 1)), dim3(256), 0, s, bs.sl_s, 4 * E,
+                           bs.cnt + 1, K + 1, h->cptr);
+        // b plan: (edge, side) grouped by row, edge order kept
+        t = bs.tmp_bytes;
+        if (!q(rocprim::radix_sort_pairs(bs.tmp, t, bs.bkey, bs.bkey_s, bs.bval, h->blist, (size_t)(2 * E),
+                                         0, tbits, s)))
+            goto rfail;
+        hipLaunchKernelGGL(gb_offsets_kernel, dim3(nblk(nt_ub + 1)), dim3(256), 0, s, bs.bkey_s, 2 * E,
+                           bs.cnt, nt_ub + 1, h->bptr);
+        SLAM_HIP_TRY(hipGetLastError());
+        int64_t cnt[2];
+        SLAM_HIP_TRY(hipMemcpyAsync(cnt, bs.cnt, sizeof(cnt), hipMemcpyDeviceToHost, s));
+        SLAM_HIP_TRY(hipStreamSynchronize(s));
+        h->times_h.resize(cnt[0]);
+        SLAM_HIP_TRY(hipMemcpyAsync(h->times_h.data(), h->times, cnt[0] * sizeof(int64_t),
+                                    hipMemcpyDeviceToHost, s));
+        GTRY(finish_structure(h, E, cnt[0], cnt[1]));
+        SLAM_HIP_TRY(hipStreamSynchronize(s));
+        return SLAM_OK;
+    }
+rfail:
+    return fail(SLAM_ERR_HIP, "graph structure build: rocPRIM call failed");
+qfail:
+    return fail(SLAM_ERR_HIP, "graph structure build: rocPRIM size query failed");
+}
+
+// the same arrays from a host pass (SLAM_GRAPH_HOST_BUILD=1; the tests compare the two)
+int build_structure_host(slam_graph* h, int64_t E, const slam_graph_edge* ed) {
     std::vector<int64_t> tl;
     tl.reserve(2 * E);
     for (int64_t e = 0; e < E; ++e) {
@@ -137,48 +339,10 @@ int build_structure(slam_graph* h, int64_t E, const slam_graph_edge* ed) {
         blist[bc[rb[e]]++] = 2 * e;
         blist[bc[ra[e]]++] = 2 * e + 1;
     }
-    // device buffers
-    free_list(h->allocs);
-    h->E = E;
-    h->pcg_last_iters = 0;
-    h->nt = nt;
-    h->n_slots = ns;
+    // device buffers (the same carve as the device build)
+    GTRY(carve_edge_set(h, E, std::min<int64_t>(2 * E, h->T), 0, nullptr));
     h->times_h = tl;
-    const int64_t n = 3 * nt;
-    GTRY(galloc(h, &h->edges, E));
-    GTRY(galloc(h, &h->blocks, 42 * E));
-    GTRY(galloc(h, &h->times, nt));
-    GTRY(galloc(h, &h->srow, ns));
-    GTRY(galloc(h, &h->scol, ns));
-    GTRY(galloc(h, &h->rptr, nt + 1));
-    GTRY(galloc(h, &h->cptr, ns + 1));
-    GTRY(galloc(h, &h->clist, 4 * E));
-    GTRY(galloc(h, &h->bptr, nt + 1));
-    GTRY(galloc(h, &h->blist, 2 * E));
-    GTRY(galloc(h, &h->dslot, nt));
-    GTRY(galloc(h, &h->val, 9 * ns));
-    GTRY(galloc(h, &h->b, n));
-    GTRY(galloc(h, &h->delta, n));
-    GTRY(galloc(h, &h->dsum, 1));
-    GTRY(galloc(h, &h->minv, 9 * nt));
-    GTRY(galloc(h, &h->r, n));
-    GTRY(galloc(h, &h->z, n));
-    GTRY(galloc(h, &h->p, n));
-    GTRY(galloc(h, &h->q, n));
-    GTRY(galloc(h, &h->part, 3 * (int64_t)nblk(n, kPcgThreads) + 3));
-    GTRY(galloc(h, &h->st, 1));
-    GTRY(galloc(h, &h->luout, 8));
-    if (n <= kGraphDenseMax) {
-        GTRY(galloc(h, &h->A, n * n));
-        GTRY(galloc(h, &h->LU, n * n));
-        GTRY(galloc(h, &h->S, n * n));
-        GTRY(galloc(h, &h->V, n * (n + 1)));
-        GTRY(galloc(h, &h->lan, 3 * n + 8));
-        GTRY(galloc(h, &h->piv, n));
-    } else {
-        h->A = h->LU = h->S = h->V = h->lan = nullptr;
-        h->piv = nullptr;
-    }
+    GTRY(finish_structure(h, E, nt, ns));
     SLAM_HIP_TRY(hipMemcpyAsync(h->edges, ed, E * sizeof(slam_graph_edge), hipMemcpyHostToDevice,
                                 h->stream));
     GTRY(upload(h, h->times, tl));
@@ -192,6 +356,12 @@ int build_structure(slam_graph* h, int64_t E, const slam_graph_edge* ed) {
     GTRY(upload(h, h->dslot, dslot));
     SLAM_HIP_TRY(hipStreamSynchronize(h->stream));
     return SLAM_OK;
+}
+
+int build_structure(slam_graph* h, int64_t E, const slam_graph_edge* ed) {
+    const char* hb = std::getenv("SLAM_GRAPH_HOST_BUILD");
+    if (hb && hb[0] == '1') return build_structure_host(h, E, ed);
+    return build_structure_device(h, E, ed);
 }
 
 GraphConst gconst(const slam_graph_config& c) { return GraphConst{c.r_dist, c.r_dir, c.r_orient}; }
@@ -357,6 +527,7 @@ int slam_graph_destroy(slam_graph* h) {
     if (!h) return SLAM_OK;
     (void)hipSetDevice(h->device);
     free_list(h->allocs);
+    if (h->arena) (void)hipFree(h->arena);
     if (h->poses) (void)hipFree(h->poses);
     for (auto& e : h->ev)
         if (e) (void)hipEventDestroy(e);
@@ -401,7 +572,6 @@ int slam_graph_set_edges(slam_graph* h, int64_t n_edges, const slam_graph_edge* 
     }
     SLAM_HIP_TRY(hipSetDevice(h->device));
     if (n_edges == 0) {
-        free_list(h->allocs);
         h->E = h->nt = h->n_slots = 0;
         h->times_h.clear();
         return SLAM_OK;
