@@ -399,6 +399,20 @@ int slam_graph_linearize_solve(const slam_graph_config* cfg, const slam_graph_ed
                                int64_t n_edges, double* poses, int64_t n_poses, double* stats,
                                int device);
 
+/* ====================================================================
+ * ScanSensor.scan (graph_based_slam.py:128-172) over poses x landmarks.
+ * yaw_cs[p] = (cos(yaw), sin(yaw), yaw) with yaw = BASE_ANG - theta_p (NumPy's
+ * values); tan_scan = tan(BASE_ANG - scan angle).  detect / obs are p-major
+ * [n_poses][n_landmarks] (flag; dist, dir, orient).  slam_scan_noise adds the
+ * reference's noise to n observations from 3n standard normals in its draw
+ * order (dist, dir, orient per detected landmark).
+ * ==================================================================== */
+int slam_scan_detect(int64_t n_poses, const double* poses, const double* yaw_cs, int64_t n_landmarks,
+                     const double* landmarks, double range, double tan_scan, int32_t* detect,
+                     double* obs, int device);
+int slam_scan_noise(int64_t n, const double* clean, const double* normals, double r_dist,
+                    double r_dir, double r_orient, double* out, int device);
+
 #ifdef __cplusplus
 }
 #endif

@@ -21,7 +21,7 @@ import itertools
 
 import numpy as np
 
-from pf_oracle import HALF_PI, wrap_angle
+from pf_oracle import HALF_PI, to_robot_frame, wrap_angle
 
 # graph_based_slam.py:604 -- Robot sets ScanSensor.setNoiseParam(5, 2, 2)
 R_DIST = 5 / 100
@@ -148,3 +148,28 @@ def update_est_pose(edges, poses):
             poses[t, 2] = wrap_angle(poses[t, 2] + delta[i * 3 + 2, 0])
         return np.array([1.0, float((delta.T @ delta)[0, 0]), det, cond]), poses, H, b[:, 0], times
     return np.array([0.0, 0.0, det, cond]), poses, H, b[:, 0], times
+
+
+def scan_sensor(pose, lm, scan_range, scan_angle, r_dist, r_dir, r_orient):
+    """ScanSensor.scan (graph_based_slam.py:128-172) for one pose (3,): the
+    detected landmark ids, the noise-free and the noisy (dist, dir, orient),
+    drawing from NumPy's global stream in the reference's order (three
+    np.random.normal calls per detected landmark, :163-165)."""
+    pose = np.asarray(pose, dtype=np.float64).reshape(3)
+    rl = to_robot_frame(pose, lm)                                  # :149
+    dist = np.linalg.norm(rl, axis=1)                              # :150
+    dirs = np.arctan2(rl[:, 1], rl[:, 0])                          # :151
+    orient = np.ones(rl.shape[0]) * (HALF_PI - pose[2])            # :152
+    scan_rad = HALF_PI - scan_angle                                # :155
+    det = [i for i in range(len(rl))
+           if dist[i] <= scan_range and rl[i, 1] >= np.absolute(rl[i, 0]) * np.tan(scan_rad)]
+    ids, clean, noisy = [], [], []
+    for i in det:
+        d = np.random.normal(dist[i], dist[i] * r_dist)
+        a = wrap_angle(np.random.normal(dirs[i], r_dir))
+        o = wrap_angle(np.random.normal(orient[i], r_orient))
+        ids.append(i)
+        clean.append([dist[i], dirs[i], orient[i]])
+        noisy.append([d, a, o])
+    return (np.array(ids, dtype=np.int64), np.array(clean).reshape(-1, 3),
+            np.array(noisy).reshape(-1, 3))

@@ -10,6 +10,12 @@ GPU (csrc/graph_kernels.inl), then writes the updated poses back into the
 caller's (3,1) arrays in place -- the reference mutates them in place too
 (:499-502), and its Robot relies on that aliasing.
 
+``ScanSensor`` (:78-213) is the sensor simulator: ``scan(pose)`` (and
+``scan_batch(poses)`` for many poses at once) computes the noise-free
+observations and the field-of-view test of every landmark on the GPU
+(csrc/sensor_api.hip) and adds the reference's noise from NumPy's global
+stream in the reference's draw order.
+
 ``estimate_trajectory(halves, n_landmarks)`` is Robot.estimateOpticalTrajectory
 (:685-715): all 2-combinations of each landmark's half-edges, then
 Gauss-Newton until sum(delta^2) < 0.01, with the poses resident on the GPU
@@ -18,9 +24,15 @@ between iterations.
 from __future__ import annotations
 
 
+import ctypes as C
+
 import numpy as np
 
+from slamhip import _lib
+from slamhip._lib import check, dptr
 from slamhip.graph import DeviceGraph, edge_array, pair_halves
+
+BASE_ANG = np.pi / 2.0       # mylib/transform.py:12
 
 DELTA_SUM_TH = 0.01          # graph_based_slam.py:662
 
@@ -42,6 +54,100 @@ class Observation:
 
     def getOrient(self):
         return self._or
+
+
+class ScanSensor(object):
+    """graph_based_slam.py:78-213: a fan-shaped scan sensor.  The noise
+    parameters are class-wide, as in the reference (setNoiseParam writes the
+    class attributes)."""
+
+    _R_Dist = 10 / 100                      # :85-87 defaults
+    _R_DirSigma = np.deg2rad(3.0)
+    _R_OrientSigma = np.deg2rad(3.0)
+
+    def __init__(self, aRange_m, aAngle_rad, aLandMarks, device=0):
+        self._range = aRange_m
+        self._angle = aAngle_rad
+        self._resl = int(np.rad2deg(aAngle_rad))
+        self._lm = np.ascontiguousarray(aLandMarks, dtype=np.float64).reshape(-1, 2)
+        self._device = int(device)
+        self._tan = float(np.tan(BASE_ANG - aAngle_rad))          # :154
+        ang = np.rad2deg(aAngle_rad)                               # :99-112 (the drawn fan)
+        ofs = np.rad2deg(BASE_ANG)
+        xs = np.arange(-ang + ofs, ang + ofs + 1.0, 1.0)
+        p0 = [aRange_m * np.cos(np.deg2rad(x)) for x in xs] + [0.0]
+        p1 = [aRange_m * np.sin(np.deg2rad(x)) for x in xs] + [0.0]
+        p0.append(p0[0])
+        p1.append(p1[0])
+        self.local = np.array([p0, p1])
+
+    def setNoiseParam(self, aDist, aDirSigma, aOrientSigma):
+        """:115-126 (percent, degrees, degrees)."""
+        ScanSensor._R_Dist = aDist / 100
+        ScanSensor._R_DirSigma = np.deg2rad(aDirSigma)
+        ScanSensor._R_OrientSigma = np.deg2rad(aOrientSigma)
+
+    def _detect(self, poses):
+        poses = np.ascontiguousarray(poses, dtype=np.float64).reshape(-1, 3)
+        yaw = BASE_ANG - poses[:, 2]                               # transform.py:31, :152
+        cs = np.ascontiguousarray(np.column_stack([np.cos(yaw), np.sin(yaw), yaw]))
+        P, L = len(poses), len(self._lm)
+        det = np.zeros((P, L), dtype=np.int32)
+        obs = np.zeros((P, L, 3))
+        lib = _lib.load()
+        check(lib.slam_scan_detect(P, dptr(poses), dptr(cs), L, dptr(self._lm), float(self._range),
+                                   self._tan, det.ctypes.data_as(C.POINTER(C.c_int32)), dptr(obs),
+                                   self._device), "slam_scan_detect")
+        return det.astype(bool), obs
+
+    def _noisy(self, clean):
+        """:163-165 for the detected observations, in order: three draws each."""
+        n = len(clean)
+        if np.any(clean[:, 0] * ScanSensor._R_Dist < 0) or ScanSensor._R_DirSigma < 0 or \
+                ScanSensor._R_OrientSigma < 0:
+            raise ValueError("scale < 0")                          # np.random.normal's check
+        g = np.random.standard_normal(3 * n)                       # = 3n np.random.normal calls
+        out = np.zeros((n, 3))
+        if n:
+            clean = np.ascontiguousarray(clean)
+            check(_lib.load().slam_scan_noise(n, dptr(clean), dptr(g), float(ScanSensor._R_Dist),
+                                              float(ScanSensor._R_DirSigma),
+                                              float(ScanSensor._R_OrientSigma), dptr(out),
+                                              self._device), "slam_scan_noise")
+        return out
+
+    def scan(self, aRobotPose):
+        """:128-172: (obsWithNoise, obsWithoutNoise), lists of Observation."""
+        return self.scan_batch(np.asarray(aRobotPose, dtype=np.float64).reshape(1, 3))[0]
+
+    def scan_batch(self, poses):
+        """scan() of every pose in order (the noise stream as consecutive calls)."""
+        det, obs = self._detect(poses)
+        p_idx, l_idx = np.nonzero(det)                             # pose-major, landmark order
+        clean = obs[p_idx, l_idx]
+        noisy = self._noisy(clean)
+        out = [([], []) for _ in range(len(det))]
+        for k, (p, i) in enumerate(zip(p_idx, l_idx)):
+            out[p][0].append(Observation(int(i), noisy[k, 0], noisy[k, 1], noisy[k, 2]))
+            out[p][1].append(Observation(int(i), clean[k, 0], clean[k, 1], clean[k, 2]))
+        return out
+
+    @classmethod
+    def getLandMarkCovMatrixOnMeasurementSys(cls, aLandMarkDist):
+        """:176-194."""
+        dist = aLandMarkDist * ScanSensor._R_Dist
+        dir_cov = (aLandMarkDist * np.sin(ScanSensor._R_DirSigma)) ** 2
+        orient_cov = ScanSensor._R_DirSigma ** 2 + ScanSensor._R_OrientSigma ** 2
+        return np.array([[dist ** 2, 0, 0], [0, dir_cov, 0], [0, 0, orient_cov]])
+
+    @classmethod
+    def tfMeasurement2World(cls, aCovMat, aLandMarkDir, aRobotDir):
+        """:196-213."""
+        ang = aLandMarkDir + aRobotDir - BASE_ANG
+        c = np.cos(ang)
+        s = np.sin(ang)
+        rot = np.array([[c, -s, 0], [s, c, 0], [0, 0, 1]])
+        return rot @ aCovMat @ rot.T
 
 
 class HalfEdge:

@@ -393,8 +393,38 @@ def gen_ellipse(seed=5):
                         out99=out, out95=out95, chi_l=chi_l)
 
 
+# ------------------------------------------------------------- scan sensor
+def gen_scan(seed=13, n_poses=40, n_lm=300):
+    """graph_based_slam.py:78-172 ScanSensor.scan: random poses among random
+    landmarks (the demo's 15 m / +-80 deg fan and noise setting, :899-902 /
+    :604), one scan per pose from a seeded global stream; per pose the
+    detected ids and the noise-free and noisy (dist, dir, orient)."""
+    np.random.seed(seed)                         # the module draws at import
+    with _quiet():
+        import graph_based_slam as gs
+    rs = np.random.RandomState(seed)
+    lm = rs.uniform(-20.0, 20.0, (n_lm, 2))
+    poses = np.column_stack([rs.uniform(-10, 10, n_poses), rs.uniform(-10, 10, n_poses),
+                             rs.uniform(-np.pi, np.pi, n_poses)])
+    sensor = gs.ScanSensor(15.0, np.deg2rad(80.0), lm)
+    sensor.setNoiseParam(5, 2, 2)
+    np.random.seed(seed + 1)
+    ids, clean, noisy, npp = [], [], [], []
+    for p in poses:
+        wn, wo = sensor.scan(p.reshape(3, 1))
+        npp.append(len(wn))
+        for a, b in zip(wn, wo):
+            ids.append(a.getLandMarkId())
+            noisy.append([a.getDist(), a.getDir(), a.getOrient()])
+            clean.append([b.getDist(), b.getDir(), b.getOrient()])
+    np.savez_compressed(os.path.join(OUT, "scan.npz"), seed=seed, lm=lm, poses=poses,
+                        n_per_pose=np.array(npp), ids=np.array(ids, dtype=np.int64),
+                        clean=np.array(clean).reshape(-1, 3), noisy=np.array(noisy).reshape(-1, 3))
+
+
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["units", "pf_c1", "pf_stages", "motion", "ekf", "graph", "ellipse"]
+    which = sys.argv[1:] or ["units", "pf_c1", "pf_stages", "motion", "ekf", "graph", "ellipse",
+                             "scan"]
     for w in which:
         print("generating", w, flush=True)
         globals()["gen_" + w]()

@@ -185,3 +185,22 @@ def test_graph_t300_pairing_and_gauss_newton_bit_exact():
         _eq(H[::7, ::11], g[f"big{i}_H_sample"])
         _eq(stats, g[f"big{i}_stats"])
         _eq(poses, g[f"big{i}_poses_after"])
+
+
+def test_scan_sensor_fixture():
+    """ScanSensor.scan (graph_based_slam.py:128-172) restated: the reference's
+    detections, noise-free and noisy observations, bit-exact, from the same
+    seeded global stream (tests/golden/make_golden.py gen_scan)."""
+    import graph_oracle as go
+    g = golden("scan")
+    np.random.seed(int(g["seed"]) + 1)
+    ids, clean, noisy = [], [], []
+    for p in g["poses"]:
+        a, b, c = go.scan_sensor(p, g["lm"], 15.0, np.deg2rad(80.0), 0.05, np.deg2rad(2.0),
+                                 np.deg2rad(2.0))
+        ids.append(a)
+        clean.append(b)
+        noisy.append(c)
+    np.testing.assert_array_equal(np.concatenate(ids), g["ids"])
+    np.testing.assert_array_equal(np.concatenate(clean), g["clean"])
+    np.testing.assert_array_equal(np.concatenate(noisy), g["noisy"])
