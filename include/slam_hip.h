@@ -413,6 +413,13 @@ int slam_scan_detect(int64_t n_poses, const double* poses, const double* yaw_cs,
 int slam_scan_noise(int64_t n, const double* clean, const double* normals, double r_dist,
                     double r_dir, double r_orient, double* out, int device);
 
+/* ErrorEllipse.calc_error_ellipse (mylib/error_ellipse.py:39-55) over n 2x2
+ * covariances (row-major [n][4]): out[n][3] = (major, minor, angle); chi from
+ * the chi-squared table on the host; column_vectors = 0 keeps the reference's
+ * vec[idxmax] row quirk (:51). */
+int slam_error_ellipse(int64_t n, const double* covs, double chi, int32_t column_vectors,
+                       double* out, int device);
+
 #ifdef __cplusplus
 }
 #endif

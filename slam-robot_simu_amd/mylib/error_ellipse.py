@@ -1,8 +1,8 @@
 """Error-ellipse parameters with the semantics of the reference's
 mylib/error_ellipse.py:15-68 (reporting helper).
 
-Host-side NumPy, like the reference module; nothing here is on the estimator's
-device path.  The drop-ins' callers (animation front-ends, user code) draw the
+Host-side NumPy, like the reference module, plus ``calc_error_ellipse_device``
+for a batch of covariances on the GPU (csrc/ellipse_api.hip).  The drop-ins' callers (animation front-ends, user code) draw the
 pose / landmark covariances returned by ``step()`` with it.
 
 Differences from the reference, none of which changes a result:
@@ -96,6 +96,23 @@ class ErrorEllipse(object):
         l = np.sqrt(val[rows, idxmax] * self.__chi) * 2
         y = np.sqrt(val[rows, idxmin] * self.__chi) * 2
         return l, y, ang
+
+    def calc_error_ellipse_device(self, sigmas, device=0):
+        """calc_error_ellipse_batch on the GPU (csrc/ellipse_api.hip: dsyevd's
+        2x2 path restated, LAPACK's eigen-decomposition doubles): three (N,)
+        arrays."""
+        import ctypes as C
+        from slamhip import _lib
+        from slamhip._lib import check
+        s = np.ascontiguousarray(sigmas, dtype=np.float64)
+        if s.ndim != 3 or s.shape[1:] != (2, 2):
+            raise ValueError("sigmas must have shape (N, 2, 2)")
+        out = np.empty((len(s), 3))
+        dp = C.POINTER(C.c_double)
+        check(_lib.load().slam_error_ellipse(len(s), s.ctypes.data_as(dp), float(self.__chi),
+                                             int(self._column), out.ctypes.data_as(dp), int(device)),
+              "slam_error_ellipse")
+        return out[:, 0], out[:, 1], out[:, 2]
 
     def calc_chi(self, p, sigma):
         """Major axis length at percentage point p (error_ellipse.py:57-68)."""

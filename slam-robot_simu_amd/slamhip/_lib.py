@@ -97,6 +97,7 @@ SIGNATURES = {
     "slam_scan_detect": (C.c_int, [C.c_int64, _D, _D, C.c_int64, _D, C.c_double, C.c_double, _I32, _D,
                                    C.c_int]),
     "slam_scan_noise": (C.c_int, [C.c_int64, _D, _D, C.c_double, C.c_double, C.c_double, _D, C.c_int]),
+    "slam_error_ellipse": (C.c_int, [C.c_int64, _D, C.c_double, C.c_int32, _D, C.c_int]),
     "slam_comm_unique_id": (C.c_int, [C.c_char_p]),
     "slam_comm_create": (C.c_int, [C.c_char_p, C.c_int32, C.c_int32, C.c_int, C.POINTER(_P)]),
     "slam_comm_destroy": (C.c_int, [_P]),
