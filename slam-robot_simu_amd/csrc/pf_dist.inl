@@ -70,8 +70,7 @@ struct DistLayout {
     int64_t rec_stride = 0, cap_spec = 0, cap_item = 0;
 };
 
-// a resampled particle with its destination positions [lo, hi) (global), 48 B:
-// three 16-byte stores
+// a resampled particle with its destination positions [lo, hi) (global), 48 B
 struct alignas(16) DistItem {
     double x, y, th;
     int64_t lo, hi, pad;
@@ -95,7 +94,7 @@ struct DistScratch {
     double c_left;              // exact cumsum just before local element 0 (-inf on rank 0)
     int64_t lo0;                // positions <= c_left
     int64_t covered;            // positions covered by the received items (unpack; reset by its last block)
-    int32_t rel[2];             // dist_resample_merged_kernel: release tokens of phases A / B
+    int32_t rel[4];             // dist_resample_merged_kernel: release tokens of phases A / B / D
     int64_t dbase[kDistMaxWorld];   // per destination: selected sources before its range
     int64_t dcnt[kDistMaxWorld];    // per destination: items sent
 };
@@ -154,20 +153,23 @@ __device__ __forceinline__ S ld_sys_struct(const S* p) {
     return v;
 }
 
-typedef unsigned long long dist_u64x2 __attribute__((ext_vector_type(2)));
 
-// own items: three 16-byte stores to regular memory (read by a later launch on
-// this device); a peer's: system-scope stores into its exchange region, so
+// own items: write-through stores to regular memory; a peer's: system-scope
+// stores into its exchange region, so
 // they have completed at system scope once the storing block's vmcnt drains
 // (before its ticket) -- no per-block L2 writeback
 __device__ __forceinline__ void dist_store_item(const DistPeers& P, const int d, const int64_t slot,
                                                 const double x, const double y, const double th,
                                                 const int64_t lo, const int64_t hi) {
     if (d == P.rank) {
-        dist_u64x2* p = reinterpret_cast<dist_u64x2*>(P.self_items + slot);
-        p[0] = dist_u64x2{(unsigned long long)__double_as_longlong(x), (unsigned long long)__double_as_longlong(y)};
-        p[1] = dist_u64x2{(unsigned long long)__double_as_longlong(th), (unsigned long long)lo};
-        p[2] = dist_u64x2{(unsigned long long)hi, 0ull};
+        // write-through (agent scope): the one-launch exchange unpacks them on other
+        // XCDs, whose L2s do not see this one's dirty lines
+        uint64_t* p = reinterpret_cast<uint64_t*>(P.self_items + slot);
+        st_wt(p + 0, (uint64_t)__double_as_longlong(x));
+        st_wt(p + 1, (uint64_t)__double_as_longlong(y));
+        st_wt(p + 2, (uint64_t)__double_as_longlong(th));
+        st_wt(p + 3, (uint64_t)lo);
+        st_wt(p + 4, (uint64_t)hi);
         return;
     }
     uint64_t* p = reinterpret_cast<uint64_t*>(reinterpret_cast<DistItem*>(P.base[d] + P.L.item) +
@@ -439,26 +441,27 @@ __global__ __launch_bounds__(kScanThreads) void dist_pack_push_kernel(
 // positions (disjoint, non-empty ranges), so k < n.  The last block checks that
 // the ranges tile the shard (status kDistStItems otherwise).  The resample flag
 // stays 1: the fused kernel gathers through the marks, at weight 1/NP.
-__global__ __launch_bounds__(256) void dist_unpack_kernel(
-    const int64_t n, double* __restrict__ xs, double* __restrict__ ys, double* __restrict__ ts,
-    int64_t* __restrict__ mark, int32_t* __restrict__ carry, unsigned* __restrict__ counter,
-    int32_t* __restrict__ flags, DistScratch* __restrict__ scr, const DistPeers P, StepIO io) {
-    if (!dist_resampling(flags) || flags[kFlagFallback]) return;
-    dist_wait(P, kXItem, dist_epoch(io), flags);
-    __shared__ int64_t s_off[kDistMaxWorld + 1];
-    __shared__ unsigned long long s_cov;
+// the item offsets of every source rank in this rank's region (thread 0)
+__device__ __forceinline__ void dist_item_offsets(const DistPeers& P, int64_t* s_off) {
     const char* mine = P.base[P.rank];
-    const DistItem* items = reinterpret_cast<const DistItem*>(mine + P.L.item);
-    if (threadIdx.x == 0) {
-        int64_t o = 0;
-        for (int q = 0; q < P.world; ++q) {
-            s_off[q] = o;
-            o += (int64_t)ld_sys(reinterpret_cast<const int64_t*>(mine + P.L.item_hdr) + 2 * q);
-        }
-        s_off[P.world] = o;
-        s_cov = 0;
+    int64_t o = 0;
+    for (int q = 0; q < P.world; ++q) {
+        s_off[q] = o;
+        o += (int64_t)ld_sys(reinterpret_cast<const int64_t*>(mine + P.L.item_hdr) + 2 * q);
     }
+    s_off[P.world] = o;
+}
+
+// grid-stride over the received items (s_off: offsets per source rank, in LDS)
+__device__ void dist_unpack_items(const int64_t n, double* __restrict__ xs, double* __restrict__ ys,
+                                  double* __restrict__ ts, int64_t* __restrict__ mark,
+                                  int32_t* __restrict__ carry, unsigned* __restrict__ counter,
+                                  int32_t* __restrict__ flags, DistScratch* __restrict__ scr,
+                                  const DistPeers& P, const int64_t* s_off) {
+    __shared__ unsigned long long s_cov;
+    if (threadIdx.x == 0) s_cov = 0;
     __syncthreads();
+    const DistItem* items = reinterpret_cast<const DistItem*>(P.base[P.rank] + P.L.item);
     const int64_t ntot = s_off[P.world] < n ? s_off[P.world] : n;
     const int64_t gb = P.gb[P.rank];
     const int64_t gen = (int64_t)(uint32_t)flags[kFlagMarkGen] << 32;
@@ -470,13 +473,12 @@ __global__ __launch_bounds__(256) void dist_unpack_kernel(
         int64_t lo, hi;
         double x, y, th;
         if (q == P.rank) {                                  // own items: regular memory
-            const dist_u64x2* it = reinterpret_cast<const dist_u64x2*>(P.self_items + (k - s_off[q]));
-            const dist_u64x2 a = it[0], b = it[1], c = it[2];
-            x = __longlong_as_double((long long)a.x);
-            y = __longlong_as_double((long long)a.y);
-            th = __longlong_as_double((long long)b.x);
-            lo = (int64_t)b.y - gb;
-            hi = (int64_t)c.x - gb;
+            const uint64_t* it = reinterpret_cast<const uint64_t*>(P.self_items + (k - s_off[q]));
+            x = __longlong_as_double((long long)ld_wt(it + 0));
+            y = __longlong_as_double((long long)ld_wt(it + 1));
+            th = __longlong_as_double((long long)ld_wt(it + 2));
+            lo = (int64_t)ld_wt(it + 3) - gb;
+            hi = (int64_t)ld_wt(it + 4) - gb;
         } else {
             const DistItem* it = items + (int64_t)q * P.L.cap_item + (k - s_off[q]);
             lo = (int64_t)ld_sys(&it->lo) - gb;
@@ -508,6 +510,27 @@ __global__ __launch_bounds__(256) void dist_unpack_kernel(
     }
 }
 
+// wait for every rank's items and hand them to the fused kernel's resample
+// gather (the single-GPU expand pass's inverse map): item k (ranks in order,
+// each rank's items in position order) is stored at local index k of the
+// particle arrays -- the pre-resample particles were packed already -- with a
+// run mark (mark generation | k) at its first local position and the carry of
+// every fused block whose first position it covers.  Items never outnumber the
+// positions (disjoint, non-empty ranges), so k < n.  The last block checks that
+// the ranges tile the shard (status kDistStItems otherwise).  The resample flag
+// stays 1: the fused kernel gathers through the marks, at weight 1/NP.
+__global__ __launch_bounds__(256) void dist_unpack_kernel(
+    const int64_t n, double* __restrict__ xs, double* __restrict__ ys, double* __restrict__ ts,
+    int64_t* __restrict__ mark, int32_t* __restrict__ carry, unsigned* __restrict__ counter,
+    int32_t* __restrict__ flags, DistScratch* __restrict__ scr, const DistPeers P, StepIO io) {
+    if (!dist_resampling(flags) || flags[kFlagFallback]) return;
+    dist_wait(P, kXItem, dist_epoch(io), flags);
+    __shared__ int64_t s_off[kDistMaxWorld + 1];
+    if (threadIdx.x == 0) dist_item_offsets(P, s_off);
+    __syncthreads();
+    dist_unpack_items(n, xs, ys, ts, mark, carry, counter, flags, scr, P, s_off);
+}
+
 // ---------------------------------------------------------------- resample, one launch
 // The whole exchange side of a resample step in ONE launch (one shard per
 // process; the grid must be co-resident -- checked on the host -- because its
@@ -528,6 +551,7 @@ __global__ __launch_bounds__(256) void dist_unpack_kernel(
 //      block publishes the counts and signals kXItem.
 // dist_unpack_kernel then hands the received items to the fused kernel.
 constexpr int kDistTokenWait = 1 << 22;
+constexpr int kDistBfLds = 2048;            // block offsets staged in LDS (nb_scan <= 2048: n <= 2^22)
 
 // bounded wait of thread 0 for `token` in a write-through word; the block's
 // threads then all see the released data (agent-scope acquire)
@@ -642,8 +666,9 @@ __global__ __launch_bounds__(kScanThreads) void dist_resample_merged_kernel(
     int32_t* __restrict__ nspec_p, unsigned* __restrict__ tk, int32_t* __restrict__ flags,
     SpecialOut* __restrict__ spec_go, DistScratch* __restrict__ scr,
     int32_t* __restrict__ bsel, int32_t* __restrict__ bsel_off, int32_t* __restrict__ bdst,
-    const double* __restrict__ xs, const double* __restrict__ ys, const double* __restrict__ ts,
-    const DistPeers P, StepIO io, const PredictConst pc, const uint64_t seed, const int ntiles) {
+    double* __restrict__ xs, double* __restrict__ ys, double* __restrict__ ts,
+    int64_t* __restrict__ mark, int32_t* __restrict__ carry, const DistPeers P, StepIO io,
+    const PredictConst pc, const uint64_t seed, const int ntiles) {
     if (!dist_resampling(flags)) return;
     __shared__ int64_t s_off[kDistMaxWorld + 1];
     __shared__ uint64_t s_koff[kDistMaxWorld + 1];
@@ -651,6 +676,7 @@ __global__ __launch_bounds__(kScanThreads) void dist_resample_merged_kernel(
     const uint64_t epoch = dist_epoch(io);
     const int32_t tokA = ld_wt_i(&scr->rel[0]) + 1;        // read before this block arrives
     const int32_t tokB = ld_wt_i(&scr->rel[1]) + 1;
+    const int32_t tokD = ld_wt_i(&scr->rel[2]) + 1;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int64_t tile = (int64_t)blockIdx.x * kTilesPerBlock + wave;
     const bool active = tile < ntiles;
@@ -680,15 +706,22 @@ __global__ __launch_bounds__(kScanThreads) void dist_resample_merged_kernel(
         const int32_t ns = ld_wt_i(nspec_p);
         const uint64_t kt = ld_wt(ktot_p);
         PROBE_AT(18);
-        // this rank's specials in order -> every peer's slot (tile by bofff search)
+        // this rank's specials in order -> every peer's slot (tile by a search of
+        // the block offsets, staged in LDS)
+        __shared__ int32_t s_bf[kDistBfLds];
+        const bool bf_lds = (int)gridDim.x <= kDistBfLds;
+        if (bf_lds)
+            for (int k = threadIdx.x; k < (int)gridDim.x; k += blockDim.x) s_bf[k] = ld_wt_i(&bofff[k]);
+        __syncthreads();
+        auto bf_at = [&](const int k) { return bf_lds ? s_bf[k] : ld_wt_i(&bofff[k]); };
         for (int32_t m = threadIdx.x; m < ns; m += blockDim.x) {
             int lo = 0, hi = (int)gridDim.x - 1;
             while (lo < hi) {
                 const int mid = (lo + hi + 1) >> 1;
-                if (ld_wt_i(&bofff[mid]) <= m) lo = mid;
+                if (bf_at(mid) <= m) lo = mid;
                 else hi = mid - 1;
             }
-            SpecialIn e = ld_wt_struct(&stage[(int64_t)lo * kScanBlock + (m - ld_wt_i(&bofff[lo]))]);
+            SpecialIn e = ld_wt_struct(&stage[(int64_t)lo * kScanBlock + (m - bf_at(lo))]);
             e.P += ld_wt(&boffk[lo]);
             e.idx += gbase;
             if (m < P.L.cap_spec)
@@ -842,8 +875,16 @@ __global__ __launch_bounds__(kScanThreads) void dist_resample_merged_kernel(
         // wave per destination pair, lanes striding over the blocks)
         for (int e = wave; e < 2 * P.world; e += kScanThreads / 64) {
             int64_t a = 0;
-            for (int b = lane; b < (int)gridDim.x; b += 64)
-                a += ld_wt_i(&bdst[(int64_t)b * 2 * kDistMaxWorld + e]);
+            for (int b0 = lane; b0 < (int)gridDim.x; b0 += 64 * 8) {
+                int32_t v[8];                               // eight loads in flight
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const int b = b0 + 64 * u;
+                    v[u] = (b < (int)gridDim.x) ? ld_wt_i(&bdst[(int64_t)b * 2 * kDistMaxWorld + e]) : 0;
+                }
+#pragma unroll
+                for (int u = 0; u < 8; ++u) a += v[u];
+            }
 #pragma unroll
             for (int o = 1; o < 64; o <<= 1) a += __shfl_xor(a, o, 64);
             if (lane == 0) st_wt((e & 1) ? (void*)&scr->dcnt[e >> 1] : (void*)&scr->dbase[e >> 1], (uint64_t)a);
@@ -853,7 +894,6 @@ __global__ __launch_bounds__(kScanThreads) void dist_resample_merged_kernel(
     } else {
         dist_token_wait(&scr->rel[1], tokB, flags);
     }
-    PROBE_MAX(14);
     __shared__ int64_t s_dbase[kDistMaxWorld];
     __shared__ int64_t s_ps0;
     if ((int)threadIdx.x < P.world) s_dbase[threadIdx.x] = (int64_t)ld_wt(&scr->dbase[threadIdx.x]);
@@ -863,7 +903,6 @@ __global__ __launch_bounds__(kScanThreads) void dist_resample_merged_kernel(
         g_probe[15] = (unsigned long long)(ld_wt_i(&bsel_off[blockIdx.x]) + tot);
 #endif
     __syncthreads();
-    PROBE_MAX(12);
     // ---- C: items to every destination
     if (active) {
         int64_t ps = s_ps0 + cex;
@@ -885,14 +924,25 @@ __global__ __launch_bounds__(kScanThreads) void dist_resample_merged_kernel(
         }
     }
     PROBE_MAX(25);
-    if (!arrive_last(tk + 2 * kTicketWords)) return;       // (drains this block's item stores)
-    if ((int)threadIdx.x < P.world) {
-        int64_t* hdr = reinterpret_cast<int64_t*>(P.base[threadIdx.x] + P.L.item_hdr) + 2 * P.rank;
-        hdr[0] = (int64_t)ld_wt(&scr->dcnt[threadIdx.x]);
+    // ---- D: publish, wait for every rank's items, unpack them (dist_unpack_items)
+    if (arrive_last(tk + 2 * kTicketWords)) {              // (drains this block's item stores)
+        if ((int)threadIdx.x < P.world) {
+            int64_t* hdr = reinterpret_cast<int64_t*>(P.base[threadIdx.x] + P.L.item_hdr) + 2 * P.rank;
+            hdr[0] = (int64_t)ld_wt(&scr->dcnt[threadIdx.x]);
+        }
+        __syncthreads();
+        dist_signal(P, kXItem, epoch);
+        PROBE_AT(26);
+        dist_wait(P, kXItem, epoch, flags);
+        dist_token_release(&scr->rel[2], tokD);
+    } else {
+        dist_token_wait(&scr->rel[2], tokD, flags);
     }
     __syncthreads();
-    dist_signal(P, kXItem, epoch);
-    PROBE_AT(26);
+    __shared__ int64_t s_ioff[kDistMaxWorld + 1];
+    if (threadIdx.x == 0) dist_item_offsets(P, s_ioff);
+    __syncthreads();
+    dist_unpack_items(n, xs, ys, ts, mark, carry, tk + 3 * kTicketWords, flags, scr, P, s_ioff);
 }
 
 // ---------------------------------------------------------------- record

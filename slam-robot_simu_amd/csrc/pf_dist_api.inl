@@ -61,8 +61,8 @@ int dist_enqueue_step(slam_dist* d) {
         dist_resample_merged_kernel<<<h->nb_scan, kScanThreads, 0, h->stream>>>(
             h->w_un, h->s_cur, h->pc.np_recip, h->n, h->boff, delta, h->stage, h->bk, h->bf,
             h->boffk, h->bofff, h->ktot, h->nspec, d->tk[0], h->flags, d->spec_go[0], d->scr[0],
-            d->bsel[0], d->bsel_off[0], d->bdst[0], h->x[c], h->y[c], h->th[c], d->peers[0],
-            step_io(h), h->pc, h->cfg.seed, h->nb_part);
+            d->bsel[0], d->bsel_off[0], d->bdst[0], h->x[c], h->y[c], h->th[c], h->dp.mark,
+            h->dp.carry, d->peers[0], step_io(h), h->pc, h->cfg.seed, h->nb_part);
     }
     for (int i = 0; i < m && !d->merged; ++i) {           // exact cumsum: classify
         slam_pf* h = d->sh[i];
@@ -98,7 +98,7 @@ int dist_enqueue_step(slam_dist* d) {
             h->n, h->x[c], h->y[c], h->th[c], d->hi[i], d->bsel_off[i], d->tk[i] + 2 * kTicketWords,
             h->flags, d->scr[i], d->peers[i], step_io(h));
     }
-    for (int i = 0; i < m; ++i) {                         // unpack (waits for the items)
+    for (int i = 0; i < m && !d->merged; ++i) {           // unpack (waits for the items)
         slam_pf* h = d->sh[i];
         const int c = h->cur;
         dist_unpack_kernel<<<std::min<unsigned>(grid_for(h->n, 256), 1024), 256, 0, h->stream>>>(

@@ -38,7 +38,7 @@ for r in range(10):
     d = lambda a, b: (t[b] - t[a]) * tick if t[a] and t[b] else float("nan")
     print(f"batch {r}: resample A {d(16, 17):6.2f} scans {d(17, 18):5.2f} push {d(18, 19):5.2f} "
           f"wait {d(19, 20):5.2f} fold {d(20, 21):5.2f} rel {d(21, 22):5.2f} | B {d(22, 23):6.2f} "
-          f"relB {d(23, 24):5.2f} wake {d(24, 14):5.2f} pre {d(14, 12):5.2f} | C {d(24, 25):6.2f} sig {d(25, 26):5.2f} | total {d(16, 26):6.2f} || "
+          f"relB {d(23, 24):5.2f} | C {d(24, 25):6.2f} sig {d(25, 26):5.2f} | total(to signal) {d(16, 26):6.2f} || "
           f"reduce: rec[ld {d(27, 0):5.2f} red {d(0, 1):5.2f} cand {d(1, 2):5.2f} misc {d(2, 3):5.2f} win {d(3, 28):5.2f}] record {d(27, 28):5.2f} push {d(28, 29):5.2f} wait {d(29, 30):5.2f} "
           f"finalize {d(30, 31):5.2f} total {d(27, 31):6.2f}  resampled {sum(o['resampled'] for o in out)} "
           f"selected {t[15]}")
