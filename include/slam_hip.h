@@ -420,6 +420,43 @@ int slam_scan_noise(int64_t n, const double* clean, const double* normals, doubl
 int slam_error_ellipse(int64_t n, const double* covs, double chi, int32_t column_vectors,
                        double* out, int device);
 
+/* ====================================================================
+ * NumPy's legacy RandomState stream on the device (MT19937 + polar
+ * Box-Muller with the cached normal): the reference's noise source
+ * (particle_filter.py:152, :165, :214; motion_model.py:46-48), drawn
+ * bit-identically.  State = np.random.get_state()[1:5]: key[624], pos,
+ * has_gauss, cached_gaussian.  log() is glibc's, restated with the table of
+ * this process's libm (checked against its log() on first use).
+ * ==================================================================== */
+typedef struct slam_mt slam_mt;
+int slam_mt_create(const uint32_t* key, int32_t pos, int32_t has_gauss, double gauss, int device,
+                   slam_mt** out);
+int slam_mt_destroy(slam_mt* h);
+int slam_mt_set_state(slam_mt* h, const uint32_t* key, int32_t pos, int32_t has_gauss, double gauss);
+int slam_mt_get_state(slam_mt* h, uint32_t* key, int32_t* pos, int32_t* has_gauss, double* gauss);
+/* RandomState.random_sample(n) / standard_normal(n) into host arrays */
+int slam_mt_random_sample(slam_mt* h, int64_t n, double* out);
+int slam_mt_standard_normal(slam_mt* h, int64_t n, double* out);
+/* glibc's log restated (host; the function the device kernels evaluate) */
+int slam_glibc_log(int64_t n, const double* x, double* out);
+
+/* Particle filter with the reference's own noise stream on the device
+ * (main_pf, particle_filter.py:86-119): each step draws [rand() if resampling]
+ * -> mvn(0, Q, NP) -> mvn(0, R, NL) from the device stream, observes the
+ * landmarks from the true pose on the device (__observation :144-154) and runs
+ * the estimator.  r_factor = sqrt(s)[:, None] * v of svd(R) (row-major 2x2).
+ * truth[4] per step = (x, y, cos(yaw'), sin(yaw')) of the true pose with
+ * yaw' = pi/2 - theta (mylib/transform.py:31-35, NumPy's cos / sin). */
+int slam_pf_set_rng_mt19937(slam_pf* h, const uint32_t* key, int32_t pos, int32_t has_gauss,
+                            double gauss, const double* r_factor);
+int slam_pf_get_rng_mt19937(slam_pf* h, uint32_t* key, int32_t* pos, int32_t* has_gauss,
+                            double* gauss);
+int slam_pf_step_truth(slam_pf* h, const double* control, const double* truth, double* z_out,
+                       slam_pf_result* res);
+/* device-resident batch: truth[n_steps][4]; slam_pf_run then simulates the
+ * observations of steps [first, first + k) on the device */
+int slam_pf_load_truth(slam_pf* h, int32_t n_steps, const double* truth);
+
 #ifdef __cplusplus
 }
 #endif

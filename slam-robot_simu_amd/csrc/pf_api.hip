@@ -10,6 +10,7 @@
 #include <limits>
 #include <vector>
 
+#include "mt_stream.hpp"
 #include "pf_kernels.inl"
 #include "pf_shard.inl"
 #include "pf_dist.inl"
@@ -113,6 +114,13 @@ struct slam_pf {
     double* s_cur = nullptr;
     DeferParts dp{};
     int32_t nb_part = 0;
+    // NumPy's RandomState stream on the device (slam_pf_set_rng_mt19937)
+    bool mt = false;
+    MtBuffers mtb;
+    double mr[4] = {0, 0, 0, 0};         // svd factor of R (mvn of the observation noise)
+    double* truth = nullptr;             // [cap][4] true pose (x, y, cos, sin) per step
+    int32_t truth_steps = 0;
+    const double* noise_src = nullptr;   // fused kernel's host-noise input (default h->noise)
 };
 
 namespace {
@@ -237,6 +245,7 @@ int ensure_steps(slam_pf* h, int32_t steps) {
     release(h, h->z_all);
     release(h, h->zc);
     release(h, h->ofs);
+    release(h, h->truth);
     release(h, h->res_dev);
     if (h->res_host) (void)hipHostFree(h->res_host);
     h->res_host = nullptr;
@@ -244,11 +253,13 @@ int ensure_steps(slam_pf* h, int32_t steps) {
     const size_t nlz = 2 * (size_t)std::max<int32_t>(h->nl, 1);
     if ((rc = dalloc(h, &h->ctl, 2 * (size_t)steps)) || (rc = dalloc(h, &h->z_all, nlz * steps)) ||
         (rc = dalloc(h, &h->zc, (size_t)kClosedWords * steps)) ||
-        (rc = dalloc(h, &h->ofs, (size_t)steps)) || (rc = dalloc(h, &h->res_dev, (size_t)steps)))
+        (rc = dalloc(h, &h->ofs, (size_t)steps)) || (rc = dalloc(h, &h->truth, 4 * (size_t)steps)) ||
+        (rc = dalloc(h, &h->res_dev, (size_t)steps)))
         return rc;
     SLAM_HIP_TRY(hipHostMalloc((void**)&h->res_host, sizeof(slam_pf_result) * steps));
     h->cap = steps;
     h->z_steps = 0;
+    h->truth_steps = 0;
     return SLAM_OK;
 }
 
@@ -336,10 +347,11 @@ int launch_fused(slam_pf* h, int motion, bool host_noise) {
     const StepIO io = step_io(h);
     tic(h, 0);
     const double* w_in = h->deferred ? nullptr : h->w;     // deferred: read from w_un
+    const double* nsrc = h->noise_src ? h->noise_src : h->noise;
 #define SLAM_FUSED_D(M, L, HN, D)                                                                \
     pf_fused_kernel<M, L, HN, D><<<g, 256, 0, s>>>(n, h->x[src], h->y[src], h->th[src],         \
                                                    h->x[dst], h->y[dst], h->th[dst], w_in,      \
-                                                   h->w_un, h->c, h->flags, h->noise, h->lm, io, \
+                                                   h->w_un, h->c, h->flags, nsrc, h->lm, io,     \
                                                    h->pc, h->lc, h->cfg.seed, h->s_cur, h->refp, \
                                                    h->dp)
 #define SLAM_FUSED(M, L, HN)                 \
@@ -401,9 +413,74 @@ int launch_reduce(slam_pf* h, int32_t resampled_known) {
     return SLAM_OK;
 }
 
+// ---- NumPy's stream on the device (slam_pf_set_rng_mt19937)
+//
+// __observation (particle_filter.py:144-154) of step ctr[0] from the true pose:
+// world2robot (mylib/transform.py:31-35: the 2x2 rotation through OpenBLAS's
+// fused dgemm) plus the mvn(0, R) noise of normals [n3, n3 + 2 NL) (x @ M,
+// dgemm order); then the step's closed-form log-sum sums (iso handles).
+__global__ __launch_bounds__(256) void pf_mt_observe_kernel(
+    const double* __restrict__ normals, const int64_t n3, const double* __restrict__ lm,
+    const int32_t nl, const double* __restrict__ truth, const int32_t* __restrict__ ctr,
+    const double r0, const double r1, const double r2, const double r3, double* __restrict__ z_all,
+    double* __restrict__ zc, const int32_t closed) {
+    extern __shared__ double s_z[];
+    const int32_t st = ctr[0];
+    const double* t = truth + 4 * (size_t)st;
+    const double tx = t[0], ty = t[1], c = t[2], s = t[3];
+    double* z = z_all + (size_t)st * 2 * nl;
+    for (int32_t l = threadIdx.x; l < nl; l += blockDim.x) {
+        const double n0 = normals[n3 + 2 * l], n1 = normals[n3 + 2 * l + 1];
+        const double w0 = fma(n1, r2, n0 * r0), w1 = fma(n1, r3, n0 * r1);
+        const double dx = lm[2 * l] - tx, dy = lm[2 * l + 1] - ty;
+        const double zx = fma(-s, dy, c * dx) + w0;
+        const double zy = fma(c, dy, s * dx) + w1;
+        z[2 * l] = zx;
+        z[2 * l + 1] = zy;
+        s_z[2 * l] = zx;
+        s_z[2 * l + 1] = zy;
+    }
+    __syncthreads();
+    if (closed && threadIdx.x == 0) closed_sums(lm, s_z, nl, zc + (size_t)st * kClosedWords);
+}
+
+// mvn(0, Q, NP) (particle_filter.py:165): noise = normals @ M, OpenBLAS's order
+__global__ __launch_bounds__(256) void pf_mt_noise_kernel(const int64_t n,
+                                                          const double* __restrict__ g,
+                                                          const PredictConst pc,
+                                                          double* __restrict__ noise) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const double n0 = g[3 * i], n1 = g[3 * i + 1], n2 = g[3 * i + 2];
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+        noise[3 * i + j] = fma(n2, pc.q[6 + j], fma(n1, pc.q[3 + j], n0 * pc.q[j]));
+}
+
+// the step's draws: [rand() if resampling] -> mvn(Q, NP) -> mvn(R, NL)
+int launch_mt(slam_pf* h) {
+    const int64_t n3 = 3 * h->n;
+    int rc = mt_enqueue(h->mtb, 0, h->flags + kFlagResample, h->pc.np_recip, h->ofs, h->ctr,
+                        n3 + 2 * (int64_t)h->nl, h->flags + kFlagStatus, h->stream);
+    if (rc) return rc;
+    if (h->nl > 0)
+        pf_mt_observe_kernel<<<1, 256, 16 * (size_t)h->nl, h->stream>>>(
+            h->mtb.normals, n3, h->lm, h->nl, h->truth, h->ctr, h->mr[0], h->mr[1], h->mr[2],
+            h->mr[3], h->z_all, h->zc, h->lc.closed);
+    if (h->cfg.motion == SLAM_MOTION_LINEAR)
+        pf_mt_noise_kernel<<<grid_for(h->n, 256), 256, 0, h->stream>>>(h->n, h->mtb.normals, h->pc,
+                                                                     h->noise);
+    SLAM_HIP_TRY(hipGetLastError());
+    return SLAM_OK;
+}
+
 // One whole device-decided step (scans gate on the flag; no host decision).
 int launch_step(slam_pf* h, bool host_noise) {
     int rc;
+    if (h->mt) {
+        if ((rc = launch_mt(h))) return rc;
+        host_noise = true;
+    }
     tic(h, 2);
     if ((rc = launch_scans(h, 0, false))) return rc;
     toc(h, 2);
@@ -420,6 +497,8 @@ int sync_results(slam_pf* h, int32_t first, int32_t count, slam_pf_result* out) 
         if (out) out[i] = h->res_host[i];
         if (h->res_host[i].status & 8)
             rc = fail(SLAM_ERR_HIP, "exact-cumsum launch: release token timed out");
+        if (h->res_host[i].status & 256)
+            rc = fail(SLAM_ERR_HIP, "mt19937 draw: candidate bound exhausted");
         if (h->res_host[i].status & 1)
             rc = fail(SLAM_ERR_INDEX, "resample position beyond the last cumulative weight "
                                       "(IndexError in particle_filter.py:219); clamped to NP-1");
@@ -597,48 +676,6 @@ int set_s_one(slam_pf* h) {
     return SLAM_OK;
 }
 
-// Closed-form log-sum sums of one step (likelihood_lanes, iso): S_ll = sum |l|^2,
-// S_l = sum l, S_zz = sum |z|^2, S_z = sum z, D = sum z.l, E = sum (z_y l_x - z_x l_y),
-// each a double-double (hi, lo) -- exact products, compensated sums.
-struct HostDD {
-    double h = 0.0, l = 0.0;
-    void add(const double bh, const double bl = 0.0) {
-        const double t = h + bh;
-        const double bb = t - h;
-        const double e = ((h - (t - bb)) + (bh - bb)) + (l + bl);
-        h = t + e;
-        l = e - (h - t);
-    }
-    void add_prod(const double a, const double b) {
-        const double p = a * b;
-        add(p, std::fma(a, b, -p));
-    }
-};
-
-void closed_sums(const double* lm, const double* z, const int32_t nl, double* out) {
-    HostDD Sll, Slx, Sly, Szz, Szx, Szy, D, E;
-    for (int32_t j = 0; j < nl; ++j) {
-        const double lx = lm[2 * j], ly = lm[2 * j + 1], zx = z[2 * j], zy = z[2 * j + 1];
-        Sll.add_prod(lx, lx);
-        Sll.add_prod(ly, ly);
-        Slx.add(lx);
-        Sly.add(ly);
-        Szz.add_prod(zx, zx);
-        Szz.add_prod(zy, zy);
-        Szx.add(zx);
-        Szy.add(zy);
-        D.add_prod(zx, lx);
-        D.add_prod(zy, ly);
-        E.add_prod(zy, lx);
-        E.add_prod(-zx, ly);
-    }
-    const HostDD* v[8] = {&Sll, &Slx, &Sly, &Szz, &Szx, &Szy, &D, &E};
-    for (int k = 0; k < 8; ++k) {
-        out[2 * k] = v[k]->h;
-        out[2 * k + 1] = v[k]->l;
-    }
-}
-
 // the closed-form sums of steps [0, n_steps) of z_host (or of one staged z) into zc
 int upload_closed(slam_pf* h, const double* z, const int32_t n_steps) {
     if (!h->nl || !h->lc.iso) return SLAM_OK;
@@ -711,6 +748,7 @@ int slam_pf_destroy(slam_pf* h) {
     (void)hipSetDevice(h->device);
     if (h->stream) (void)hipStreamSynchronize(h->stream);
     drop_graphs(h);
+    mt_free(h->mtb);
     for (void* p : h->allocs) (void)hipFree(p);
     if (h->res_host) (void)hipHostFree(h->res_host);
     for (int k = 0; k < 4; ++k)
@@ -960,8 +998,9 @@ int slam_pf_run(slam_pf* h, int32_t first_step, int32_t n_steps, const double* c
                 slam_pf_result* results) {
     SLAM_ARG_CHECK(h && controls && n_steps > 0, "slam_pf_run: bad argument");
     SLAM_ARG_CHECK(h->n == h->n_global, "slam_pf_run: sharded handle");
-    SLAM_ARG_CHECK(first_step >= 0 && first_step + n_steps <= h->z_steps,
-                   "slam_pf_run: steps outside the loaded observations");
+    SLAM_ARG_CHECK(first_step >= 0 && first_step + n_steps <= (h->mt ? h->truth_steps : h->z_steps),
+                   h->mt ? "slam_pf_run: steps outside the loaded true poses (slam_pf_load_truth)"
+                         : "slam_pf_run: steps outside the loaded observations");
     SLAM_HIP_TRY(hipSetDevice(h->device));
     int rc;
     SLAM_HIP_TRY(hipMemcpyAsync(h->ctl + 2 * first_step, controls, 2 * n_steps * sizeof(double),
@@ -1006,6 +1045,72 @@ int slam_pf_run(slam_pf* h, int32_t first_step, int32_t n_steps, const double* c
         }
     }
     return sync_results(h, first_step, n_steps, results);
+}
+
+int slam_pf_set_rng_mt19937(slam_pf* h, const uint32_t* key, int32_t pos, int32_t has_gauss,
+                            double gauss, const double* r_factor) {
+    SLAM_ARG_CHECK(h && key && r_factor, "slam_pf_set_rng_mt19937: NULL argument");
+    SLAM_ARG_CHECK(h->n == h->n_global, "slam_pf_set_rng_mt19937: sharded handle");
+    SLAM_ARG_CHECK(h->nl <= 4096, "slam_pf_set_rng_mt19937: at most 4096 landmarks");
+    SLAM_HIP_TRY(hipSetDevice(h->device));
+    SLAM_HIP_TRY(hipStreamSynchronize(h->stream));
+    int rc = mt_reserve(h->mtb, 3 * h->n + 2 * (int64_t)h->nl, 1, h->device);
+    if (rc) return rc;
+    if ((rc = mt_set_state(h->mtb, key, pos, has_gauss, gauss, h->stream))) return rc;
+    for (int k = 0; k < 4; ++k) h->mr[k] = r_factor[k];
+    if (!h->mt) drop_graphs(h);              // captured steps without the draws
+    h->mt = true;
+    h->noise_src = h->cfg.motion == SLAM_MOTION_LINEAR ? h->noise : h->mtb.normals;
+    return SLAM_OK;
+}
+
+int slam_pf_get_rng_mt19937(slam_pf* h, uint32_t* key, int32_t* pos, int32_t* has_gauss,
+                            double* gauss) {
+    SLAM_ARG_CHECK(h, "slam_pf_get_rng_mt19937: NULL handle");
+    SLAM_ARG_CHECK(h->mt, "slam_pf_get_rng_mt19937: the device stream is not enabled");
+    SLAM_HIP_TRY(hipSetDevice(h->device));
+    return mt_get_state(h->mtb, key, pos, has_gauss, gauss, h->stream);
+}
+
+int slam_pf_step_truth(slam_pf* h, const double* control, const double* truth, double* z_out,
+                       slam_pf_result* res) {
+    SLAM_ARG_CHECK(h && control && truth, "slam_pf_step_truth: NULL argument");
+    SLAM_ARG_CHECK(h->mt, "slam_pf_step_truth: enable the device stream first (slam_pf_set_rng_mt19937)");
+    SLAM_HIP_TRY(hipSetDevice(h->device));
+    int rc;
+    SLAM_HIP_TRY(hipMemcpyAsync(h->ctl, control, 2 * sizeof(double), hipMemcpyHostToDevice, h->stream));
+    SLAM_HIP_TRY(hipMemcpyAsync(h->truth, truth, 4 * sizeof(double), hipMemcpyHostToDevice, h->stream));
+    h->z_steps = 0;
+    h->truth_steps = 0;
+    const int32_t resampling = h->resample_next;
+    if ((rc = set_ctr(h, 0)) || (rc = set_flag(h, kFlagResample, resampling))) return rc;
+    tic(h, 3);
+    if ((rc = launch_mt(h))) return rc;
+    if (resampling) {
+        tic(h, 2);
+        if ((rc = launch_scans(h, 1, true))) return rc;
+        toc(h, 2);
+    }
+    if ((rc = launch_fused(h, h->cfg.motion, true))) return rc;
+    if ((rc = launch_reduce(h, resampling))) return rc;
+    toc(h, 3);
+    h->stepno++;
+    if (z_out && h->nl)
+        SLAM_HIP_TRY(hipMemcpyAsync(z_out, h->z_all, 2 * h->nl * sizeof(double), hipMemcpyDeviceToHost,
+                                    h->stream));
+    return sync_results(h, 0, 1, res);
+}
+
+int slam_pf_load_truth(slam_pf* h, int32_t n_steps, const double* truth) {
+    SLAM_ARG_CHECK(h && n_steps > 0 && truth, "slam_pf_load_truth: bad argument");
+    SLAM_HIP_TRY(hipSetDevice(h->device));
+    int rc = ensure_steps(h, n_steps);
+    if (rc) return rc;
+    SLAM_HIP_TRY(hipMemcpyAsync(h->truth, truth, (size_t)n_steps * 4 * sizeof(double),
+                                hipMemcpyHostToDevice, h->stream));
+    SLAM_HIP_TRY(hipStreamSynchronize(h->stream));
+    h->truth_steps = n_steps;
+    return SLAM_OK;
 }
 
 int slam_pf_enable_timing(slam_pf* h, int32_t on) {

@@ -114,4 +114,49 @@ enum : int {
     kFlagWords = 8,
 };
 
+// Closed-form log-sum sums of one step (likelihood_lanes, iso): S_ll = sum |l|^2,
+// S_l = sum l, S_zz = sum |z|^2, S_z = sum z, D = sum z.l, E = sum (z_y l_x - z_x l_y),
+// each a double-double (hi, lo) -- exact products, compensated sums.  The same
+// operations on the host (observations loaded from the caller) and on the
+// device (observations simulated there).
+struct DDSum {
+    double h = 0.0, l = 0.0;
+    __host__ __device__ void add(const double bh, const double bl = 0.0) {
+        const double t = h + bh;
+        const double bb = t - h;
+        const double e = ((h - (t - bb)) + (bh - bb)) + (l + bl);
+        h = t + e;
+        l = e - (h - t);
+    }
+    __host__ __device__ void add_prod(const double a, const double b) {
+        const double p = a * b;
+        add(p, fma(a, b, -p));
+    }
+};
+
+__host__ __device__ inline void closed_sums(const double* lm, const double* z, const int32_t nl,
+                                            double* out) {
+    DDSum Sll, Slx, Sly, Szz, Szx, Szy, D, E;
+    for (int32_t j = 0; j < nl; ++j) {
+        const double lx = lm[2 * j], ly = lm[2 * j + 1], zx = z[2 * j], zy = z[2 * j + 1];
+        Sll.add_prod(lx, lx);
+        Sll.add_prod(ly, ly);
+        Slx.add(lx);
+        Sly.add(ly);
+        Szz.add_prod(zx, zx);
+        Szz.add_prod(zy, zy);
+        Szx.add(zx);
+        Szy.add(zy);
+        D.add_prod(zx, lx);
+        D.add_prod(zy, ly);
+        E.add_prod(zy, lx);
+        E.add_prod(-zx, ly);
+    }
+    const DDSum* v[8] = {&Sll, &Slx, &Sly, &Szz, &Szx, &Szy, &D, &E};
+    for (int k = 0; k < 8; ++k) {
+        out[2 * k] = v[k]->h;
+        out[2 * k + 1] = v[k]->l;
+    }
+}
+
 }  // namespace slam

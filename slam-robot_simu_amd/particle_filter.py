@@ -12,6 +12,12 @@ Noise streams
       reference's order -- [rand() if resampling] -> mvn(0, Q, NP) ->
       observation noise -- so a seeded run reproduces the reference's
       trajectory (tests/test_gpu_pf.py).
+  noise="mt19937": the same NumPy stream, drawn on the GPU: the device holds
+      np.random's MT19937 state and draws rand() / mvn(0, Q, NP) / mvn(0, R,
+      NL) itself, observing the landmarks from the true pose there; only the
+      2.5 KB state crosses the boundary (taken from np.random before a step
+      when the host changed it, handed back after), so the global stream
+      continues exactly as the reference's would.
   noise="device": Philox-4x32-10 on the GPU (no per-step host->device
       noise traffic); statistically equivalent, not stream-identical.
 """
@@ -41,14 +47,15 @@ class ParticleFilter(object):
         self.Q = np.diag([0.03, 0.03, np.deg2rad(2.0)]) ** 2        # :62-65
         self.R = np.diag([0.3, 0.3]) ** 2                          # :68-70
         self.x_true = np.array([[self.radius], [0.0], [np.deg2rad(90.0)]])   # :74-79
-        if noise not in ("numpy", "device"):
-            raise ValueError("noise must be 'numpy' or 'device'")
+        if noise not in ("numpy", "mt19937", "device"):
+            raise ValueError("noise must be 'numpy', 'mt19937' or 'device'")
         self.noise = noise
         self.motion = motion
         self.alphas = tuple(alphas)
         self.dev = DeviceParticleFilter(
             self.n_particles, self.lm, dt=self.dt, q=self.Q, r=self.R, x0=self.x_true[:, 0],
             motion=motion, likelihood=likelihood, alphas=alphas, seed=seed, device=device)
+        self._rng_seen = None
 
     # ------------------------------------------------------------- world
     def _truth_step(self, x):
@@ -83,9 +90,29 @@ class ParticleFilter(object):
         out = self.dev.step(control, observations, noise, u_resample)
         return out["x_est"].reshape(3, 1), out["cov"]
 
+    def _rng_to_device(self):
+        """np.random's state -> the device stream, unless it is the one the
+        device handed back last step (nothing drew from np.random since)."""
+        cur = np.random.get_state()
+        seen = self._rng_seen
+        if (seen is None or cur[2:] != seen[2:] or not np.array_equal(cur[1], seen[1])):
+            self.dev.use_numpy_stream(cur)
+
+    def _rng_from_device(self):
+        st = self.dev.rng_state()
+        np.random.set_state(st)
+        self._rng_seen = st
+
     def main_pf(self):
         """particle_filter.py:86-119 -> (LM, x_true, x_est, px, Q, max_idx, max_val)."""
         self.x_true = self._truth_step(self.x_true)
+        if self.noise == "mt19937":
+            self._rng_to_device()
+            out = self.dev.step_truth((self.vel, self.yaw_rate), self.x_true)
+            self._rng_from_device()
+            x, y, th, _ = self.dev.get_state()
+            return (self.lm, self.x_true, out["x_est"].reshape(3, 1), np.vstack([x, y, th]),
+                    self.Q, out["max_idx"], out["max_val"])
         if self.noise == "numpy":
             u = np.random.rand() if self.dev.resample_next else float("nan")
             noise = self._draw_noise()

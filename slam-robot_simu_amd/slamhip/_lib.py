@@ -67,6 +67,7 @@ _P = C.c_void_p
 _D = C.POINTER(C.c_double)
 _I64 = C.POINTER(C.c_int64)
 _I32 = C.POINTER(C.c_int32)
+_U32 = C.POINTER(C.c_uint32)
 
 # name -> (restype, argtypes)
 SIGNATURES = {
@@ -98,6 +99,17 @@ SIGNATURES = {
                                    C.c_int]),
     "slam_scan_noise": (C.c_int, [C.c_int64, _D, _D, C.c_double, C.c_double, C.c_double, _D, C.c_int]),
     "slam_error_ellipse": (C.c_int, [C.c_int64, _D, C.c_double, C.c_int32, _D, C.c_int]),
+    "slam_mt_create": (C.c_int, [_U32, C.c_int32, C.c_int32, C.c_double, C.c_int, C.POINTER(_P)]),
+    "slam_mt_destroy": (C.c_int, [_P]),
+    "slam_mt_set_state": (C.c_int, [_P, _U32, C.c_int32, C.c_int32, C.c_double]),
+    "slam_mt_get_state": (C.c_int, [_P, _U32, _I32, _I32, _D]),
+    "slam_mt_random_sample": (C.c_int, [_P, C.c_int64, _D]),
+    "slam_mt_standard_normal": (C.c_int, [_P, C.c_int64, _D]),
+    "slam_glibc_log": (C.c_int, [C.c_int64, _D, _D]),
+    "slam_pf_set_rng_mt19937": (C.c_int, [_P, _U32, C.c_int32, C.c_int32, C.c_double, _D]),
+    "slam_pf_get_rng_mt19937": (C.c_int, [_P, _U32, _I32, _I32, _D]),
+    "slam_pf_step_truth": (C.c_int, [_P, _D, _D, _D, C.POINTER(PFResult)]),
+    "slam_pf_load_truth": (C.c_int, [_P, C.c_int32, _D]),
     "slam_comm_unique_id": (C.c_int, [C.c_char_p]),
     "slam_comm_create": (C.c_int, [C.c_char_p, C.c_int32, C.c_int32, C.c_int, C.POINTER(_P)]),
     "slam_comm_destroy": (C.c_int, [_P]),

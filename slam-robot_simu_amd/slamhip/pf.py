@@ -11,6 +11,9 @@ import numpy as np
 
 from . import _lib
 from ._lib import PFConfig, PFResult, check, dptr
+from .rng import state_fields
+
+BASE_ANG = np.pi / 2.0          # mylib/transform.py:12
 
 
 def _f64(a, shape=None):
@@ -60,6 +63,8 @@ class DeviceParticleFilter:
                           alphas=alphas, ess_threshold=ess_threshold, seed=seed)
         self.motion = motion
         self.cfg = cfg
+        self.r = np.diag([0.3, 0.3]) ** 2 if r is None else np.asarray(r, float)
+        self.mt = False
         h = C.c_void_p()
         check(lib.slam_pf_create(C.byref(cfg), self.n, self.nl, dptr(self.lm), int(device),
                                  C.byref(h)), "slam_pf_create")
@@ -176,6 +181,59 @@ class DeviceParticleFilter:
               "slam_pf_run")
         self.resample_next = bool(res[k - 1].resample_next)
         return [self._res(r) for r in res] if want_results else None
+
+    # ------------------------------------------------ NumPy stream on device
+    def use_numpy_stream(self, state=None):
+        """Draw the reference's noise from NumPy's RandomState stream on the
+        device, starting from `state` (np.random's global state when None):
+        each step then draws [rand() if resampling] -> mvn(0, Q, NP) ->
+        mvn(0, R, NL) in the reference's order (particle_filter.py:214, :165,
+        :152) and observes the landmarks from the true pose on the device."""
+        key, pos, hg, g = state_fields(state)
+        rf = _f64(numpy_noise_factor(self.r))
+        check(self._lib.slam_pf_set_rng_mt19937(self._h, key.ctypes.data_as(_lib._U32), pos, hg, g,
+                                                dptr(rf)), "slam_pf_set_rng_mt19937")
+        self.mt = True
+
+    def rng_state(self):
+        """The device stream's state as an np.random.get_state() tuple."""
+        key = np.empty(624, dtype=np.uint32)
+        pos, hg, g = C.c_int32(0), C.c_int32(0), C.c_double(0.0)
+        check(self._lib.slam_pf_get_rng_mt19937(self._h, key.ctypes.data_as(_lib._U32), C.byref(pos),
+                                                C.byref(hg), C.byref(g)), "slam_pf_get_rng_mt19937")
+        return ("MT19937", key, pos.value, hg.value, g.value)
+
+    @staticmethod
+    def truth_input(x_true):
+        """(x, y, cos, sin) of a (3, 1) true pose as world2robot forms them
+        (mylib/transform.py:31-35)."""
+        x_true = np.asarray(x_true, dtype=np.float64).reshape(3, 1)
+        yaw = BASE_ANG - x_true[2, 0]
+        return np.array([x_true[0, 0], x_true[1, 0], np.cos(yaw), np.sin(yaw)])
+
+    def step_truth(self, control, x_true, want_z=False):
+        """One step with the device stream: the observation of x_true is
+        simulated on the device (z returned with want_z)."""
+        ctl = _f64(control, (2,))
+        t4 = self.truth_input(x_true)
+        z = np.empty((self.nl, 2)) if want_z else None
+        res = PFResult()
+        check(self._lib.slam_pf_step_truth(self._h, dptr(ctl), dptr(t4), dptr(z), C.byref(res)),
+              "slam_pf_step_truth")
+        out = self._res(res)
+        if want_z:
+            out["z"] = z
+        self.resample_next = out["resample_next"]
+        self.last = out
+        return out
+
+    def load_truth(self, poses):
+        """True poses [k][3] of a device-resident batch (run() then simulates
+        every step's observation on the device)."""
+        poses = _f64(poses).reshape(-1, 3)
+        t4 = np.ascontiguousarray(np.stack([self.truth_input(p) for p in poses]))
+        check(self._lib.slam_pf_load_truth(self._h, t4.shape[0], dptr(t4)), "slam_pf_load_truth")
+        self._truth_steps = t4.shape[0]
 
     def set_scan_merged(self, on=True):
         """Exact cumsum of a resample step in one launch (default where the
