@@ -64,6 +64,7 @@ def simulate_world(n_steps, seed=1):
     r = np.diag([0.3, 0.3]) ** 2
     x = np.array([[10.0], [0.0], [np.pi / 2]])
     zs = np.empty((n_steps, NL, 2))
+    poses = np.empty((n_steps, 3))
     for k in range(n_steps):
         a = vel / omega
         b = limit.limit_angle(omega * dt)
@@ -71,6 +72,8 @@ def simulate_world(n_steps, seed=1):
         x = np.array([[x[0, 0] + a * (-np.sin(x[2, 0]) + np.sin(y2))],
                       [x[1, 0] + a * (np.cos(x[2, 0]) - np.cos(y2))], [y2]])
         zs[k] = tf.world2robot(x, lm) + rs.multivariate_normal([0.0, 0.0], r, NL)
+        poses[k] = x[:, 0]
+    simulate_world.poses = poses
     return lm, zs, (vel, omega, dt)
 
 
@@ -513,6 +516,24 @@ def main():
         pf.close()
         return elapsed, out, timing
 
+    def measure_numpy_stream(likelihood):
+        # parity mode on the device: NumPy's RandomState stream drawn there
+        # (rand / mvn(Q, NP) / mvn(R, NL) per step, bit-identical to the
+        # reference's draws) and the observations simulated from the true pose
+        pf = DeviceParticleFilter(NP_PER_GPU, lm, dt=dt, motion="velocity",
+                                  likelihood=likelihood, seed=1234, device=local_rank)
+        pf.use_numpy_stream(np.random.RandomState(1234))
+        pf.load_truth(simulate_world.poses)
+        if args.warmup:
+            pf.run(0, ctl[:args.warmup], want_results=False)
+        barrier_sync()
+        t0 = time.perf_counter()
+        pf.run(args.warmup, ctl[args.warmup:args.warmup + args.steps])
+        barrier_sync()
+        el = time.perf_counter() - t0
+        pf.close()
+        return el
+
     elapsed, out, timing = measure(args.likelihood)
     fused_ms, fused_n = timing[0]
     red_ms, red_n = timing[1]
@@ -583,6 +604,11 @@ def main():
         e2, _, t2 = measure("product")
         line["alt_modes"] = {"product": {"value": NP_PER_GPU * NL * args.steps / e2,
                                          "fused_avg_ms": t2[0][0] / max(t2[0][1], 1)}}
+        e4 = measure_numpy_stream(args.likelihood)
+        line["alt_modes"]["numpy_stream"] = {
+            "value": NP_PER_GPU * NL * args.steps / e4, "ms_per_step": e4 * 1e3 / args.steps,
+            "note": "the reference's own noise stream (MT19937 + polar normals, bit-identical to "
+                    "np.random) drawn on the device with the observations simulated there"}
     if world == 1 and args.mode == "replicas":
         # the sharded step's kernels on one shard (its overhead over the single handle)
         e3, _, t3 = measure_sharded(args.likelihood)

@@ -419,7 +419,7 @@ int launch_reduce(slam_pf* h, int32_t resampled_known) {
 // world2robot (mylib/transform.py:31-35: the 2x2 rotation through OpenBLAS's
 // fused dgemm) plus the mvn(0, R) noise of normals [n3, n3 + 2 NL) (x @ M,
 // dgemm order); then the step's closed-form log-sum sums (iso handles).
-__global__ __launch_bounds__(256) void pf_mt_observe_kernel(
+__global__ __launch_bounds__(512) void pf_mt_observe_kernel(
     const double* __restrict__ normals, const int64_t n3, const double* __restrict__ lm,
     const int32_t nl, const double* __restrict__ truth, const int32_t* __restrict__ ctr,
     const double r0, const double r1, const double r2, const double r3, double* __restrict__ z_all,
@@ -439,9 +439,18 @@ __global__ __launch_bounds__(256) void pf_mt_observe_kernel(
         z[2 * l + 1] = zy;
         s_z[2 * l] = zx;
         s_z[2 * l + 1] = zy;
+        s_z[2 * (nl + l)] = lm[2 * l];          // the sums read both from LDS
+        s_z[2 * (nl + l) + 1] = lm[2 * l + 1];
     }
     __syncthreads();
-    if (closed && threadIdx.x == 0) closed_sums(lm, s_z, nl, zc + (size_t)st * kClosedWords);
+    // one component per wave (lane 0): the eight compensated sums run side by
+    // side without divergence
+    const int k = threadIdx.x >> 6;
+    if (closed && (threadIdx.x & 63) == 0 && k < 8) {
+        const DDSum S = closed_sum_component(k, s_z + 2 * nl, s_z, nl);
+        zc[(size_t)st * kClosedWords + 2 * k] = S.h;
+        zc[(size_t)st * kClosedWords + 2 * k + 1] = S.l;
+    }
 }
 
 // mvn(0, Q, NP) (particle_filter.py:165): noise = normals @ M, OpenBLAS's order
@@ -464,7 +473,7 @@ int launch_mt(slam_pf* h) {
                         n3 + 2 * (int64_t)h->nl, h->flags + kFlagStatus, h->stream);
     if (rc) return rc;
     if (h->nl > 0)
-        pf_mt_observe_kernel<<<1, 256, 16 * (size_t)h->nl, h->stream>>>(
+        pf_mt_observe_kernel<<<1, 512, 32 * (size_t)h->nl, h->stream>>>(
             h->mtb.normals, n3, h->lm, h->nl, h->truth, h->ctr, h->mr[0], h->mr[1], h->mr[2],
             h->mr[3], h->z_all, h->zc, h->lc.closed);
     if (h->cfg.motion == SLAM_MOTION_LINEAR)
@@ -1051,7 +1060,7 @@ int slam_pf_set_rng_mt19937(slam_pf* h, const uint32_t* key, int32_t pos, int32_
                             double gauss, const double* r_factor) {
     SLAM_ARG_CHECK(h && key && r_factor, "slam_pf_set_rng_mt19937: NULL argument");
     SLAM_ARG_CHECK(h->n == h->n_global, "slam_pf_set_rng_mt19937: sharded handle");
-    SLAM_ARG_CHECK(h->nl <= 4096, "slam_pf_set_rng_mt19937: at most 4096 landmarks");
+    SLAM_ARG_CHECK(h->nl <= 2048, "slam_pf_set_rng_mt19937: at most 2048 landmarks");
     SLAM_HIP_TRY(hipSetDevice(h->device));
     SLAM_HIP_TRY(hipStreamSynchronize(h->stream));
     int rc = mt_reserve(h->mtb, 3 * h->n + 2 * (int64_t)h->nl, 1, h->device);

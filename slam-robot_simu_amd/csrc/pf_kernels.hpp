@@ -134,28 +134,34 @@ struct DDSum {
     }
 };
 
-__host__ __device__ inline void closed_sums(const double* lm, const double* z, const int32_t nl,
-                                            double* out) {
-    DDSum Sll, Slx, Sly, Szz, Szx, Szy, D, E;
+// component k of the sums (0 S_ll, 1 S_lx, 2 S_ly, 3 S_zz, 4 S_zx, 5 S_zy, 6 D,
+// 7 E): each is its own compensated sum in landmark order, so the eight can be
+// formed independently (one lane each on the device)
+__host__ __device__ inline DDSum closed_sum_component(const int k, const double* lm,
+                                                      const double* z, const int32_t nl) {
+    DDSum S;
     for (int32_t j = 0; j < nl; ++j) {
         const double lx = lm[2 * j], ly = lm[2 * j + 1], zx = z[2 * j], zy = z[2 * j + 1];
-        Sll.add_prod(lx, lx);
-        Sll.add_prod(ly, ly);
-        Slx.add(lx);
-        Sly.add(ly);
-        Szz.add_prod(zx, zx);
-        Szz.add_prod(zy, zy);
-        Szx.add(zx);
-        Szy.add(zy);
-        D.add_prod(zx, lx);
-        D.add_prod(zy, ly);
-        E.add_prod(zy, lx);
-        E.add_prod(-zx, ly);
+        switch (k) {
+            case 0: S.add_prod(lx, lx); S.add_prod(ly, ly); break;
+            case 1: S.add(lx); break;
+            case 2: S.add(ly); break;
+            case 3: S.add_prod(zx, zx); S.add_prod(zy, zy); break;
+            case 4: S.add(zx); break;
+            case 5: S.add(zy); break;
+            case 6: S.add_prod(zx, lx); S.add_prod(zy, ly); break;
+            default: S.add_prod(zy, lx); S.add_prod(-zx, ly); break;
+        }
     }
-    const DDSum* v[8] = {&Sll, &Slx, &Sly, &Szz, &Szx, &Szy, &D, &E};
+    return S;
+}
+
+__host__ __device__ inline void closed_sums(const double* lm, const double* z, const int32_t nl,
+                                            double* out) {
     for (int k = 0; k < 8; ++k) {
-        out[2 * k] = v[k]->h;
-        out[2 * k + 1] = v[k]->l;
+        const DDSum S = closed_sum_component(k, lm, z, nl);
+        out[2 * k] = S.h;
+        out[2 * k + 1] = S.l;
     }
 }
 

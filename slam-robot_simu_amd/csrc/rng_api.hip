@@ -2,8 +2,8 @@
 //
 // A request (mt_enqueue) is five launches, none of which needs the host:
 //   mt_gen_kernel     one workgroup: the untempered MT19937 sequence from the
-//                     current key, 624 words per block in three dependent
-//                     phases of <= 227 lanes (X[n+624] needs X[n+397]);
+//                     current key, one block of 624 words per barrier (every
+//                     word expanded from the previous block alone);
 //   mt_count_kernel   per candidate pair (4 words): the polar test
 //                     0 < x1^2 + x2^2 < 1, accepted candidates per block;
 //   mt_scan_kernel    exclusive prefix of the block counts;
@@ -27,13 +27,35 @@
 
 namespace slam {
 
-constexpr int kMtGenThreads = 256;
+constexpr int kMtGenThreads = 640;   // one lane per word of a block
 constexpr int kMtCandPerThread = 4;
 constexpr int kMtCountThreads = 256;
 constexpr int kMtCandPerBlock = kMtCountThreads * kMtCandPerThread;
 constexpr int kMtScanThreads = 1024;
 
 // ------------------------------------------------------------------ kernels
+
+// word i of the block after A, from A alone: the words it needs from its own
+// block (X[n + 397] for i >= 227) are expanded through the recurrence, so a
+// block is one parallel phase (one barrier) instead of three dependent ones
+__device__ __forceinline__ uint32_t mt_block_word(const uint32_t* A, const int i) {
+    constexpr int D = kMtN - kMtM;   // 227
+    if (i < D) return mt_next(A[i], A[i + 1], A[i + kMtM]);
+    if (i < 2 * D) {
+        const int j = i - D;
+        return mt_next(A[i], A[i + 1], mt_next(A[j], A[j + 1], A[j + kMtM]));
+    }
+    if (i < kMtN - 1) {
+        const int j = i - D, k = j - D;
+        const uint32_t p1 = mt_next(A[k], A[k + 1], A[k + kMtM]);
+        return mt_next(A[i], A[i + 1], mt_next(A[j], A[j + 1], p1));
+    }
+    // i = 623: X[n + 1] is the new block's word 0, X[n + 397] its word 396
+    const uint32_t w0 = mt_next(A[0], A[1], A[kMtM]);
+    const int k = kMtM - 1 - D;      // 169
+    const uint32_t w396 = mt_next(A[kMtM - 1], A[kMtM], mt_next(A[k], A[k + 1], A[k + kMtM]));
+    return mt_next(A[kMtN - 1], w0, w396);
+}
 
 __global__ __launch_bounds__(kMtGenThreads) void mt_gen_kernel(const MtDeviceState* __restrict__ st,
                                                                uint32_t* __restrict__ X,
@@ -51,27 +73,14 @@ __global__ __launch_bounds__(kMtGenThreads) void mt_gen_kernel(const MtDeviceSta
         const uint32_t* A = buf[a];
         uint32_t* Bn = buf[a ^ 1];
         uint32_t* out = X + b * kMtN;
-        if (t < kMtN - kMtM) {                                  // i in [0, 227): old block only
-            const uint32_t v = mt_next(A[t], A[t + 1], A[t + kMtM]);
+        if (t < kMtN) {
+            const uint32_t v = mt_block_word(A, t);
             Bn[t] = v;
             out[t] = v;
         }
-        __syncthreads();
-        if (t < kMtN - kMtM) {                                  // [227, 454)
-            const int i = t + (kMtN - kMtM);
-            const uint32_t v = mt_next(A[i], A[i + 1], Bn[i - (kMtN - kMtM)]);
-            Bn[i] = v;
-            out[i] = v;
-        }
-        __syncthreads();
-        if (t < kMtN - 2 * (kMtN - kMtM)) {                      // [454, 624)
-            const int i = t + 2 * (kMtN - kMtM);
-            const uint32_t nx = (i == kMtN - 1) ? Bn[0] : A[i + 1];
-            const uint32_t v = mt_next(A[i], nx, Bn[i - (kMtN - kMtM)]);
-            Bn[i] = v;
-            out[i] = v;
-        }
-        __syncthreads();
+        // LDS-only barrier: __syncthreads() would also wait for the global
+        // stores of the block (a full store round trip per block)
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
         a ^= 1;
     }
 }
