@@ -437,6 +437,10 @@ int slam_mt_get_state(slam_mt* h, uint32_t* key, int32_t* pos, int32_t* has_gaus
 /* RandomState.random_sample(n) / standard_normal(n) into host arrays */
 int slam_mt_random_sample(slam_mt* h, int64_t n, double* out);
 int slam_mt_standard_normal(slam_mt* h, int64_t n, double* out);
+/* jump-ahead (host): the 624-word window n_words further along the stream
+ * than `window` (word 0's low 31 bits are not part of the MT19937 state and
+ * come back unspecified) -- x^n mod the MT19937 characteristic polynomial */
+int slam_mt_jump_window(const uint32_t* window, uint64_t n_words, uint32_t* out);
 /* glibc's log restated (host; the function the device kernels evaluate) */
 int slam_glibc_log(int64_t n, const double* x, double* out);
 

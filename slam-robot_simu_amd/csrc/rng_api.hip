@@ -1,9 +1,11 @@
 // rng_api.hip -- NumPy's legacy RandomState stream on the device (mt19937.hpp).
 //
 // A request (mt_enqueue) is five launches, none of which needs the host:
-//   mt_gen_kernel     one workgroup: the untempered MT19937 sequence from the
-//                     current key, one block of 624 words per barrier (every
-//                     word expanded from the previous block alone);
+//   mt_round_kernel   when fewer words than a request can read lie ahead: R
+//                     workgroups each generate S words of the untempered
+//                     MT19937 sequence (one 624-word block per barrier) from
+//                     their segment's pre-window, then jump that pre-window
+//                     R S words ahead (mt_stream.hpp);
 //   mt_count_kernel   per candidate pair (4 words): the polar test
 //                     0 < x1^2 + x2^2 < 1, accepted candidates per block;
 //   mt_scan_kernel    exclusive prefix of the block counts;
@@ -16,6 +18,7 @@
 // f x2 and caches f x1; random_sample takes two words per double.
 #include <dlfcn.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -57,45 +60,126 @@ __device__ __forceinline__ uint32_t mt_block_word(const uint32_t* A, const int i
     return mt_next(A[kMtN - 1], w0, w396);
 }
 
-__global__ __launch_bounds__(kMtGenThreads) void mt_gen_kernel(const MtDeviceState* __restrict__ st,
-                                                               uint32_t* __restrict__ X,
-                                                               const int64_t nblk) {
+// LDS-only barrier: __syncthreads() would also wait for the ring stores of the
+// block (a full store round trip per 624 words)
+__device__ __forceinline__ void mt_lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+// One round: segment r (workgroup r) = stream words [g1 + r S, g1 + (r + 1) S),
+// generated from its pre-window seg[r]; then seg[r] <- the pre-window one round
+// later (R > 1: jump-ahead by R S; R = 1: the segment's last block).  Runs only
+// when fewer than `need` words lie ahead of the position.
+__global__ __launch_bounds__(kMtGenThreads) void mt_round_kernel(
+    const MtDeviceState* __restrict__ st, uint32_t* __restrict__ X, const int64_t cap,
+    uint32_t* __restrict__ seg, const uint32_t* __restrict__ q_idx, const int32_t n_idx,
+    const int64_t S, const int32_t R, const int64_t need) {
+    extern __shared__ uint32_t sm[];
+    const int64_t p = st->p, g1 = st->g1;
+    if (g1 - p >= need) return;
+    uint32_t* Wl = sm + 2 * kMtN;                       // Y[0 .. kMtConvWords] (R > 1)
+    const int t = threadIdx.x;
+    const int64_t m = g1 + (int64_t)blockIdx.x * S;     // the segment's first word
+    uint32_t* sg = seg + (size_t)blockIdx.x * kMtN;
+    // Y[0..623] = the pre-window (stream words m - 1 ...); stream word m + k = Y[k + 1]
+    if (t < kMtN) {
+        const uint32_t v = sg[t];
+        sm[t] = v;
+        if (R > 1) {
+            Wl[t] = v;
+            Wl[kMtConvWords + 1 + t] = 0u;              // the padding offset's window
+        }
+        if (t >= 1) X[(m + t - 1) & (cap - 1)] = v;
+    }
+    __syncthreads();
+    const int64_t K = S / kMtN;
+    int a = 0;
+    for (int64_t b = 1; b <= K; ++b) {
+        if (t < kMtN) {
+            const uint32_t v = mt_block_word(sm + a * kMtN, t);
+            sm[(a ^ 1) * kMtN + t] = v;
+            const int64_t y = b * kMtN + t;
+            if (y <= S) X[(m + y - 1) & (cap - 1)] = v;
+            if (R > 1 && y < kMtConvWords + 1) Wl[y] = v;
+        }
+        mt_lds_barrier();
+        a ^= 1;
+    }
+    if (t >= kMtN) return;
+    if (R == 1) {
+        sg[t] = sm[a * kMtN + t];                       // Y[S .. S + 623]
+        return;
+    }
+    // pre-window R S words on: word j = XOR over the set bits i of q of Y[i + j]
+    // (q's set bits as a list of 16-bit offsets, padded with an offset that
+    // lands in the zero tail of Wl; 16 LDS reads in flight per round)
+    uint32_t acc = 0;
+    for (int k = 0; k < n_idx; k += 16) {
+        uint32_t v[16];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const uint32_t pr = q_idx[k / 2 + u];
+            v[2 * u] = Wl[(pr & 0xffffu) + t];
+            v[2 * u + 1] = Wl[(pr >> 16) + t];
+        }
+#pragma unroll
+        for (int u = 0; u < 16; ++u) acc ^= v[u];
+    }
+    sg[t] = acc;
+}
+
+// Set-state priming: stream words [0, 624 + R S + 624) from the key in one
+// workgroup, so that every segment's first pre-window can be read off.
+__global__ __launch_bounds__(kMtGenThreads) void mt_prime_kernel(const uint32_t* __restrict__ key,
+                                                                 uint32_t* __restrict__ X,
+                                                                 const int64_t cap,
+                                                                 const int64_t nblk) {
     __shared__ uint32_t buf[2][kMtN];
     const int t = threadIdx.x;
-    for (int i = t; i < kMtN; i += kMtGenThreads) {
-        const uint32_t v = st->key[i];
-        buf[0][i] = v;
-        X[i] = v;
+    if (t < kMtN) {
+        const uint32_t v = key[t];
+        buf[0][t] = v;
+        X[t] = v;
     }
     __syncthreads();
     int a = 0;
     for (int64_t b = 1; b <= nblk; ++b) {
-        const uint32_t* A = buf[a];
-        uint32_t* Bn = buf[a ^ 1];
-        uint32_t* out = X + b * kMtN;
         if (t < kMtN) {
-            const uint32_t v = mt_block_word(A, t);
-            Bn[t] = v;
-            out[t] = v;
+            const uint32_t v = mt_block_word(buf[a], t);
+            buf[a ^ 1][t] = v;
+            X[(b * kMtN + t) & (cap - 1)] = v;
         }
-        // LDS-only barrier: __syncthreads() would also wait for the global
-        // stores of the block (a full store round trip per block)
-        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        mt_lds_barrier();
         a ^= 1;
     }
+}
+
+// seg[r] <- stream words [623 + r S, 623 + r S + 624) (the first round's pre-windows)
+__global__ void mt_seed_segments_kernel(const uint32_t* __restrict__ X, const int64_t cap,
+                                        uint32_t* __restrict__ seg, const int64_t S) {
+    const int r = blockIdx.x;
+    for (int j = threadIdx.x; j < kMtN; j += blockDim.x)
+        seg[(size_t)r * kMtN + j] = X[(kMtN - 1 + (int64_t)r * S + j) & (cap - 1)];
 }
 
 __device__ __forceinline__ int64_t mt_pre_words(const int32_t* pre_flag, const int64_t n_pre) {
     return pre_flag ? (*pre_flag ? 2 : 0) : 2 * n_pre;
 }
 
-// candidate c: words X[w], ..., X[w + 3] (two legacy doubles)
+__device__ __forceinline__ uint32_t mt_word(const uint32_t* __restrict__ X, const int64_t k,
+                                            const int64_t cap) {
+    return mt_temper(X[k & (cap - 1)]);
+}
+
+// candidate pair at stream word w: words w .. w + 3 (two legacy doubles)
 __device__ __forceinline__ bool mt_candidate(const uint32_t* __restrict__ X, const int64_t w,
-                                             double& x1, double& x2, double& r2) {
-    const uint32_t w0 = mt_temper(X[w]), w1 = mt_temper(X[w + 1]);
-    const uint32_t w2 = mt_temper(X[w + 2]), w3 = mt_temper(X[w + 3]);
-    x1 = 2.0 * mt_legacy_double(w0, w1) - 1.0;
-    x2 = 2.0 * mt_legacy_double(w2, w3) - 1.0;
+                                             const int64_t cap, double& x1, double& x2,
+                                             double& r2) {
+    uint32_t v[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = mt_temper(X[(w + j) & (cap - 1)]);
+    x1 = 2.0 * mt_legacy_double(v[0], v[1]) - 1.0;
+    x2 = 2.0 * mt_legacy_double(v[2], v[3]) - 1.0;
     r2 = x1 * x1 + x2 * x2;
     return !(r2 >= 1.0 || r2 == 0.0);
 }
@@ -127,21 +211,26 @@ __device__ __forceinline__ int mt_block_scan(int v, int* tot) {
 }
 
 __global__ __launch_bounds__(kMtCountThreads) void mt_count_kernel(
-    const MtDeviceState* __restrict__ st, const uint32_t* __restrict__ X,
+    MtDeviceState* __restrict__ st, const uint32_t* __restrict__ X, const int64_t cap,
     const int32_t* __restrict__ pre_flag, const int64_t n_pre, const int64_t ncand,
-    unsigned* __restrict__ bcnt) {
-    const int64_t w0 = st->pos + mt_pre_words(pre_flag, n_pre);
+    unsigned* __restrict__ bcnt, const int64_t round_words, const int64_t need) {
+    const int64_t p = st->p;
+    const int64_t w0 = p + mt_pre_words(pre_flag, n_pre);
     const int64_t c0 = (int64_t)blockIdx.x * kMtCandPerBlock + threadIdx.x * kMtCandPerThread;
     int cnt = 0;
 #pragma unroll
     for (int k = 0; k < kMtCandPerThread; ++k) {
         const int64_t c = c0 + k;
         double x1, x2, r2;
-        if (c < ncand && mt_candidate(X, w0 + 4 * c, x1, x2, r2)) ++cnt;
+        if (c < ncand && mt_candidate(X, w0 + 4 * c, cap, x1, x2, r2)) ++cnt;
     }
     int tot;
     (void)mt_block_scan(cnt, &tot);
-    if (threadIdx.x == 0) bcnt[blockIdx.x] = (unsigned)tot;
+    if (threadIdx.x == 0) {
+        bcnt[blockIdx.x] = (unsigned)tot;
+        // the round launched before this pass generated R S words if it ran
+        if (blockIdx.x == 0 && st->g1 - p < need) st->g1 += round_words;
+    }
 }
 
 __global__ __launch_bounds__(kMtScanThreads) void mt_scan_kernel(
@@ -181,12 +270,12 @@ __global__ __launch_bounds__(kMtScanThreads) void mt_scan_kernel(
 }
 
 __global__ __launch_bounds__(kMtCountThreads) void mt_emit_kernel(
-    MtDeviceState* __restrict__ st, const uint32_t* __restrict__ X,
+    MtDeviceState* __restrict__ st, const uint32_t* __restrict__ X, const int64_t cap,
     const int32_t* __restrict__ pre_flag, const int64_t n_pre, const int64_t ncand,
     const int64_t* __restrict__ boff, const int64_t g, const GlibcLogTable* __restrict__ tab,
     double* __restrict__ normals) {
     const int64_t pw = mt_pre_words(pre_flag, n_pre);
-    const int64_t w0 = st->pos + pw;
+    const int64_t w0 = st->p + pw;
     const int h = st->has_gauss ? 1 : 0;
     const int64_t P = mt_pairs(st, g);
     const int64_t c0 = (int64_t)blockIdx.x * kMtCandPerBlock + threadIdx.x * kMtCandPerThread;
@@ -196,7 +285,7 @@ __global__ __launch_bounds__(kMtCountThreads) void mt_emit_kernel(
 #pragma unroll
     for (int k = 0; k < kMtCandPerThread; ++k) {
         const int64_t c = c0 + k;
-        acc[k] = c < ncand && mt_candidate(X, w0 + 4 * c, x1[k], x2[k], r2[k]);
+        acc[k] = c < ncand && mt_candidate(X, w0 + 4 * c, cap, x1[k], x2[k], r2[k]);
         cnt += acc[k] ? 1 : 0;
     }
     int tot;
@@ -219,44 +308,30 @@ __global__ __launch_bounds__(kMtCountThreads) void mt_emit_kernel(
 }
 
 __global__ __launch_bounds__(kMtGenThreads) void mt_finish_kernel(
-    MtDeviceState* __restrict__ st, const uint32_t* __restrict__ X,
+    MtDeviceState* __restrict__ st, const uint32_t* __restrict__ X, const int64_t cap,
     const int32_t* __restrict__ pre_flag, const int64_t n_pre, const double pre_scale,
     double* __restrict__ pre_out, const int32_t* __restrict__ pre_index, const int64_t g,
     double* __restrict__ normals) {
-    __shared__ int64_t s_blk;
-    __shared__ int32_t s_pos;
-    const int64_t p = st->pos;
+    const int64_t p = st->p;
     const int64_t pw = mt_pre_words(pre_flag, n_pre);
     const int h = st->has_gauss ? 1 : 0;
     const int64_t P = mt_pairs(st, g);
-    // pre-draw doubles (random_sample): words X[p + 2k], X[p + 2k + 1]
+    // pre-draw doubles (random_sample): stream words p + 2k, p + 2k + 1
     if (pre_flag) {
         if (threadIdx.x == 0 && pre_out) {
             double* o = pre_out + (pre_index ? *pre_index : 0);
-            *o = *pre_flag ? mt_legacy_double(mt_temper(X[p]), mt_temper(X[p + 1])) * pre_scale
+            *o = *pre_flag ? mt_legacy_double(mt_word(X, p, cap), mt_word(X, p + 1, cap)) * pre_scale
                            : (double)NAN;
         }
     } else if (pre_out) {
         for (int64_t k = threadIdx.x; k < n_pre; k += blockDim.x)
-            pre_out[k] = mt_legacy_double(mt_temper(X[p + 2 * k]), mt_temper(X[p + 2 * k + 1])) *
+            pre_out[k] = mt_legacy_double(mt_word(X, p + 2 * k, cap), mt_word(X, p + 2 * k + 1, cap)) *
                          pre_scale;
     }
+    __syncthreads();                                    // every lane has read st->p
     if (threadIdx.x == 0) {
         if (h && g > 0) normals[0] = st->gauss;
-        const int64_t e = p + (P > 0 ? st->j_end : pw);
-        if (e > 0 && e % kMtN == 0) {                        // NumPy regenerates lazily: pos 624
-            s_blk = e / kMtN - 1;
-            s_pos = kMtN;
-        } else {
-            s_blk = e / kMtN;
-            s_pos = (int32_t)(e % kMtN);
-        }
-    }
-    __syncthreads();
-    const uint32_t* src = X + s_blk * kMtN;
-    for (int i = threadIdx.x; i < kMtN; i += blockDim.x) st->key[i] = src[i];
-    if (threadIdx.x == 0) {
-        st->pos = s_pos;
+        st->p = p + (P > 0 ? st->j_end : pw);
         if (g > 0) {
             const int64_t m = g - h;
             const bool odd = m > 0 && (m & 1);
@@ -279,9 +354,148 @@ int64_t cand_bound(int64_t g) {
     return (int64_t)std::ceil(mean + 12.0 * sd) + 64;
 }
 
-int64_t blocks_for(int64_t pre_words, int64_t ncand) {
-    // pos <= 624; the state after the draw needs the whole block it ends in
-    return (kMtN + pre_words + 4 * ncand) / kMtN + 2;
+// ---- MT19937's characteristic polynomial and jump polynomials (GF(2))
+typedef std::vector<uint64_t> Bits;
+
+inline int bit_of(const Bits& v, size_t i) { return (int)((v[i >> 6] >> (i & 63)) & 1u); }
+
+// dst ^= src << sh (bit shift toward higher degree), dst/src of equal length
+void xor_shifted(Bits& dst, const Bits& src, size_t sh) {
+    const size_t q = sh >> 6, r = sh & 63, W = dst.size();
+    for (size_t w = W; w-- > q;) {
+        uint64_t v = src[w - q] << r;
+        if (r && w >= q + 1) v |= src[w - q - 1] >> (64 - r);
+        dst[w] ^= v;
+    }
+}
+
+// Berlekamp-Massey over GF(2): the minimal polynomial of the bit sequence s
+// as phi(x) = sum_i C_i x^(L - i) (bits 0 .. L), and its degree L.
+Bits berlekamp_massey(const std::vector<uint8_t>& s, int& L_out) {
+    const size_t n = s.size(), W = (n + 127) / 64 + 2;
+    Bits R(W + 2, 0);                                    // reversed sequence
+    for (size_t t = 0; t < n; ++t)
+        if (s[n - 1 - t]) R[t >> 6] |= 1ull << (t & 63);
+    auto window = [&](size_t off, size_t w) -> uint64_t {
+        const size_t bit = off + 64 * w, qq = bit >> 6, rr = bit & 63;
+        const uint64_t lo = qq < R.size() ? R[qq] : 0, hi = qq + 1 < R.size() ? R[qq + 1] : 0;
+        return rr ? (lo >> rr) | (hi << (64 - rr)) : lo;
+    };
+    Bits C(W, 0), B(W, 0), T;
+    C[0] = B[0] = 1;
+    int L = 0;
+    size_t m = 1;
+    for (size_t k = 0; k < n; ++k) {
+        uint64_t acc = 0;                                // s_k + sum_i C_i s_(k-i)
+        for (size_t w = 0; w <= (size_t)L / 64; ++w) acc ^= C[w] & window(n - 1 - k, w);
+        if (!__builtin_parityll(acc)) {
+            ++m;
+            continue;
+        }
+        if ((size_t)2 * L <= k) {
+            T = C;
+            xor_shifted(C, B, m);
+            L = (int)(k + 1) - L;
+            B = T;
+            m = 1;
+        } else {
+            xor_shifted(C, B, m);
+            ++m;
+        }
+    }
+    L_out = L;
+    Bits phi((size_t)L / 64 + 2, 0);
+    for (int i = 0; i <= L; ++i)
+        if (bit_of(C, i)) phi[(size_t)(L - i) >> 6] |= 1ull << ((L - i) & 63);
+    return phi;
+}
+
+struct Gf2Mod {
+    int L = 0;
+    size_t W = 0;                                        // words of a residue
+    Bits phi;
+    void reduce(Bits& r) const {                          // r: 2 W + 2 words, bits >= L cleared
+        for (long bit = (long)(r.size() * 64) - 1; bit >= L; --bit) {
+            if (!((r[(size_t)bit >> 6] >> (bit & 63)) & 1u)) continue;
+            const size_t d = (size_t)bit - (size_t)L;
+            // r ^= phi << d
+            const size_t q = d >> 6, rr = d & 63;
+            for (size_t w = 0; w < phi.size() && w + q < r.size(); ++w) {
+                r[w + q] ^= phi[w] << rr;
+                if (rr && w + q + 1 < r.size()) r[w + q + 1] ^= phi[w] >> (64 - rr);
+            }
+        }
+    }
+    Bits sqr(const Bits& a) const {
+        Bits r(2 * W + 2, 0);
+        for (size_t w = 0; w < W; ++w) {
+            uint64_t lo = 0, hi = 0;
+            for (int k = 0; k < 32; ++k) {
+                lo |= ((a[w] >> k) & 1ull) << (2 * k);
+                hi |= ((a[w] >> (32 + k)) & 1ull) << (2 * k);
+            }
+            r[2 * w] = lo;
+            r[2 * w + 1] = hi;
+        }
+        reduce(r);
+        r.resize(W);
+        return r;
+    }
+    Bits mulx(const Bits& a) const {
+        Bits r(2 * W + 2, 0);
+        for (size_t w = 0; w < W; ++w) {
+            r[w] |= a[w] << 1;
+            r[w + 1] |= a[w] >> 63;
+        }
+        reduce(r);
+        r.resize(W);
+        return r;
+    }
+    Bits xpow(uint64_t E) const {                          // x^E mod phi
+        Bits r(W, 0);
+        r[0] = 1;
+        for (int b = 63; b >= 0; --b) {
+            r = sqr(r);
+            if ((E >> b) & 1u) r = mulx(r);
+        }
+        return r;
+    }
+};
+
+// phi from the most significant bit of the stream of NumPy's default seed
+// (any non-zero state has the same minimal polynomial: phi is irreducible)
+int mt_phi(Gf2Mod& out) {
+    static std::mutex mu;
+    static Gf2Mod G;
+    static bool ok = false;
+    std::lock_guard<std::mutex> lock(mu);
+    if (!ok) {
+        std::vector<uint32_t> X(kMtN);
+        X[0] = 5489u;
+        for (int i = 1; i < kMtN; ++i) X[i] = 1812433253u * (X[i - 1] ^ (X[i - 1] >> 30)) + (uint32_t)i;
+        const size_t n = 2 * (size_t)kMtDeg + 256;
+        X.resize(n);
+        for (size_t k = kMtN; k < n; ++k) X[k] = mt_next(X[k - kMtN], X[k - kMtN + 1], X[k - kMtN + kMtM]);
+        std::vector<uint8_t> s(n);
+        for (size_t k = 0; k < n; ++k) s[k] = (uint8_t)(X[k] >> 31);
+        int L = 0;
+        Bits phi = berlekamp_massey(s, L);
+        if (L != kMtDeg) return fail(SLAM_ERR_ARG, "mt19937: characteristic polynomial of wrong degree");
+        G.L = L;
+        G.W = (size_t)kMtQWords;
+        G.phi = phi;
+        ok = true;
+    }
+    out = G;
+    return SLAM_OK;
+}
+
+int jump_poly(uint64_t J, Bits& q) {
+    Gf2Mod G;
+    const int rc = mt_phi(G);
+    if (rc) return rc;
+    q = G.xpow(J);
+    return SLAM_OK;
 }
 
 typedef double (*log_fn)(double);
@@ -373,53 +587,109 @@ int glibc_log_table(GlibcLogTable* out) {
 }
 
 void mt_free(MtBuffers& b) {
-    void* ps[] = {b.st, b.tab, b.X, b.bcnt, b.boff, b.normals, b.pre};
+    void* ps[] = {b.st, b.tab, b.X, b.seg, b.q, b.bcnt, b.boff, b.normals, b.pre};
     for (void* p : ps)
         if (p) (void)hipFree(p);
     b = MtBuffers{};
 }
+
+namespace {
+
+size_t round_lds_bytes(int32_t R) {
+    return sizeof(uint32_t) * (2 * (size_t)kMtN + (R > 1 ? (size_t)kMtConvWords + 1 + kMtN : 0));
+}
+
+// the first round's pre-windows from the key (one workgroup, R S + 1248 words)
+int mt_prime(const MtBuffers& b, const uint32_t* key_dev, hipStream_t s) {
+    const int64_t nblk = (b.R * b.S + 2 * kMtN) / kMtN + 1;
+    mt_prime_kernel<<<1, kMtGenThreads, 0, s>>>(key_dev, b.X, b.cap, nblk);
+    mt_seed_segments_kernel<<<b.R, 256, 0, s>>>(b.X, b.cap, b.seg, b.S);
+    SLAM_HIP_TRY(hipGetLastError());
+    return SLAM_OK;
+}
+
+}  // namespace
 
 int mt_reserve(MtBuffers& b, int64_t g_cap, int64_t pre_cap, int device) {
     if (b.st && g_cap <= b.g_cap && pre_cap <= b.pre_cap) return SLAM_OK;
     g_cap = std::max<int64_t>(g_cap, b.g_cap);
     pre_cap = std::max<int64_t>(pre_cap, b.pre_cap);
     SLAM_HIP_TRY(hipSetDevice(device));
-    // keep the state across a regrow
-    MtDeviceState keep{};
+    // a regrow keeps the stream where it is
+    std::vector<uint32_t> key(kMtN, 0);
+    int32_t pos = kMtN, hg = 0;
+    double gs = 0.0;
     const bool had = b.st != nullptr;
-    if (had) SLAM_HIP_TRY(hipMemcpy(&keep, b.st, sizeof(keep), hipMemcpyDeviceToHost));
+    int rc = SLAM_OK;
+    if (had && (rc = mt_get_state(b, key.data(), &pos, &hg, &gs, nullptr))) return rc;
     GlibcLogTable T;
-    int rc = glibc_log_table(&T);
+    rc = glibc_log_table(&T);
     if (rc) return rc;
     mt_free(b);
     b.device = device;
     b.g_cap = g_cap;
     b.pre_cap = pre_cap;
     b.cand_cap = cand_bound(std::max<int64_t>(g_cap, 1));
-    b.nblk = blocks_for(2 * pre_cap, b.cand_cap);
     b.nb_count = (b.cand_cap + kMtCandPerBlock - 1) / kMtCandPerBlock;
+    // a request reads at most 2 pre_cap + 4 cand_cap words past the position,
+    // then the block it ends in (the state NumPy reports)
+    b.need = 2 * pre_cap + 4 * b.cand_cap + 2 * kMtN;
+    int cus = 256;
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
+    b.R = (int32_t)std::min<int64_t>(std::min<int64_t>(kMtMaxSegs, cus), b.need / kMtMinSeg);
+    if (b.R < 1) b.R = 1;
+    b.S = (b.need + (int64_t)b.R * kMtN - 1) / ((int64_t)b.R * kMtN) * kMtN;
+    if (b.R > 1 && b.S < kMtMinSeg) b.S = kMtMinSeg;
+    if (b.S < kMtN) b.S = kMtN;
+    const int64_t RS = (int64_t)b.R * b.S;
+    // live words: [p - 624, g1) with g1 - p < need + R S, plus the round being written
+    const int64_t live = std::max<int64_t>(b.need + 2 * RS + 4 * kMtN, RS + 3 * kMtN);
+    b.cap = 1;
+    while (b.cap < live) b.cap <<= 1;                    // a power of two: index & (cap - 1)
     SLAM_HIP_TRY(hipMalloc(&b.st, sizeof(MtDeviceState)));
     SLAM_HIP_TRY(hipMalloc(&b.tab, sizeof(GlibcLogTable)));
-    SLAM_HIP_TRY(hipMalloc(&b.X, sizeof(uint32_t) * kMtN * (size_t)(b.nblk + 1)));
-    SLAM_HIP_TRY(hipMalloc(&b.bcnt, sizeof(unsigned) * (size_t)b.nb_count));
-    SLAM_HIP_TRY(hipMalloc(&b.boff, sizeof(int64_t) * (size_t)b.nb_count));
+    SLAM_HIP_TRY(hipMalloc(&b.X, sizeof(uint32_t) * (size_t)b.cap));
+    SLAM_HIP_TRY(hipMalloc(&b.seg, sizeof(uint32_t) * kMtN * (size_t)b.R));
+    SLAM_HIP_TRY(hipMalloc(&b.q, sizeof(uint32_t) * (kMtDeg / 2 + 16)));
+    SLAM_HIP_TRY(hipMalloc(&b.bcnt, sizeof(unsigned) * (size_t)std::max<int64_t>(b.nb_count, 1)));
+    SLAM_HIP_TRY(hipMalloc(&b.boff, sizeof(int64_t) * (size_t)std::max<int64_t>(b.nb_count, 1)));
     SLAM_HIP_TRY(hipMalloc(&b.normals, sizeof(double) * (size_t)std::max<int64_t>(g_cap, 1)));
     SLAM_HIP_TRY(hipMalloc(&b.pre, sizeof(double) * (size_t)std::max<int64_t>(pre_cap, 1)));
     SLAM_HIP_TRY(hipMemcpy(b.tab, &T, sizeof(T), hipMemcpyHostToDevice));
-    SLAM_HIP_TRY(hipMemcpy(b.st, &keep, sizeof(keep), hipMemcpyHostToDevice));
-    return SLAM_OK;
+    b.n_idx = 0;
+    if (b.R > 1) {
+        Bits q;
+        if ((rc = jump_poly((uint64_t)RS, q))) return rc;
+        std::vector<uint16_t> idx;
+        for (int i = 0; i < kMtDeg; ++i)
+            if (bit_of(q, (size_t)i)) idx.push_back((uint16_t)i);
+        while (idx.size() % 16) idx.push_back((uint16_t)(kMtConvWords + 1));   // -> zero words
+        b.n_idx = (int32_t)idx.size();
+        SLAM_HIP_TRY(hipMemcpy(b.q, idx.data(), sizeof(uint16_t) * idx.size(), hipMemcpyHostToDevice));
+    }
+    const size_t lds = round_lds_bytes(b.R);
+    if (lds > 64 * 1024)
+        SLAM_HIP_TRY(hipFuncSetAttribute((const void*)mt_round_kernel,
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    return had ? mt_set_state(b, key.data(), pos, hg, gs, nullptr) : SLAM_OK;
 }
 
 int mt_set_state(MtBuffers& b, const uint32_t* key, int32_t pos, int32_t has_gauss, double gauss,
                  hipStream_t s) {
     SLAM_ARG_CHECK(b.st && key, "mt19937 state: no buffers / key");
     SLAM_ARG_CHECK(pos >= 0 && pos <= kMtN, "mt19937 state: pos outside [0, 624]");
+    SLAM_HIP_TRY(hipSetDevice(b.device));
     MtDeviceState h{};
-    std::memcpy(h.key, key, sizeof(h.key));
-    h.pos = pos;
+    h.p = pos;
+    h.g1 = kMtN;                                          // the key itself
     h.has_gauss = has_gauss ? 1 : 0;
     h.gauss = has_gauss ? gauss : 0.0;
     SLAM_HIP_TRY(hipMemcpyAsync(b.st, &h, sizeof(h), hipMemcpyHostToDevice, s));
+    // the key is staged in seg[0] for the priming pass (which reads it first
+    // and then the seeding pass overwrites seg)
+    SLAM_HIP_TRY(hipMemcpyAsync(b.seg, key, sizeof(uint32_t) * kMtN, hipMemcpyHostToDevice, s));
+    const int rc = mt_prime(b, b.seg, s);
+    if (rc) return rc;
     SLAM_HIP_TRY(hipStreamSynchronize(s));
     return SLAM_OK;
 }
@@ -427,11 +697,32 @@ int mt_set_state(MtBuffers& b, const uint32_t* key, int32_t pos, int32_t has_gau
 int mt_get_state(const MtBuffers& b, uint32_t* key, int32_t* pos, int32_t* has_gauss, double* gauss,
                  hipStream_t s) {
     SLAM_ARG_CHECK(b.st, "mt19937 state: no buffers");
+    SLAM_HIP_TRY(hipSetDevice(b.device));
     MtDeviceState h;
     SLAM_HIP_TRY(hipMemcpyAsync(&h, b.st, sizeof(h), hipMemcpyDeviceToHost, s));
     SLAM_HIP_TRY(hipStreamSynchronize(s));
-    if (key) std::memcpy(key, h.key, sizeof(h.key));
-    if (pos) *pos = h.pos;
+    // NumPy's (key, pos): the block holding the next word; pos = 624 when the
+    // last draw ended on a block boundary (it regenerates lazily)
+    int64_t blk;
+    int32_t ps;
+    if (h.p > 0 && h.p % kMtN == 0) {
+        blk = h.p / kMtN - 1;
+        ps = kMtN;
+    } else {
+        blk = h.p / kMtN;
+        ps = (int32_t)(h.p % kMtN);
+    }
+    if (key) {
+        SLAM_ARG_CHECK((blk + 1) * kMtN <= h.g1, "mt19937 state: block not generated (internal)");
+        const int64_t k0 = (blk * kMtN) & (b.cap - 1);
+        const int64_t n0 = std::min<int64_t>(kMtN, b.cap - k0);   // the ring may wrap inside the block
+        SLAM_HIP_TRY(hipMemcpyAsync(key, b.X + k0, sizeof(uint32_t) * n0, hipMemcpyDeviceToHost, s));
+        if (n0 < kMtN)
+            SLAM_HIP_TRY(hipMemcpyAsync(key + n0, b.X, sizeof(uint32_t) * (kMtN - n0),
+                                        hipMemcpyDeviceToHost, s));
+        SLAM_HIP_TRY(hipStreamSynchronize(s));
+    }
+    if (pos) *pos = ps;
     if (has_gauss) *has_gauss = h.has_gauss;
     if (gauss) *gauss = h.gauss;
     return SLAM_OK;
@@ -443,23 +734,40 @@ int mt_enqueue(const MtBuffers& b, int64_t n_pre, const int32_t* pre_flag, doubl
     SLAM_ARG_CHECK(g >= 0 && g <= b.g_cap && n_pre >= 0 && n_pre <= b.pre_cap &&
                        (pre_flag == nullptr || b.pre_cap >= 1),
                    "mt19937 draw: request larger than the reserved buffers");
-    const int64_t pre_words = pre_flag ? 2 : 2 * n_pre;
     const int64_t ncand = g > 0 ? cand_bound(g) : 0;
-    const int64_t nblk = blocks_for(pre_words, ncand);
-    SLAM_ARG_CHECK(nblk <= b.nblk, "mt19937 draw: stream buffer too small");
-    mt_gen_kernel<<<1, kMtGenThreads, 0, s>>>(b.st, b.X, nblk);
+    SLAM_ARG_CHECK(ncand <= b.cand_cap, "mt19937 draw: candidate buffers too small");
+    const int64_t RS = (int64_t)b.R * b.S;
+    mt_round_kernel<<<b.R, kMtGenThreads, round_lds_bytes(b.R), s>>>(b.st, b.X, b.cap, b.seg, b.q,
+                                                                   b.n_idx, b.S, b.R, b.need);
     SLAM_HIP_TRY(hipGetLastError());
     const unsigned nbc = (unsigned)((ncand + kMtCandPerBlock - 1) / kMtCandPerBlock);
+    mt_count_kernel<<<std::max(nbc, 1u), kMtCountThreads, 0, s>>>(b.st, b.X, b.cap, pre_flag, n_pre,
+                                                                   ncand, b.bcnt, RS, b.need);
     if (nbc > 0) {
-        mt_count_kernel<<<nbc, kMtCountThreads, 0, s>>>(b.st, b.X, pre_flag, n_pre, ncand, b.bcnt);
         mt_scan_kernel<<<1, kMtScanThreads, 0, s>>>(b.st, b.bcnt, nbc, b.boff, g, status);
-        mt_emit_kernel<<<nbc, kMtCountThreads, 0, s>>>(b.st, b.X, pre_flag, n_pre, ncand, b.boff, g,
-                                                       b.tab, b.normals);
-        SLAM_HIP_TRY(hipGetLastError());
+        mt_emit_kernel<<<nbc, kMtCountThreads, 0, s>>>(b.st, b.X, b.cap, pre_flag, n_pre, ncand,
+                                                       b.boff, g, b.tab, b.normals);
     }
-    mt_finish_kernel<<<1, kMtGenThreads, 0, s>>>(b.st, b.X, pre_flag, n_pre, pre_scale, pre_out,
+    SLAM_HIP_TRY(hipGetLastError());
+    mt_finish_kernel<<<1, kMtGenThreads, 0, s>>>(b.st, b.X, b.cap, pre_flag, n_pre, pre_scale, pre_out,
                                                  pre_index, g, b.normals);
     SLAM_HIP_TRY(hipGetLastError());
+    return SLAM_OK;
+}
+
+int mt_jump_window_host(const uint32_t* win, uint64_t J, uint32_t* out) {
+    Bits q;
+    int rc = jump_poly(J, q);
+    if (rc) return rc;
+    std::vector<uint32_t> Y(win, win + kMtN);
+    Y.resize(kMtConvWords + 1);
+    for (size_t k = kMtN; k < Y.size(); ++k) Y[k] = mt_next(Y[k - kMtN], Y[k - kMtN + 1], Y[k - kMtN + kMtM]);
+    for (int j = 0; j < kMtN; ++j) {
+        uint32_t acc = 0;
+        for (int i = 0; i < kMtDeg; ++i)
+            if (bit_of(q, (size_t)i)) acc ^= Y[(size_t)i + j];
+        out[j] = acc;
+    }
     return SLAM_OK;
 }
 
@@ -485,6 +793,11 @@ int slam_glibc_log(int64_t n, const double* x, double* out) {
     if (rc) return rc;
     for (int64_t i = 0; i < n; ++i) out[i] = glibc_log(x[i], T);
     return SLAM_OK;
+}
+
+int slam_mt_jump_window(const uint32_t* window, uint64_t n_words, uint32_t* out) {
+    SLAM_ARG_CHECK(window && out, "slam_mt_jump_window: NULL argument");
+    return mt_jump_window_host(window, n_words, out);
 }
 
 int slam_mt_create(const uint32_t* key, int32_t pos, int32_t has_gauss, double gauss, int device,

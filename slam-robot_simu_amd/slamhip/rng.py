@@ -94,3 +94,11 @@ def glibc_log(x):
     out = np.empty_like(x)
     check(_lib.load().slam_glibc_log(x.size, dptr(x), dptr(out)), "slam_glibc_log")
     return out
+
+
+def jump_window(window, n_words):
+    """The 624-word MT19937 window n_words further on (host jump-ahead)."""
+    w = np.ascontiguousarray(window, dtype=np.uint32)
+    out = np.empty(624, dtype=np.uint32)
+    check(_lib.load().slam_mt_jump_window(_u32(w), int(n_words), _u32(out)), "slam_mt_jump_window")
+    return out

@@ -63,3 +63,18 @@ def test_glibc_log_restatement_bit_exact():
     ref = np.array([libm.log(float(v)) for v in x])
     bad = np.flatnonzero(got.view(np.uint64) != ref.view(np.uint64))
     assert bad.size == 0, (x[bad[:5]], got[bad[:5]], ref[bad[:5]])
+
+
+@pytest.mark.parametrize("n_words", [1, 623, 624, 20000, 3 * 624 * 1000 + 17])
+def test_jump_ahead_window(n_words):
+    """Jump-ahead (x^n mod MT19937's characteristic polynomial, applied as an
+    XOR of shifted windows) lands on the window the recurrence reaches."""
+    from slamhip import rng
+    key = np.asarray(np.random.RandomState(n_words).get_state()[1], np.uint32)
+    start = 5                                   # a window inside the generated stream
+    X = mo.stream(key, (start + n_words + 624) // 624 + 2)
+    win = X[start:start + 624]
+    got = rng.jump_window(win, n_words)
+    ref = X[start + n_words:start + n_words + 624]
+    np.testing.assert_array_equal(got[1:], ref[1:])
+    assert (got[0] ^ ref[0]) >> 31 == 0
