@@ -35,6 +35,7 @@ constexpr int kMtCandPerThread = 4;
 constexpr int kMtCountThreads = 256;
 constexpr int kMtCandPerBlock = kMtCountThreads * kMtCandPerThread;
 constexpr int kMtScanThreads = 1024;
+constexpr int64_t kMtRoundsAhead = 4;   // requests one parallel round feeds
 
 // ------------------------------------------------------------------ kernels
 
@@ -638,7 +639,10 @@ int mt_reserve(MtBuffers& b, int64_t g_cap, int64_t pre_cap, int device) {
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
     b.R = (int32_t)std::min<int64_t>(std::min<int64_t>(kMtMaxSegs, cus), b.need / kMtMinSeg);
     if (b.R < 1) b.R = 1;
-    b.S = (b.need + (int64_t)b.R * kMtN - 1) / ((int64_t)b.R * kMtN) * kMtN;
+    // R > 1: a round covers kMtRoundsAhead requests, so the jump (a fixed
+    // cost per round) is paid once per that many requests
+    const int64_t span = b.R > 1 ? kMtRoundsAhead * b.need : b.need;
+    b.S = (span + (int64_t)b.R * kMtN - 1) / ((int64_t)b.R * kMtN) * kMtN;
     if (b.R > 1 && b.S < kMtMinSeg) b.S = kMtMinSeg;
     if (b.S < kMtN) b.S = kMtN;
     const int64_t RS = (int64_t)b.R * b.S;
