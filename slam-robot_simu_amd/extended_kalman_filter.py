@@ -69,3 +69,65 @@ class ExtendedKalmanFilter(object):
         z = np.asarray(observations, dtype=np.float64).reshape(1, 2)
         _, xh, P = self.dev.step(z, control=np.asarray(control, dtype=np.float64))
         return xh[0].reshape(3, 1), P[0]
+
+
+# ---------------------------------------------------------------- animation
+class EKFAnimation:
+    """The reference's demo frame (extended_kalman_filter.py:219-274) over
+    this filter: true track, observations, predicted track and the error
+    ellipse of P."""
+
+    def __init__(self, ekf, period_ms, confidence=99.0):
+        from mylib.error_ellipse import ErrorEllipse
+        self.ekf = ekf
+        self.period_ms = period_ms
+        self.confidence = confidence
+        self.ellipse = ErrorEllipse(confidence)
+        self.truth, self.obs, self.pred = [], [], []
+        self.time_s = 0.0
+
+    def __call__(self, i):
+        import matplotlib.pyplot as plt
+        from mylib import plots
+        self.time_s += self.period_ms / 1000
+        x_true, x_dr, obs, x_pre, P = self.ekf.main_ekf()
+        self.truth.append(x_true[0:2, :].copy())
+        self.obs.append(np.asarray(obs).reshape(2, 1).copy())
+        self.pred.append(x_pre[0:2, :].copy())
+        plt.cla()
+        ax = plt.subplot2grid((1, 1), (0, 0))
+        plots.trajectory(ax, self.truth, "red", "Ground Truth")
+        zs = np.concatenate(self.obs, axis=1)
+        ax.scatter(zs[0], zs[1], c="green", marker="o", alpha=0.5, label="Observation")
+        plots.trajectory(ax, self.pred, "blue", "Predicted")
+        plots.error_ellipse(ax, (x_pre[0, 0], x_pre[1, 0]), self.ellipse, P[0:2, 0:2],
+                            label="Error Ellipse: %.2f[%%]" % self.confidence)
+        print("time:{0:.3f}[s], x-cov:{1:.3f}[m], y-cov:{2:.3f}[m], xy-cov:{3:.3f}[m]"
+              .format(self.time_s, P[0, 0], P[1, 1], P[1, 0]))
+        ax.set_aspect("equal", adjustable="datalim")
+        plots.finish(ax, "Localization by EKF")
+        return (ax,)
+
+
+_animations = {}
+
+
+def animate(i, ekf, period_ms):
+    """FuncAnimation callback with the reference's signature (:219)."""
+    key = id(ekf)
+    if key not in _animations:
+        _animations[key] = EKFAnimation(ekf, period_ms)
+    return _animations[key](i)
+
+
+if __name__ == "__main__":
+    import matplotlib.animation as animation
+    import matplotlib.pyplot as plt
+
+    period_ms = 100
+    frame_cnt = int(36 * 1000 / period_ms)
+    fig = plt.figure(figsize=(12, 9))
+    ekf = ExtendedKalmanFilter(period_ms)
+    ani = animation.FuncAnimation(fig, animate, frames=frame_cnt, fargs=(ekf, period_ms), blit=False,
+                                  interval=period_ms, repeat=False)
+    plt.show()

@@ -20,11 +20,18 @@ stream in the reference's draw order.
 (:685-715): all 2-combinations of each landmark's half-edges, then
 Gauss-Newton until sum(delta^2) < 0.01, with the poses resident on the GPU
 between iterations.
+
+``Robot`` (:584-897) is the reference's driver: ``move(v, w)`` (motion with
+and without noise through the MotionModel drop-in, a scan of the noisy pose,
+the odometry pose handed to the estimator), ``estimateOpticalTrajectory()``
+and ``draw(ax1, ax2)``; ``graph_based_slam(i, period_ms)`` is the demo's
+animation callback (:931-975) with the demo's constants (:899-925).
 """
 from __future__ import annotations
 
 
 import ctypes as C
+from copy import deepcopy
 
 import numpy as np
 
@@ -148,6 +155,25 @@ class ScanSensor(object):
         s = np.sin(ang)
         rot = np.array([[c, -s, 0], [s, c, 0], [0, 0, 1]])
         return rot @ aCovMat @ rot.T
+
+    def tfMeasurement2Robot(self, aCovMat, aLandMarkDir):
+        """:218-234: the measurement covariance in the robot frame."""
+        c = np.cos(aLandMarkDir)
+        s = np.sin(aLandMarkDir)
+        rot = np.array([[c, -s, 0], [s, c, 0], [0, 0, 1]])
+        return rot @ aCovMat @ rot.T
+
+    def draw(self, aAx, aColor, aPose):
+        """:236-250: the scan fan at aPose and the true landmarks."""
+        from mylib import plots
+        from mylib import transform as tf
+        world = tf.robot2world(aPose, self.local.T)
+        aAx.plot(world.T[0], world.T[1], c=aColor, linewidth=1.0, linestyle="-")
+        plots.landmark_stars(aAx, self._lm[:, 0], self._lm[:, 1], label="Land Mark(True)")
+
+    def getLandMarkNum(self):
+        """:252-259."""
+        return len(self._lm)
 
 
 class HalfEdge:
@@ -273,3 +299,181 @@ class TrajectoryEstimator(object):
             st += list(self._dev.optimize(DELTA_SUM_TH, max_iter - 1))
             self._write_back(times_of(paired))
         return np.array(st, dtype=np.float64).reshape(-1, 4)
+
+
+class Robot(object):
+    """graph_based_slam.py:584-897: a robot that moves with the velocity motion
+    model, scans the landmarks and estimates its trajectory by graph SLAM on
+    the GPU.  The noise comes from NumPy's global stream in the reference's
+    order (move: three normals; each scan: three per detected landmark)."""
+
+    DELTA_SUM_TH = 0.01                                       # :630
+
+    def __init__(self, aPose, aDt, aScanRng_m, aScanAng_rad, aLandMarks, *, device=0):
+        from mylib.error_ellipse import ErrorEllipse
+        from motion_model import MotionModel
+        self._sensor = ScanSensor(aScanRng_m, aScanAng_rad, aLandMarks, device=device)
+        self._sensor.setNoiseParam(5, 2, 2)                   # :604
+        self._motion = MotionModel(aDt, 0.1, 0.1, 0.1, 0.1, 0.1, 0.1, device=device)
+        self._est = TrajectoryEstimator(aPose, device=device)
+        self._dt = aDt
+        self._time = 0
+        self._poses = [aPose]                                 # actual poses
+        self._ctl = []
+        self._obs_actu, self._obs_true, self._halves = [], [], []
+        self._confidence = 99.0
+        self._ellipse = ErrorEllipse(self._confidence)
+        self._sensor.scan(aPose)                              # :625 (its draws are consumed)
+        self._observe(aPose, len(self._poses) - 1, self._time)
+        self.is_calc, self.loop_cnt, self.delta_sum, self.det, self.cond = False, 0, 0.0, 0.0, 0.0
+
+    def move(self, aV, aW):
+        """:638-656."""
+        actual = self._motion.moveWithNoise(self._poses[-1], aV, aW)
+        odometry = self._motion.moveWithoutNoise(self._poses[-1], aV, aW)
+        self._ctl.append(np.array([aV, aW]))
+        self._poses.append(actual)
+        self._time += 1
+        seen = self._observe(actual, len(self._poses) - 1, self._time)
+        self._est.addPose(deepcopy(odometry), seen)
+
+    def _observe(self, pose, pose_id, t):
+        """:658-682: scan, keep a half-edge per observed landmark."""
+        noisy, clean = self._sensor.scan(pose)
+        self._halves.extend(HalfEdge(t, o, pose_id) for o in noisy)
+        self._obs_actu.append(noisy)
+        self._obs_true.append(clean)
+        return len(noisy) > 0
+
+    def estimateOpticalTrajectory(self):
+        """:685-715 (pairing and Gauss-Newton on the device)."""
+        st = self._est.estimate_trajectory(self._halves, self._sensor.getLandMarkNum())
+        for k, (_, dsum, det, cond) in enumerate(st):
+            print(" Loop({0}):sum(dx^2) = {1}, det(H) = {2}, cond(H) = {3}".format(k + 1, dsum, det, cond))
+        last = st[-1]
+        self.is_calc, self.loop_cnt = bool(last[0]), len(st)
+        self.delta_sum, self.det, self.cond = float(last[1]), float(last[2]), float(last[3])
+        return st
+
+    def getActualPoses(self):
+        return self._poses
+
+    def getEstTrajPose(self):
+        return self._est.getEstTrajPose()
+
+    # ---------------------------------------------------------- drawing
+    def draw(self, aAx1, aAx2):
+        """:717-724: the world frame (ax1) and the robot frame (ax2)."""
+        self._draw_world(aAx1)
+        self._draw_robot_frame(aAx2)
+
+    def _draw_track(self, ax, color, label, poses):
+        from mylib import plots
+        xs = [p[0, 0] for p in poses]
+        ys = [p[1, 0] for p in poses]
+        plots.headings(ax, xs, ys, [p[2, 0] for p in poses], color, arrow=True)
+        ax.plot(xs, ys, c=color, linewidth=1.0, linestyle="-", label=label)
+
+    def _draw_world(self, ax):
+        """:726-828."""
+        from mylib import plots
+        pose = self._poses[-1]
+        self._sensor.draw(ax, "green", pose)
+        self._draw_track(ax, "red", "Actual Trajectory", self._poses)
+        pts = []
+        for k, o in enumerate(self._obs_actu[-1]):
+            ang = o.getDir() + pose[2, 0] - BASE_ANG
+            p = (o.getDist() * np.cos(ang) + pose[0, 0], o.getDist() * np.sin(ang) + pose[1, 0])
+            cov = self._sensor.tfMeasurement2World(
+                self._sensor.getLandMarkCovMatrixOnMeasurementSys(o.getDist()), o.getDir(), pose[2, 0])
+            plots.error_ellipse(ax, p, self._ellipse, cov[0:2, 0:2],
+                                label="Error Ellipse: %.2f[%%]" % self._confidence if k == 0 else "")
+            pts.append(p)
+        if pts:
+            plots.sight_lines(ax, pose[0:2, 0], pts)
+            pts = np.array(pts)
+            plots.landmark_stars(ax, pts[:, 0], pts[:, 1], face="red", edge="red", label="Land Mark(Actual)")
+        self._draw_track(ax, "blue", "Estimated Trajectory", self._est.getEstTrajPose())
+        status = ("<Status>\n Calculated Propriety: %s\n Number of Iterations: %d\n"
+                  " $\\sum_{} \\, \\Delta{x}^T \\Delta{x}$: %e\n $det(H)$:%e\n Condition Number:%e"
+                  % ("OK" if self.is_calc else "NG", self.loop_cnt, self.delta_sum, self.det, self.cond))
+        ax.text(0.01, 0.99, status, transform=ax.transAxes, fontsize=10, verticalalignment="top",
+                bbox=dict(boxstyle="round", facecolor="wheat", alpha=0.5))
+
+    def _draw_robot_frame(self, ax, gain=2):
+        """:830-896: observations in the robot frame (true and noisy)."""
+        from mylib import plots
+        for obs, face, edge, label in ((self._obs_true[-1], "yellow", "orange", "Land Mark(True)"),
+                                       (self._obs_actu[-1], "red", "red", "Land Mark(Actual)")):
+            if not obs:
+                continue
+            xs = np.array([o.getDist() * np.cos(o.getDir()) for o in obs])
+            ys = np.array([o.getDist() * np.sin(o.getDir()) for o in obs])
+            plots.landmark_stars(ax, xs, ys, face=face, edge=edge, label=label)
+            plots.headings(ax, xs, ys, np.array([o.getOrient() for o in obs]), edge, arrow=True, gain=gain)
+        for k, o in enumerate(self._obs_actu[-1]):
+            cov = self._sensor.tfMeasurement2Robot(
+                self._sensor.getLandMarkCovMatrixOnMeasurementSys(o.getDist()), o.getDir())
+            p = (o.getDist() * np.cos(o.getDir()), o.getDist() * np.sin(o.getDir()))
+            plots.error_ellipse(ax, p, self._ellipse, cov[0:2, 0:2],
+                                label="Error Ellipse: %.2f[%%]" % self._confidence if k == 0 else "")
+            plots.sight_lines(ax, (0.0, 0.0), [p])
+        ax.scatter(0, 0, s=100, c="blue", marker="o", alpha=0.5, label="Robot")
+        ax.quiver(0, 0, 0, 1, color="blue", angles="xy", scale_units="xy", scale=1)
+
+
+# ------------------------------------------------------------- the demo
+SCN_SENS_RANGE_m = 15.0                                       # :899-925
+SCN_SENS_ANGLE_rps = np.deg2rad(80.0)
+RADIUS_m = 10.0
+OMEGA_rps = np.deg2rad(10.0)
+VEL_mps = RADIUS_m * OMEGA_rps
+LAND_MARKS = np.array([[0.0, 0.0], [14.0, 1.0], [9.0, 9.0], [0.0, 15.0], [-11.0, 10.0],
+                       [-14.0, 1.0], [-10.0, -9.0], [0.0, -16.0], [10.0, -11.0]])
+PERIOD_ms = 2000
+
+
+def make_demo_robot(device=0):
+    """The demo's robot (the reference builds it at import, :927)."""
+    x_base = np.array([[10.0], [0.0], [np.deg2rad(90.0)]])
+    return Robot(x_base, PERIOD_ms / 1000, SCN_SENS_RANGE_m, SCN_SENS_ANGLE_rps, LAND_MARKS,
+                 device=device)
+
+
+gRbt = None
+time_s = 0.0
+
+
+def graph_based_slam(i, aPeriod_ms):
+    """:931-975: move, estimate, draw both frames (the robot is made on the
+    first call, not at import, so that importing needs no GPU)."""
+    import matplotlib.pyplot as plt
+    from mylib import plots
+    global gRbt, time_s
+    if gRbt is None:
+        gRbt = make_demo_robot()
+    print("TIME:{0:.3f}[s]".format(time_s))
+    time_s += aPeriod_ms / 1000
+    gRbt.move(VEL_mps, OMEGA_rps)
+    gRbt.estimateOpticalTrajectory()
+    plt.cla()
+    ax1 = plt.subplot2grid((1, 2), (0, 0), aspect="equal")
+    ax2 = plt.subplot2grid((1, 2), (0, 1), aspect="equal")
+    gRbt.draw(ax1, ax2)
+    ax1.set_aspect("equal", adjustable="datalim")
+    plots.finish(ax1, "World System")
+    rng = SCN_SENS_RANGE_m + 5.0
+    ax2.axis([-rng, rng, -rng, rng])
+    plots.finish(ax2, "Robot System")
+    return ax1, ax2
+
+
+if __name__ == "__main__":
+    import matplotlib.animation as animation
+    import matplotlib.pyplot as plt
+
+    frame_cnt = int(36 * 1000 / PERIOD_ms)
+    fig = plt.figure(figsize=(18, 9))
+    ani = animation.FuncAnimation(fig, graph_based_slam, frames=frame_cnt, fargs=(PERIOD_ms,), blit=False,
+                                  interval=PERIOD_ms, repeat=False)
+    plt.show()

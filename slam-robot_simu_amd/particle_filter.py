@@ -128,3 +128,77 @@ class ParticleFilter(object):
     @property
     def weights(self):
         return self.dev.get_state()[3]
+
+
+# ---------------------------------------------------------------- animation
+class PFAnimation:
+    """The reference's demo frame (particle_filter.py:248-327) over this
+    filter: landmarks with sight lines from the estimate, the particle cloud
+    with headings, true and estimated tracks, the maximum-likelihood label,
+    and a zoom panel sized by the chi-square radius of Q."""
+
+    def __init__(self, pf, period_ms, confidence=99.0):
+        from mylib.error_ellipse import ErrorEllipse
+        self.pf = pf
+        self.period_ms = period_ms
+        self.confidence = confidence
+        self.ellipse = ErrorEllipse(confidence)
+        self.truth, self.est = [], []
+        self.time_s = 0.0
+
+    def __call__(self, i):
+        import matplotlib.pyplot as plt
+        from mylib import plots
+        self.time_s += self.period_ms / 1000
+        lm, x_true, x_est, px, Q, w_idx, w_val = self.pf.main_pf()
+        self.truth.append(x_true[0:2, :].copy())
+        self.est.append(x_est[0:2, :].copy())
+        plt.cla()
+        axes = (plt.subplot2grid((1, 2), (0, 0)), plt.subplot2grid((1, 2), (0, 1)))
+        for k, ax in enumerate(axes):
+            plots.landmark_stars(ax, lm[:, 0], lm[:, 1], label="Land Mark" if k == 0 else None)
+            plots.sight_lines(ax, x_est[0:2, 0], lm)
+            ax.scatter(px[0], px[1], c="cyan", marker="o", alpha=0.5)
+            plots.trajectory(ax, self.truth, "red", "Ground Truth" if k == 0 else None)
+            plots.trajectory(ax, self.est, "blue", "Estimation" if k == 0 else None)
+        zoom = axes[1]
+        plots.headings(zoom, px[0], px[1], px[2], "cyan")
+        plots.headings(zoom, x_true[0], x_true[1], x_true[2], "red")
+        plots.headings(zoom, x_est[0], x_est[1], x_est[2], "blue")
+        zoom.annotate("Maximuim Likelihood Estimate:\n[Index]:{0}\n[Weight]:{1:.3f}".format(w_idx, w_val),
+                      xy=(x_est[0, 0], x_est[1, 0]), xycoords="data", xytext=(0.55, 0.9),
+                      textcoords="axes fraction",
+                      bbox=dict(boxstyle="round,pad=0.5", fc=(1.0, 0.7, 0.7)),
+                      arrowprops=dict(arrowstyle="->", color="black", connectionstyle="arc3,rad=0"))
+        axes[0].set_aspect("equal", adjustable="datalim")
+        plots.finish(axes[0], "Localization by PF")
+        half = self.ellipse.calc_chi(self.confidence, Q[0:2, 0:2]) * 3
+        zoom.set_xlim(x_true[0][0] - half, x_true[0][0] + half)
+        zoom.set_ylim(x_true[1][0] - half, x_true[1][0] + half)
+        plots.finish(zoom, "Zoom")
+        print("time:{0:.3f}[s]".format(self.time_s))
+        return axes
+
+
+_animations = {}
+
+
+def animate(i, pf, period_ms):
+    """FuncAnimation callback with the reference's signature (:248)."""
+    key = id(pf)
+    if key not in _animations:
+        _animations[key] = PFAnimation(pf, period_ms)
+    return _animations[key](i)
+
+
+if __name__ == "__main__":
+    import matplotlib.animation as animation
+    import matplotlib.pyplot as plt
+
+    period_ms = 100
+    frame_cnt = int(36 * 1000 / period_ms)
+    fig = plt.figure(figsize=(18, 9))
+    pf = ParticleFilter(period_ms)
+    ani = animation.FuncAnimation(fig, animate, frames=frame_cnt, fargs=(pf, period_ms), blit=False,
+                                  interval=period_ms, repeat=False)
+    plt.show()
