@@ -3,8 +3,11 @@
 //
 // ExtendedKalmanFilter (extended_kalman_filter.py:17-205) -> slam_ekf_*;
 // EKF-SLAM (BASELINE config 4) -> slam_ekfslam_*.
+#include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
+#include <string>
 #include <vector>
 
 #include "ekf_kernels.inl"
@@ -29,11 +32,17 @@ struct slam_ekfslam {
     int device = 0;
     int64_t n_lm = 0, n = 0, ld = 0, n_pad = 0;
     int64_t pipe_grid = 0;         // persistent rank-update grid (resident workgroups, x8)
+    int64_t frag_grid = 0;         // resident grid of the fragment-streaming rank update
+    int32_t kernel_sel = 0;        // 0: fragment-streaming (m <= 64), 1: LDS-staged
+    int32_t frag_shape = 0;        // 0: 8 waves of 32 x 64, 1: 16 waves of 32 x 32
+    int32_t frag_pf = 0;           // experiment: where the next P block is requested
     hipStream_t stream = nullptr;
     double* P = nullptr;           // n x ld, lower triangle current
     double* mu = nullptr;          // n
     double* pht = nullptr;         // n_pad x M
     double* kg = nullptr;          // n_pad x M
+    double* kf = nullptr;          // -K quad-major: [M/4][n_pad][4]
+    double* hf = nullptr;          // PH^T quad-major
     double* hs = nullptr;          // kEksMaxM/3 x 18
     double* e = nullptr;           // M
     double* rd = nullptr;          // M
@@ -151,7 +160,35 @@ int eks_update(slam_ekfslam* h, int32_t k, const int64_t* ids, const double* obs
 #ifndef SLAM_EKS_PIPE
 #define SLAM_EKS_PIPE 1
 #endif
-    if (SLAM_EKS_PIPE && h->pipe_grid > 0 && M <= kEksPipeK) {
+    if (h->frag_grid > 0 && M <= kEksPipeK && h->kernel_sel == 0) {
+        const int64_t tot = h->n_pad * M;
+        hipLaunchKernelGGL(eks_frag_layout_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0,
+                           h->stream, h->kg, h->pht, h->n_pad, M, h->kf, h->hf);
+#define SLAM_EKS_FRAG_S(QQ, WM, WN)                                                               \
+    hipLaunchKernelGGL((eks_rank_update_frag_kernel<QQ, WM, WN>), dim3((unsigned)h->frag_grid),   \
+                       dim3(EksFragShape<WM, WN>::kThreads), 0, h->stream, h->P, h->n, h->ld,      \
+                       h->kf, h->hf, h->n_pad, tiles)
+#define SLAM_EKS_FRAG(QQ)                                                                         \
+    case QQ:                                                                                      \
+        if (h->frag_shape == 1) SLAM_EKS_FRAG_S(QQ, 2, 2); else SLAM_EKS_FRAG_S(QQ, 2, 4);          \
+        break
+#define SLAM_EKS_FRAG_P(QQ, PF)                                                                   \
+    hipLaunchKernelGGL((eks_rank_update_frag_kernel<QQ, 2, 4, PF>), dim3((unsigned)h->frag_grid), \
+                       dim3(EksFragShape<2, 4>::kThreads), 0, h->stream, h->P, h->n, h->ld,        \
+                       h->kf, h->hf, h->n_pad, tiles)
+        if (M / 4 == 15 && h->frag_pf == 1) SLAM_EKS_FRAG_P(15, 7);
+        else if (M / 4 == 15 && h->frag_pf == 2) SLAM_EKS_FRAG_P(15, 0);
+        else switch (M / 4) {
+            SLAM_EKS_FRAG(1); SLAM_EKS_FRAG(2); SLAM_EKS_FRAG(3); SLAM_EKS_FRAG(4);
+            SLAM_EKS_FRAG(5); SLAM_EKS_FRAG(6); SLAM_EKS_FRAG(7); SLAM_EKS_FRAG(8);
+            SLAM_EKS_FRAG(9); SLAM_EKS_FRAG(10); SLAM_EKS_FRAG(11); SLAM_EKS_FRAG(12);
+            SLAM_EKS_FRAG(13); SLAM_EKS_FRAG(14); SLAM_EKS_FRAG(15); SLAM_EKS_FRAG(16);
+            default: return fail(SLAM_ERR_ARG, "slam_ekfslam_update: bad operand width");
+        }
+#undef SLAM_EKS_FRAG_S
+#undef SLAM_EKS_FRAG_P
+#undef SLAM_EKS_FRAG
+    } else if (SLAM_EKS_PIPE && h->pipe_grid > 0 && M <= kEksPipeK) {
         hipLaunchKernelGGL(eks_rank_update_pipelined_kernel, dim3((unsigned)h->pipe_grid),
                            dim3(kEksPipeThreads), 0, h->stream, h->P, h->n, h->ld, h->kg, h->pht, M,
                            tiles);
@@ -357,6 +394,20 @@ int slam_ekfslam_create(const slam_ekfslam_config* cfg, int64_t n_landmarks, int
             hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) ==
                 hipSuccess)
             h->pipe_grid = (int64_t)per_cu * cus / 8 * 8;
+        // SLAM_EKS_KERNEL=pipe selects the LDS-staged kernel, =frag16 the
+        // 16-wave fragment shape (comparison runs); default: 8 waves of 32 x 64
+        const char* ks = std::getenv("SLAM_EKS_KERNEL");
+        const std::string sel = ks ? ks : "";
+        h->kernel_sel = sel == "pipe" ? 1 : 0;
+        h->frag_shape = (sel == "frag16") ? 1 : 0;
+        h->frag_pf = sel == "pfmid" ? 1 : sel == "pf0" ? 2 : 0;
+        const hipError_t oe =
+            h->frag_shape == 1
+                ? hipOccupancyMaxActiveBlocksPerMultiprocessor(
+                      &per_cu, eks_rank_update_frag_kernel<15, 2, 2>, EksFragShape<2, 2>::kThreads, 0)
+                : hipOccupancyMaxActiveBlocksPerMultiprocessor(
+                      &per_cu, eks_rank_update_frag_kernel<15, 2, 4>, EksFragShape<2, 4>::kThreads, 0);
+        if (oe == hipSuccess && cus > 0) h->frag_grid = (int64_t)std::max(per_cu, 1) * cus / 8 * 8;
     }
     const size_t pbytes = (size_t)h->n * h->ld * sizeof(double);
     const size_t rows = (size_t)h->n_pad * kEksMaxM;
@@ -365,6 +416,8 @@ int slam_ekfslam_create(const slam_ekfslam_config* cfg, int64_t n_landmarks, int
         hipMalloc(&h->mu, h->n * sizeof(double)) != hipSuccess ||
         hipMalloc(&h->pht, rows * sizeof(double)) != hipSuccess ||
         hipMalloc(&h->kg, rows * sizeof(double)) != hipSuccess ||
+        hipMalloc(&h->kf, (size_t)h->n_pad * kEksPipeK * sizeof(double)) != hipSuccess ||
+        hipMalloc(&h->hf, (size_t)h->n_pad * kEksPipeK * sizeof(double)) != hipSuccess ||
         hipMalloc(&h->hs, (kEksMaxM / 3) * 18 * sizeof(double)) != hipSuccess ||
         hipMalloc(&h->e, kEksMaxM * sizeof(double)) != hipSuccess ||
         hipMalloc(&h->rd, kEksMaxM * sizeof(double)) != hipSuccess ||
@@ -392,7 +445,8 @@ int slam_ekfslam_create(const slam_ekfslam_config* cfg, int64_t n_landmarks, int
 int slam_ekfslam_destroy(slam_ekfslam* h) {
     if (!h) return SLAM_OK;
     (void)hipSetDevice(h->device);
-    for (void* p : {(void*)h->P, (void*)h->mu, (void*)h->pht, (void*)h->kg, (void*)h->hs,
+    for (void* p : {(void*)h->P, (void*)h->mu, (void*)h->pht, (void*)h->kg, (void*)h->kf, (void*)h->hf,
+                    (void*)h->hs,
                     (void*)h->e, (void*)h->rd, (void*)h->sinv, (void*)h->ids, (void*)h->diag})
         if (p) (void)hipFree(p);
     for (auto& e : h->ev)

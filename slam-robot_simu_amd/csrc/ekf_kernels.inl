@@ -726,4 +726,127 @@ void eks_rank_update_pipelined_kernel(double* __restrict__ P, const int64_t n, c
     }
 }
 
+// ---- Fragment-streaming rank update (m <= 64): no LDS, no barriers.
+//
+// K (negated) and PH^T are first rewritten quad-major (eks_frag_layout_kernel):
+// Kf[((q * n_pad) + row) * 4 + j] = -K[row][4 q + j], so the 16 x 4 MFMA
+// operand of any 16 rows and k-quad q is one contiguous 512-byte run -- a
+// wave loads it straight from L2 into registers.  Each wave then owns a
+// 32 x 64 block of the 128 x 128 lower tile and walks the tiles on its own:
+// while the MFMAs of the tile's last quads run, the next tile's P block and
+// first operand quads are already in flight, and the waves of a SIMD drift out
+// of phase, so HBM traffic and MFMA overlap without workgroup barriers (the
+// LDS-staged kernels align every wave on two barriers per tile).
+// Wave block (16 WM) x (16 WN); the 128 x 128 tile holds (8 / WM) x (8 / WN)
+// waves.  2 x 4: 8 waves, 2 per SIMD (254 VGPRs); 2 x 2: 16 waves, 4 per SIMD.
+template <int WM, int WN>
+struct EksFragShape {
+    static constexpr int kWaves = (8 / WM) * (8 / WN);
+    static constexpr int kThreads = 64 * kWaves;
+    static constexpr int kWavesPerSimd = kWaves / 4;
+};
+
+__global__ void eks_frag_layout_kernel(const double* __restrict__ kg, const double* __restrict__ pht,
+                                       const int64_t n_pad, const int32_t M,
+                                       double* __restrict__ Kf, double* __restrict__ Hf) {
+    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= n_pad * M) return;
+    const int64_t i = idx / M;
+    const int u = (int)(idx - i * M);
+    const int64_t o = (((int64_t)(u >> 2) * n_pad) + i) * 4 + (u & 3);
+    Kf[o] = -kg[idx];
+    Hf[o] = pht[idx];
+}
+
+template <int Q, int WM, int WN, int PFQ = -1>
+__global__ __launch_bounds__(64 * (8 / WM) * (8 / WN))
+__attribute__((amdgpu_waves_per_eu((8 / WM) * (8 / WN) / 4)))
+void eks_rank_update_frag_kernel(double* __restrict__ P, const int64_t n, const int64_t ld,
+                                 const double* __restrict__ Kf, const double* __restrict__ Hf,
+                                 const int64_t n_pad, const int64_t n_tiles) {
+    const int64_t per_xcd = (n_tiles + 7) / 8;
+    const int64_t xcd = blockIdx.x % 8, stride = gridDim.x / 8;
+    const int64_t Lend = min(n_tiles, (xcd + 1) * per_xcd);
+    int64_t L = xcd * per_xcd + blockIdx.x / 8;
+    if (L >= Lend) return;
+    constexpr int WPR = 8 / WN;                              // waves along a tile row
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int wr = (wave / WPR) * (16 * WM), wc = (wave % WPR) * (16 * WN);
+    const int lr = lane & 15, lk = lane >> 4;
+    const int64_t qstride = n_pad * 4;                      // doubles per quad
+    int64_t ti, tj;
+    eks_tile_rc(L, ti, tj);
+    eks_d4 acc[WM][WN], pre[WM][WN];
+    double fa[3][WM], fb[3][WN];
+    auto load_quad = [&](double (&a)[WM], double (&b)[WN], const int64_t r0, const int64_t c0,
+                         const int q) {
+        const double* kq = Kf + q * qstride + lk;
+        const double* hq = Hf + q * qstride + lk;
+#pragma unroll
+        for (int x = 0; x < WM; ++x) a[x] = kq[(r0 + wr + 16 * x + lr) * 4];
+#pragma unroll
+        for (int y = 0; y < WN; ++y) b[y] = hq[(c0 + wc + 16 * y + lr) * 4];
+    };
+    auto load_p = [&](eks_d4 (&t)[WM][WN], const int64_t r0, const int64_t c0, const bool diag) {
+#pragma unroll
+        for (int x = 0; x < WM; ++x)
+#pragma unroll
+            for (int y = 0; y < WN; ++y)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int64_t gi = r0 + wr + 16 * x + lk + 4 * r;
+                    const int64_t gj = c0 + wc + 16 * y + lr;
+                    t[x][y][r] = (gi < n && gj < n && (!diag || gj <= gi)) ? P[gi * ld + gj] : 0.0;
+                }
+    };
+    load_p(acc, ti * kEksTile, tj * kEksTile, ti == tj);
+    load_quad(fa[0], fb[0], ti * kEksTile, tj * kEksTile, 0);
+    if (Q > 1) load_quad(fa[1], fb[1], ti * kEksTile, tj * kEksTile, 1);
+    for (;;) {
+        const int64_t r0 = ti * kEksTile, c0 = tj * kEksTile;
+        const bool diag = (ti == tj);
+        const int64_t Ln = L + stride;
+        const bool more = Ln < Lend;
+        int64_t tin = 0, tjn = 0;
+        if (more) eks_tile_rc(Ln, tin, tjn);
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
+            if (q + 2 < Q) load_quad(fa[(q + 2) % 3], fb[(q + 2) % 3], r0, c0, q + 2);
+            // the next tile's P block is requested at the top of the tile
+            // (HBM latency is the long pole; measured 1.76 ms per C4 update
+            // against 1.88 ms with the request after the last operand quad)
+            constexpr int kPf = PFQ >= 0 ? (PFQ < Q ? PFQ : Q - 1) : 0;
+            if (more && q == kPf) load_p(pre, tin * kEksTile, tjn * kEksTile, tin == tjn);
+            const int s = q % 3;
+#pragma unroll
+            for (int x = 0; x < WM; ++x)
+#pragma unroll
+                for (int y = 0; y < WN; ++y)
+                    acc[x][y] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[s][x], fb[s][y], acc[x][y], 0, 0, 0);
+        }
+        if (more) {                                          // the next tile's first quads
+            load_quad(fa[0], fb[0], tin * kEksTile, tjn * kEksTile, 0);
+            if (Q > 1) load_quad(fa[1], fb[1], tin * kEksTile, tjn * kEksTile, 1);
+        }
+#pragma unroll
+        for (int x = 0; x < WM; ++x)
+#pragma unroll
+            for (int y = 0; y < WN; ++y)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int64_t gi = r0 + wr + 16 * x + lk + 4 * r;
+                    const int64_t gj = c0 + wc + 16 * y + lr;
+                    if (gi < n && gj < n && (!diag || gj <= gi)) P[gi * ld + gj] = acc[x][y][r];
+                }
+        if (!more) break;
+#pragma unroll
+        for (int x = 0; x < WM; ++x)
+#pragma unroll
+            for (int y = 0; y < WN; ++y) acc[x][y] = pre[x][y];
+        L = Ln;
+        ti = tin;
+        tj = tjn;
+    }
+}
+
 }  // namespace slam
