@@ -788,6 +788,13 @@ void eks_rank_update_frag_kernel(double* __restrict__ P, const int64_t n, const 
         for (int y = 0; y < WN; ++y) b[y] = hq[(c0 + wc + 16 * y + lr) * 4];
     };
     auto load_p = [&](eks_d4 (&t)[WM][WN], const int64_t r0, const int64_t c0, const bool diag) {
+#ifdef EKS_PROBE_NOMEM
+#pragma unroll
+        for (int x = 0; x < WM; ++x)
+#pragma unroll
+            for (int y = 0; y < WN; ++y) t[x][y] = eks_d4{(double)r0, (double)c0, 0.0, (double)diag};
+        return;
+#endif
 #pragma unroll
         for (int x = 0; x < WM; ++x)
 #pragma unroll
@@ -822,7 +829,11 @@ void eks_rank_update_frag_kernel(double* __restrict__ P, const int64_t n, const 
             for (int x = 0; x < WM; ++x)
 #pragma unroll
                 for (int y = 0; y < WN; ++y)
+#ifdef EKS_PROBE_NOMFMA
+                    acc[x][y][0] += fa[s][x] * fb[s][y];
+#else
                     acc[x][y] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[s][x], fb[s][y], acc[x][y], 0, 0, 0);
+#endif
         }
         if (more) {                                          // the next tile's first quads
             load_quad(fa[0], fb[0], tin * kEksTile, tjn * kEksTile, 0);
@@ -836,7 +847,11 @@ void eks_rank_update_frag_kernel(double* __restrict__ P, const int64_t n, const 
                 for (int r = 0; r < 4; ++r) {
                     const int64_t gi = r0 + wr + 16 * x + lk + 4 * r;
                     const int64_t gj = c0 + wc + 16 * y + lr;
+#ifdef EKS_PROBE_NOMEM
+                    if (acc[x][y][r] == 1.2345) P[gi * ld + gj] = acc[x][y][r];
+#else
                     if (gi < n && gj < n && (!diag || gj <= gi)) P[gi * ld + gj] = acc[x][y][r];
+#endif
                 }
         if (!more) break;
 #pragma unroll

@@ -443,13 +443,24 @@ __global__ __launch_bounds__(512) void pf_mt_observe_kernel(
         s_z[2 * (nl + l) + 1] = lm[2 * l + 1];
     }
     __syncthreads();
-    // one component per wave (lane 0): the eight compensated sums run side by
-    // side without divergence
-    const int k = threadIdx.x >> 6;
-    if (closed && (threadIdx.x & 63) == 0 && k < 8) {
-        const DDSum S = closed_sum_component(k, s_z + 2 * nl, s_z, nl);
-        zc[(size_t)st * kClosedWords + 2 * k] = S.h;
-        zc[(size_t)st * kClosedWords + 2 * k + 1] = S.l;
+    // one component per wave: lane partials, then the butterfly of
+    // closed_sums (pf_kernels.hpp), so host and device sums are the same bits
+    const int k = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    if (closed && k < 8) {
+        DDSum S = closed_lane_partial(k, lane, s_z + 2 * nl, s_z, nl);
+#pragma unroll
+        for (int d = 1; d < kClosedLanes; d <<= 1) {
+            DDSum o;
+            o.h = __shfl_xor(S.h, d, 64);
+            o.l = __shfl_xor(S.l, d, 64);
+            // partner with the lower index is the left operand
+            if ((lane & d) == 0) S = dd_join(S, o);
+            else S = dd_join(o, S);
+        }
+        if (lane == 0) {
+            zc[(size_t)st * kClosedWords + 2 * k] = S.h;
+            zc[(size_t)st * kClosedWords + 2 * k + 1] = S.l;
+        }
     }
 }
 

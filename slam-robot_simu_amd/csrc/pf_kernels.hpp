@@ -134,34 +134,49 @@ struct DDSum {
     }
 };
 
-// component k of the sums (0 S_ll, 1 S_lx, 2 S_ly, 3 S_zz, 4 S_zx, 5 S_zy, 6 D,
-// 7 E): each is its own compensated sum in landmark order, so the eight can be
-// formed independently (one lane each on the device)
-__host__ __device__ inline DDSum closed_sum_component(const int k, const double* lm,
-                                                      const double* z, const int32_t nl) {
-    DDSum S;
-    for (int32_t j = 0; j < nl; ++j) {
-        const double lx = lm[2 * j], ly = lm[2 * j + 1], zx = z[2 * j], zy = z[2 * j + 1];
-        switch (k) {
-            case 0: S.add_prod(lx, lx); S.add_prod(ly, ly); break;
-            case 1: S.add(lx); break;
-            case 2: S.add(ly); break;
-            case 3: S.add_prod(zx, zx); S.add_prod(zy, zy); break;
-            case 4: S.add(zx); break;
-            case 5: S.add(zy); break;
-            case 6: S.add_prod(zx, lx); S.add_prod(zy, ly); break;
-            default: S.add_prod(zy, lx); S.add_prod(-zx, ly); break;
-        }
+// DDSum of two double-double partials (the second added as (h, l))
+__host__ __device__ inline DDSum dd_join(DDSum a, const DDSum& b) {
+    a.add(b.h, b.l);
+    return a;
+}
+
+// component k (0 S_ll, 1 S_lx, 2 S_ly, 3 S_zz, 4 S_zx, 5 S_zy, 6 D, 7 E) of
+// landmark j's terms, added to S
+__host__ __device__ inline void closed_term(DDSum& S, const int k, const double lx, const double ly,
+                                            const double zx, const double zy) {
+    switch (k) {
+        case 0: S.add_prod(lx, lx); S.add_prod(ly, ly); break;
+        case 1: S.add(lx); break;
+        case 2: S.add(ly); break;
+        case 3: S.add_prod(zx, zx); S.add_prod(zy, zy); break;
+        case 4: S.add(zx); break;
+        case 5: S.add(zy); break;
+        case 6: S.add_prod(zx, lx); S.add_prod(zy, ly); break;
+        default: S.add_prod(zy, lx); S.add_prod(-zx, ly); break;
     }
+}
+
+// The fixed summation order, shared by host and device: 64 lane partials
+// (lane t takes landmarks t, t + 64, ... in order), then a butterfly over the
+// lanes (offset 1, 2, ..., 32; the lower lane's partial on the left).
+constexpr int kClosedLanes = 64;
+
+__host__ __device__ inline DDSum closed_lane_partial(const int k, const int lane, const double* lm,
+                                                     const double* z, const int32_t nl) {
+    DDSum S;
+    for (int32_t j = lane; j < nl; j += kClosedLanes)
+        closed_term(S, k, lm[2 * j], lm[2 * j + 1], z[2 * j], z[2 * j + 1]);
     return S;
 }
 
-__host__ __device__ inline void closed_sums(const double* lm, const double* z, const int32_t nl,
-                                            double* out) {
+inline void closed_sums(const double* lm, const double* z, const int32_t nl, double* out) {
     for (int k = 0; k < 8; ++k) {
-        const DDSum S = closed_sum_component(k, lm, z, nl);
-        out[2 * k] = S.h;
-        out[2 * k + 1] = S.l;
+        DDSum v[kClosedLanes];
+        for (int t = 0; t < kClosedLanes; ++t) v[t] = closed_lane_partial(k, t, lm, z, nl);
+        for (int d = 1; d < kClosedLanes; d <<= 1)
+            for (int t = 0; t < kClosedLanes; t += 2 * d) v[t] = dd_join(v[t], v[t + d]);
+        out[2 * k] = v[0].h;
+        out[2 * k + 1] = v[0].l;
     }
 }
 

@@ -177,8 +177,14 @@ __device__ __forceinline__ bool mt_candidate(const uint32_t* __restrict__ X, con
                                              const int64_t cap, double& x1, double& x2,
                                              double& r2) {
     uint32_t v[4];
+    const int64_t k0 = w & (cap - 1);
+    if (k0 + 3 < cap) {                                  // the common case: no wrap
 #pragma unroll
-    for (int j = 0; j < 4; ++j) v[j] = mt_temper(X[(w + j) & (cap - 1)]);
+        for (int j = 0; j < 4; ++j) v[j] = mt_temper(X[k0 + j]);
+    } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = mt_temper(X[(w + j) & (cap - 1)]);
+    }
     x1 = 2.0 * mt_legacy_double(v[0], v[1]) - 1.0;
     x2 = 2.0 * mt_legacy_double(v[2], v[3]) - 1.0;
     r2 = x1 * x1 + x2 * x2;
