@@ -125,6 +125,12 @@ int slam_pf_set_graphs(slam_pf* h, int32_t on);
 /* Exact cumsum of a resample step in one launch (on = default where the grid
  * is co-resident; SLAM_ERR_ARG elsewhere) or in two; bit-identical results. */
 int slam_pf_set_scan_merged(slam_pf* h, int32_t on);
+/* Inside slam_pf_run's batches, each step's end (np.sum, ESS, argmax,
+ * particle_filter.py:115-117/:210/:234-236) and the next step's exact cumsum
+ * (:212) in one launch (on = default where the grid is co-resident and
+ * NP <= 2^20; SLAM_ERR_ARG elsewhere) or in two; bit-identical results.
+ * Also off while slam_pf_set_scan_merged(h, 0). */
+int slam_pf_set_finscan(slam_pf* h, int32_t on);
 /* external != 0: run on the caller's HIP stream (e.g. torch.cuda.current_stream();
  * NULL = the default stream).  external == 0: a private stream again. */
 int slam_pf_set_stream(slam_pf* h, void* hip_stream, int32_t external);
