@@ -131,6 +131,11 @@ int slam_pf_set_scan_merged(slam_pf* h, int32_t on);
  * NP <= 2^20; SLAM_ERR_ARG elsewhere) or in two; bit-identical results.
  * Also off while slam_pf_set_scan_merged(h, 0). */
 int slam_pf_set_finscan(slam_pf* h, int32_t on);
+/* Overrides the resample decision of the next step (particle_filter.py:210-211,
+ * `ess < ESS_TH`): the caller re-forms ESS as the reference does, `1 / (pw @ pw.T)`
+ * on the host's BLAS, when the device's ESS lies within rounding of the
+ * threshold (the device sums in its own fixed order).  Single-GPU handles. */
+int slam_pf_set_resample_next(slam_pf* h, int32_t on);
 /* external != 0: run on the caller's HIP stream (e.g. torch.cuda.current_stream();
  * NULL = the default stream).  external == 0: a private stream again. */
 int slam_pf_set_stream(slam_pf* h, void* hip_stream, int32_t external);

@@ -1219,6 +1219,17 @@ int slam_pf_set_scan_merged(slam_pf* h, int32_t on) {
     return SLAM_OK;
 }
 
+int slam_pf_set_resample_next(slam_pf* h, int32_t on) {
+    SLAM_ARG_CHECK(h, "slam_pf_set_resample_next: NULL handle");
+    SLAM_ARG_CHECK(h->n == h->n_global, "slam_pf_set_resample_next: sharded handle");
+    SLAM_HIP_TRY(hipSetDevice(h->device));
+    h->resample_next = on ? 1 : 0;
+    int rc = set_flag(h, kFlagResample, h->resample_next);
+    if (rc) return rc;
+    SLAM_HIP_TRY(hipStreamSynchronize(h->stream));
+    return SLAM_OK;
+}
+
 int slam_pf_set_finscan(slam_pf* h, int32_t on) {
     SLAM_ARG_CHECK(h, "slam_pf_set_finscan: NULL handle");
     SLAM_ARG_CHECK(!on || (h->finscan_ok && h->scan_merged),

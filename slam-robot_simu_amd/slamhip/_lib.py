@@ -93,6 +93,7 @@ SIGNATURES = {
     "slam_pf_set_graphs": (C.c_int, [_P, C.c_int32]),
     "slam_pf_set_scan_merged": (C.c_int, [_P, C.c_int32]),
     "slam_pf_set_finscan": (C.c_int, [_P, C.c_int32]),
+    "slam_pf_set_resample_next": (C.c_int, [_P, C.c_int32]),
     "slam_pf_set_stream": (C.c_int, [_P, _P, C.c_int32]),
     "slam_motion_velocity": (C.c_int, [_D, C.c_int64, _D, C.c_double, C.c_double, _D, _D,
                                        C.c_int]),

@@ -98,6 +98,39 @@ class DeviceParticleFilter:
         if w is not None:
             ww = arrs[3]
             self.resample_next = bool(1.0 / float(ww @ ww) < self.cfg.ess_threshold)
+            self.set_resample_next(self.resample_next)        # the reference's dot decides
+
+    def set_resample_next(self, on):
+        """The next step's resample decision (particle_filter.py:210-211)."""
+        check(self._lib.slam_pf_set_resample_next(self._h, int(bool(on))),
+              "slam_pf_set_resample_next")
+        self.resample_next = bool(on)
+
+    # ESS within this relative distance of the threshold: the decision is
+    # re-formed on the host as the reference forms it (its BLAS dot order)
+    ESS_CONFIRM_BAND = 1e-9
+
+    def _confirm_ess(self, out):
+        """particle_filter.py:210-211 decides from `1 / (pw @ pw.T)` in the host
+        BLAS's summation order; the device sums the same squares in its own
+        fixed order (a few ulp apart).  Where the two could disagree -- the
+        device's ESS within ESS_CONFIRM_BAND of ESS_TH -- the weights come back
+        and the reference's own expression decides (the normalised weights are
+        bit-identical, so the decision is too)."""
+        th = self.cfg.ess_threshold
+        out["ess_confirmed"] = False
+        if not abs(out["ess"] - th) <= self.ESS_CONFIRM_BAND * th:
+            return out
+        pw = self.get_state()[3]
+        ess = float(np.reciprocal(pw @ pw.T))
+        rn = ess < th
+        if rn != bool(out["resample_next"]):
+            self.set_resample_next(rn)
+        out["resample_next"] = rn
+        out["ess_host"] = ess
+        out["ess_confirmed"] = True
+        self.resample_next = rn
+        return out
 
     def get_state(self):
         out = [np.empty(self.n) for _ in range(4)]
@@ -129,6 +162,7 @@ class DeviceParticleFilter:
                                      C.byref(res)), "slam_pf_step")
         out = self._res(res)
         self.resample_next = out["resample_next"]
+        self._confirm_ess(out)
         self.last = out
         return out
 
@@ -151,6 +185,7 @@ class DeviceParticleFilter:
         check(self._lib.slam_pf_update(self._h, dptr(zz), C.byref(res)), "slam_pf_update")
         out = self._res(res)
         self.resample_next = out["resample_next"]
+        self._confirm_ess(out)
         return out
 
     def resample_indices(self, u_resample):
@@ -224,6 +259,7 @@ class DeviceParticleFilter:
         if want_z:
             out["z"] = z
         self.resample_next = out["resample_next"]
+        self._confirm_ess(out)
         self.last = out
         return out
 

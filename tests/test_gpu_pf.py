@@ -239,3 +239,48 @@ def test_finscan_matches_separate_launches(slamhip_pf, n):
             assert a[key] == b[key], key
     for a, b in zip(*states):
         np.testing.assert_array_equal(a, b)
+
+
+def test_resample_decision_by_host_dot_near_threshold(slamhip_pf):
+    """particle_filter.py:210-211 decides from `1 / (pw @ pw.T)` (host BLAS
+    order).  With the confirmation band widened to every step, each decision is
+    re-formed on the host from the device's normalised weights and the device
+    follows it: the next step resamples exactly when NumPy's ESS < ESS_TH."""
+    rs = np.random.RandomState(2)
+    n, nl, steps = 20_000, 20, 12
+    lm = rs.uniform(-10, 10, (nl, 2))
+    p = po.PFParams(n_particles=n, landmarks=lm)
+    world = po.PFWorld(p)
+    np.random.seed(5)
+    with slamhip_pf.DeviceParticleFilter(n, lm, seed=3) as d:
+        d.ESS_CONFIRM_BAND = np.inf
+        prev = False
+        n_res = 0
+        for _ in range(steps):
+            world.advance()
+            z = world.observe()
+            noise = np.random.multivariate_normal([0.0, 0.0, 0.0], p.q, n)
+            u = np.random.rand() if d.resample_next else np.nan
+            out = d.step((p.vel, p.omega), z, noise, u)
+            assert out["resampled"] == prev
+            assert out["ess_confirmed"]
+            pw = d.get_state()[3]
+            ess = float(np.reciprocal(pw @ pw.T))
+            assert out["ess_host"] == ess
+            assert out["resample_next"] == (ess < d.cfg.ess_threshold)
+            assert abs(out["ess"] - ess) <= 1e-12 * ess
+            prev = out["resample_next"]
+            n_res += prev
+        assert n_res >= 1
+        # weights placed on the threshold: set_state's decision is NumPy's dot
+        w = np.zeros(n)
+        k = int(d.cfg.ess_threshold)
+        w[:k] = 1.0 / k
+        d.set_state(w=w)
+        dec = float(np.reciprocal(w @ w.T)) < d.cfg.ess_threshold
+        assert d.resample_next == dec
+        world.advance()
+        out = d.step((p.vel, p.omega), world.observe(),
+                     np.random.multivariate_normal([0.0, 0.0, 0.0], p.q, n),
+                     np.random.rand() if dec else np.nan)
+        assert out["resampled"] == dec
