@@ -125,12 +125,6 @@ int slam_pf_set_graphs(slam_pf* h, int32_t on);
 /* Exact cumsum of a resample step in one launch (on = default where the grid
  * is co-resident; SLAM_ERR_ARG elsewhere) or in two; bit-identical results. */
 int slam_pf_set_scan_merged(slam_pf* h, int32_t on);
-/* Inside slam_pf_run's batches, each step's end (np.sum, ESS, argmax,
- * particle_filter.py:115-117/:210/:234-236) and the next step's exact cumsum
- * (:212) in one launch (on = default where the grid is co-resident and
- * NP <= 2^20; SLAM_ERR_ARG elsewhere) or in two; bit-identical results.
- * Also off while slam_pf_set_scan_merged(h, 0). */
-int slam_pf_set_finscan(slam_pf* h, int32_t on);
 /* Overrides the resample decision of the next step (particle_filter.py:210-211,
  * `ess < ESS_TH`): the caller re-forms ESS as the reference does, `1 / (pw @ pw.T)`
  * on the host's BLAS, when the device's ESS lies within rounding of the

@@ -12,7 +12,6 @@
 
 #include "mt_stream.hpp"
 #include "pf_kernels.inl"
-#include "pf_finscan.inl"
 #include "pf_shard.inl"
 #include "pf_dist.inl"
 
@@ -112,11 +111,6 @@ struct slam_pf {
     bool deferred = false;
     bool scan_merged = false;   // exact cumsum in one launch (co-resident grid)
     bool scan_merged_ok = false;  // the merged launch is allowed for this handle
-    // step end + the next step's exact cumsum in one launch (finscan_kernel):
-    // inside a captured batch of device-decided steps
-    bool finscan = false;
-    bool finscan_ok = false;
-    FinStage fs{};
     double* s_cur = nullptr;
     DeferParts dp{};
     int32_t nb_part = 0;
@@ -419,22 +413,6 @@ int launch_reduce(slam_pf* h, int32_t resampled_known) {
     return SLAM_OK;
 }
 
-// Step end + the next step's exact cumsum (finscan_kernel, pf_finscan.inl):
-// one launch in place of finalize_deferred_kernel + scan_lean_merged_kernel.
-int launch_finscan(slam_pf* h) {
-    const int c = h->cur;
-    const double delta = 4.0 * (double)h->n_global * 0x1p-53 + 0x1p-45;
-    finscan_kernel<<<h->nb_scan, kScanThreads, 0, h->stream>>>(
-        h->n, h->dp, h->fs, h->w_un, h->s_cur, h->tail_leaves, h->tail_ops, h->n_tail_leaves,
-        h->n_tail_ops, h->x[c], h->y[c], h->th[c], h->refp, h->flags, h->cfg.ess_threshold,
-        step_io(h), h->pc.np_recip, h->boff, h->tk + 3 * kTicketWords, h->flags + kFlagFinToken,
-        delta, h->stage, h->bk, h->bf, h->boffk, h->bofff, h->ktot, h->nspec,
-        h->tk + 2 * kTicketWords, h->spec_out, h->c, h->pc, h->cfg.seed, h->flags + kFlagScanToken,
-        h->nb_part);
-    SLAM_HIP_TRY(hipGetLastError());
-    return SLAM_OK;
-}
-
 // ---- NumPy's stream on the device (slam_pf_set_rng_mt19937)
 //
 // __observation (particle_filter.py:144-154) of step ctr[0] from the true pose:
@@ -528,28 +506,6 @@ int launch_step(slam_pf* h, bool host_noise) {
     toc(h, 2);
     if ((rc = launch_fused(h, h->cfg.motion, host_noise))) return rc;
     return launch_reduce(h, -1);
-}
-
-// `steps` device-decided steps of a loaded batch.  With finscan, every step
-// but the last ends in finscan_kernel, which also runs the next step's exact
-// cumsum (the batch's resample offsets are already on the device); the first
-// step's scan and the last step's end are the separate kernels.
-int launch_steps(slam_pf* h, int steps) {
-    const bool merge = h->finscan && !h->mt && !h->timing && steps > 1;
-    if (!merge) {
-        for (int k = 0; k < steps; ++k) {
-            const int rc = launch_step(h, false);
-            if (rc) return rc;
-        }
-        return SLAM_OK;
-    }
-    int rc;
-    if ((rc = launch_scans(h, 0, false))) return rc;
-    for (int k = 0; k < steps; ++k) {
-        if ((rc = launch_fused(h, h->cfg.motion, false))) return rc;
-        if ((rc = (k + 1 < steps) ? launch_finscan(h) : launch_reduce(h, -1))) return rc;
-    }
-    return SLAM_OK;
 }
 
 int sync_results(slam_pf* h, int32_t first, int32_t count, slam_pf_result* out) {
@@ -681,11 +637,6 @@ int create_impl(const slam_pf_config* cfg, int64_t n_local, int64_t n_global, in
     A(h->refp, 4);
     A(h->flags, kFlagWords);
     A(h->tk, 4 * kTicketWords);
-    if (deferred) {
-        A(h->fs.a, (size_t)kFsLanes * kFsA);
-        A(h->fs.pm, (size_t)kFsLanes * 4);
-        A(h->fs.buf, 128);
-    }
     A(h->lm, 2 * std::max<int32_t>(n_landmarks, 1));
     A(h->noise, 3 * n);
     A(h->ctr, 4);
@@ -695,20 +646,6 @@ int create_impl(const slam_pf_config* cfg, int64_t n_local, int64_t n_global, in
     if (tail) build_tail(0, tail, leaves, ops);
     h->n_tail_leaves = (int32_t)(leaves.size() / 2);
     h->n_tail_ops = (int32_t)ops.size();
-    {
-        // finscan: the merged scan's co-resident grid, the register-held
-        // finalize lanes (NP <= 2^20) and its LDS for the tail leaves;
-        // SLAM_PF_FINSCAN=0 keeps the separate launches
-        int per_cu = 0, cus = 0;
-        const char* fe = std::getenv("SLAM_PF_FINSCAN");
-        if (deferred && h->scan_merged_ok && h->nb_part <= 4 * kFsLanes &&
-            h->n_tail_leaves <= kFsMaxTailLeaves && !(fe && fe[0] == '0') &&
-            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, finscan_kernel, kScanThreads, 0) ==
-                hipSuccess &&
-            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess)
-            h->finscan_ok = (int64_t)h->nb_scan <= (int64_t)per_cu * cus / 2;
-        h->finscan = h->finscan_ok;
-    }
     if ((rc = dalloc(h, &h->tail_leaves, leaves.size() + 2)) ||
         (rc = dalloc(h, &h->tail_ops, ops.size() + 1)) || (rc = ensure_steps(h, 1))) {
         slam_pf_destroy(h);
@@ -1098,7 +1035,8 @@ int slam_pf_run(slam_pf* h, int32_t first_step, int32_t n_steps, const double* c
         const int cur0 = h->cur;
         hipGraph_t g;
         SLAM_HIP_TRY(hipStreamBeginCapture(h->stream, hipStreamCaptureModeThreadLocal));
-        int rc2 = launch_steps(h, steps);
+        int rc2 = SLAM_OK;
+        for (int k = 0; k < steps && rc2 == SLAM_OK; ++k) rc2 = launch_step(h, false);
         hipError_t e = hipStreamEndCapture(h->stream, &g);
         h->cur = cur0;
         if (rc2) return rc2;
@@ -1214,7 +1152,6 @@ int slam_pf_set_scan_merged(slam_pf* h, int32_t on) {
                    "slam_pf_set_scan_merged: the merged launch needs a single-GPU handle whose "
                    "scan grid is co-resident");
     h->scan_merged = on != 0;
-    h->finscan = h->scan_merged && h->finscan_ok;     // finscan runs the merged scan
     drop_graphs(h);
     return SLAM_OK;
 }
@@ -1227,16 +1164,6 @@ int slam_pf_set_resample_next(slam_pf* h, int32_t on) {
     int rc = set_flag(h, kFlagResample, h->resample_next);
     if (rc) return rc;
     SLAM_HIP_TRY(hipStreamSynchronize(h->stream));
-    return SLAM_OK;
-}
-
-int slam_pf_set_finscan(slam_pf* h, int32_t on) {
-    SLAM_ARG_CHECK(h, "slam_pf_set_finscan: NULL handle");
-    SLAM_ARG_CHECK(!on || (h->finscan_ok && h->scan_merged),
-                   "slam_pf_set_finscan: needs a single-GPU handle with NP <= 2^20 whose scan "
-                   "grid is co-resident, and the merged exact cumsum on");
-    h->finscan = on != 0;
-    drop_graphs(h);
     return SLAM_OK;
 }
 

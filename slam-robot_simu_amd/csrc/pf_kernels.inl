@@ -1902,7 +1902,7 @@ __device__ __forceinline__ int64_t positions_upto(const double v, const int64_t 
 // weight (the reference's IndexError) are marked with j = n.  The fused block
 // then reads its marks and carry and takes a running max -- no search.
 // wt: the folded data were handed over inside the same launch.
-__device__ __forceinline__ void wave_tile_expand(const int64_t tile, const TileScan& ts, const int64_t n,
+__device__ void wave_tile_expand(const int64_t tile, const TileScan& ts, const int64_t n,
                                  const uint64_t* __restrict__ boffk,
                                  const int32_t* __restrict__ bofff, const uint64_t kofs,
                                  const int32_t fofs, const SpecialOut* __restrict__ so,

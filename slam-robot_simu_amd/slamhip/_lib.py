@@ -92,7 +92,6 @@ SIGNATURES = {
     "slam_pf_timing": (C.c_int, [_P, C.c_int32, _D, _I64]),
     "slam_pf_set_graphs": (C.c_int, [_P, C.c_int32]),
     "slam_pf_set_scan_merged": (C.c_int, [_P, C.c_int32]),
-    "slam_pf_set_finscan": (C.c_int, [_P, C.c_int32]),
     "slam_pf_set_resample_next": (C.c_int, [_P, C.c_int32]),
     "slam_pf_set_stream": (C.c_int, [_P, _P, C.c_int32]),
     "slam_motion_velocity": (C.c_int, [_D, C.c_int64, _D, C.c_double, C.c_double, _D, _D,

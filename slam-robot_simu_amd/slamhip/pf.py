@@ -276,11 +276,6 @@ class DeviceParticleFilter:
         grid is co-resident) or two; the results are bit-identical."""
         check(self._lib.slam_pf_set_scan_merged(self._h, int(bool(on))), "slam_pf_set_scan_merged")
 
-    def set_finscan(self, on=True):
-        """Step end + the next step's exact cumsum in one launch inside run()'s
-        batches (default where possible) or in two; bit-identical results."""
-        check(self._lib.slam_pf_set_finscan(self._h, int(bool(on))), "slam_pf_set_finscan")
-
     def enable_timing(self, on=True):
         check(self._lib.slam_pf_enable_timing(self._h, int(bool(on))), "slam_pf_enable_timing")
 

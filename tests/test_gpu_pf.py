@@ -205,42 +205,6 @@ def test_scan_merged_matches_two_launch(slamhip_pf):
         np.testing.assert_array_equal(a, b)
 
 
-@pytest.mark.parametrize("n", [1 << 20, 300_000, 5_000])
-def test_finscan_matches_separate_launches(slamhip_pf, n):
-    """Step end + next step's exact cumsum in one launch (finscan_kernel) against
-    finalize_deferred_kernel + scan_lean_merged_kernel: bit-identical records
-    and final state over graph-replayed batches with resamples.  Sizes: the
-    bench (2^20), a tail np.sum buffer (300,000), a grid smaller than the 512
-    finalize lanes (5,000)."""
-    rs = np.random.RandomState(9)
-    nl, steps = 100, 21
-    lm = rs.uniform(-10, 10, (nl, 2))
-    p = po.PFParams(n_particles=n, landmarks=lm, motion="velocity")
-    world = po.PFWorld(p)
-    np.random.seed(12)
-    zs = []
-    for _ in range(steps):
-        world.advance()
-        zs.append(world.observe())
-    ctl = np.tile([p.vel, p.omega], (steps, 1))
-    outs, states = [], []
-    for fin in (True, False):
-        with slamhip_pf.DeviceParticleFilter(n, lm, motion="velocity", seed=5) as d:
-            d.set_finscan(fin)
-            d.load_observations(np.array(zs))
-            outs.append(d.run(0, ctl[:9]) + d.run(9, ctl[9:]))
-            states.append(d.get_state())
-    assert sum(o["resampled"] for o in outs[0]) >= 2
-    for a, b in zip(*outs):
-        for key in ("x_est", "cov"):
-            np.testing.assert_array_equal(a[key], b[key])
-        for key in ("max_idx", "max_val", "ess", "weight_sum", "resampled", "resample_next",
-                    "status"):
-            assert a[key] == b[key], key
-    for a, b in zip(*states):
-        np.testing.assert_array_equal(a, b)
-
-
 def test_resample_decision_by_host_dot_near_threshold(slamhip_pf):
     """particle_filter.py:210-211 decides from `1 / (pw @ pw.T)` (host BLAS
     order).  With the confirmation band widened to every step, each decision is
