@@ -803,7 +803,13 @@ void eks_rank_update_frag_kernel(double* __restrict__ P, const int64_t n, const 
                 for (int r = 0; r < 4; ++r) {
                     const int64_t gi = r0 + wr + 16 * x + lk + 4 * r;
                     const int64_t gj = c0 + wc + 16 * y + lr;
-                    t[x][y][r] = (gi < n && gj < n && (!diag || gj <= gi)) ? P[gi * ld + gj] : 0.0;
+                    // P streams through once per update: non-temporal loads keep
+                    // it from evicting the K / PH^T operand quads from L2
+                    // (1.91 -> 1.81 ms per C4 update; non-temporal stores too:
+                    // 1.84 ms)
+                    t[x][y][r] = (gi < n && gj < n && (!diag || gj <= gi))
+                                     ? __builtin_nontemporal_load(&P[gi * ld + gj])
+                                     : 0.0;
                 }
     };
     load_p(acc, ti * kEksTile, tj * kEksTile, ti == tj);

@@ -167,12 +167,13 @@ def _rank_main(rank, world, n, lm, zs, ctl, q_out, q_in, conn):
         q_out.put((rank, repr(e), None))
 
 
-def test_dist_two_processes_share_one_gpu():
-    """Two ranks, two processes, one GPU: the IPC path of one process per GPU
-    (exchange regions exported / opened, device-side signalling across
+@pytest.mark.parametrize("world", [2, 4])
+def test_dist_two_processes_share_one_gpu(world):
+    """Two (four) ranks, one process each, one GPU: the IPC path of one process
+    per GPU (exchange regions exported / opened, device-side signalling across
     processes), replayed as hipGraphs; compared with one handle."""
     from slamhip.pf import DeviceParticleFilter
-    world, n, nl, steps = 2, 2 * 65536, 50, 16
+    n, nl, steps = world * 65536, 50, 16
     lm, zs, p = _world(n, nl, steps, 23)
     ctl = np.tile([p.vel, p.omega], (steps, 1))
     ctx = mp.get_context("spawn")
@@ -208,4 +209,4 @@ def test_dist_two_processes_share_one_gpu():
         assert st[4], "one shard per process: the one-launch resample exchange"
         assert [(r["max_idx"], r["weight_sum"], r["resampled"]) for r in ref] == res
     for k in range(4):
-        np.testing.assert_array_equal(np.concatenate([out[0][1][k], out[1][1][k]]), xs[k])
+        np.testing.assert_array_equal(np.concatenate([out[r][1][k] for r in range(world)]), xs[k])
