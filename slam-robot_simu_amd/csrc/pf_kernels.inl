@@ -1881,15 +1881,17 @@ __device__ void lean_place_fold(const SpecialIn* __restrict__ stage,
 // Number of systematic positions at or below v: #{i in [0, n) :
 // fl(fl(i (1/NP)) + ofs) <= v} (particle_filter.py:213-215; the positions are
 // monotone in i).  An estimate from the inverse, then exact steps.
+// The count is carried as a double (exact: n < 2^31), so the position of index
+// i is fl(fl(i (1/NP)) + ofs) without an int64 -> double conversion per probe.
 __device__ __forceinline__ int64_t positions_upto(const double v, const int64_t n,
                                                   const double rstep, const double ofs) {
     if (!(v >= ofs)) return 0;
-    double e = floor((v - ofs) * (double)n) + 1.0;
-    e = e < 0.0 ? 0.0 : (e > (double)n ? (double)n : e);
-    int64_t i = (int64_t)e;
-    while (i > 0 && (double)(i - 1) * rstep + ofs > v) --i;
-    while (i < n && (double)i * rstep + ofs <= v) ++i;
-    return i;
+    const double dn = (double)n;
+    double e = floor((v - ofs) * dn) + 1.0;
+    e = e < 0.0 ? 0.0 : (e > dn ? dn : e);
+    while (e > 0.0 && (e - 1.0) * rstep + ofs > v) e = e - 1.0;
+    while (e < dn && e * rstep + ofs <= v) e = e + 1.0;
+    return (int64_t)e;
 }
 
 // Pass C for one tile, once the specials are folded: every c_i from the

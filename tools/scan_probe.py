@@ -1,8 +1,8 @@
 """Phase timing of the resample passes (development tool): runs the C2
 workload through a probe build (tools/build_variant.sh probe -DSLAM_PROBE) and
 prints, for the last resample step of each batch, the wall-clock phases of
-scan_lean_classify_kernel (main / scans / place / fold) and of
-scan_lean_expand_kernel (c stored / inverse map) in microseconds."""
+scan_lean_merged_kernel (classify, ticket, tile-total scans, place + fold,
+release, c stored, inverse map) in microseconds."""
 import ctypes as C
 import os
 import sys
@@ -32,6 +32,6 @@ for r in range(10):
         print(f"batch {r}: no resample")
         continue
     d = lambda a, b: (t[b] - t[a]) * tick_us
-    print(f"batch {r}: classify main {d(0, 1):6.2f}  scans {d(1, 2):5.2f}  place {d(2, 3):5.2f}  "
-          f"fold {d(3, 4):5.2f} | expand: c {d(5, 6):6.2f}  inverse {d(6, 7):5.2f} | "
-          f"gap classify-end->expand {d(4, 5):5.2f}  nspecial {out[-1]['n_special'] if 'n_special' in out[-1] else '?'}")
+    print(f"batch {r}: classify {d(0, 12):6.2f}  ticket {d(12, 1):5.2f}  scans {d(1, 2):5.2f}  "
+          f"place+fold {d(2, 4):5.2f}  release {d(4, 5):5.2f} | expand: c {d(5, 6):6.2f}  "
+          f"inverse {d(6, 7):5.2f}  | total {d(0, 7):6.2f}  nspecial {out[-1].get('n_special', '?')}")
