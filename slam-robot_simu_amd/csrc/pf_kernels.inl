@@ -1910,7 +1910,7 @@ __device__ void wave_tile_expand(const int64_t tile, const TileScan& ts, const i
                                  const int32_t fofs, const SpecialOut* __restrict__ so,
                                  double* __restrict__ c, int64_t* __restrict__ mark,
                                  int32_t* __restrict__ carry, const double ofs, const int64_t gen,
-                                 const PredictConst& pc, const bool wt) {
+                                 const PredictConst& pc, const bool wt, const bool store_c = true) {
     const int lane = threadIdx.x & 63;
     auto ld_so = [wt, so](const int32_t m) { return wt ? ld_wt_struct(&so[m]) : so[m]; };
     const int64_t b = blockIdx.x;
@@ -1932,9 +1932,11 @@ __device__ void wave_tile_expand(const int64_t tile, const TileScan& ts, const i
         }
     }
     const int64_t j0 = tile * kWaveTile + 8 * lane;
+    if (store_c) {                                 // (the device-decided step needs only the marks)
 #pragma unroll
-    for (int h = 0; h < kScanPer; h += 2)          // c is padded to whole tiles
-        *reinterpret_cast<double2*>(c + j0 + h) = double2{out[h], out[h + 1]};
+        for (int h = 0; h < kScanPer; h += 2)      // c is padded to whole tiles
+            *reinterpret_cast<double2*>(c + j0 + h) = double2{out[h], out[h + 1]};
+    }
     PROBE_MAX(6);
     if (!mark) return;
     // ---- inverse map: runs of this lane's elements
@@ -2124,7 +2126,7 @@ __global__ __launch_bounds__(kScanThreads) void scan_lean_merged_kernel(
     if (blockIdx.x == 0) PROBE_AT(5);
     if (!active || !s_go || ld_wt_i(&flags[kFlagFallback])) return;
     wave_tile_expand(tile, ts, n, boffk, bofff, kofs, fofs, spec_out, c, mark, carry, ofs, gen, pc,
-                     true);
+                     true, force != 0);
 }
 
 // gather for the stand-alone resampling stage (particle_filter.py:216-222)
