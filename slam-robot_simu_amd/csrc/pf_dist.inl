@@ -986,12 +986,12 @@ __device__ __forceinline__ void dist_record(const int64_t n, const DeferParts& d
         for (int j = 0; j < 11; ++j) q[k][j] = dp.ps[j][bb];
     }
     const int part = tid & (kFinLeafLanes - 1);
-    double L[16];
+    double L[4];                                   // fused-block subtree sums
     {
         const int64_t c = tid / kFinLeafLanes;
-        const double* Lp = dp.leaf + 64 * (c < nfull ? c : 0) + 16 * part;
+        const double* Lp = dp.leaf + 16 * (c < nfull ? c : 0) + 4 * part;
 #pragma unroll
-        for (int j = 0; j < 16; ++j) L[j] = Lp[j];
+        for (int j = 0; j < 4; ++j) L[j] = Lp[j];
     }
     const int64_t bx0 = tid + (int64_t)kFinThreads * kFinRegBlocks;   // NP > 2^20 only
     double mlane = -1.0;
@@ -1035,11 +1035,11 @@ __device__ __forceinline__ void dist_record(const int64_t n, const DeferParts& d
         double v = 0.0;
         if (c < nfull) {
             if (c0 > 0) {
-                const double* Lp = dp.leaf + 64 * c + 16 * part;
+                const double* Lp = dp.leaf + 16 * c + 4 * part;
 #pragma unroll
-                for (int j = 0; j < 16; ++j) L[j] = Lp[j];
+                for (int j = 0; j < 4; ++j) L[j] = Lp[j];
             }
-            v = tree16(L);
+            v = (L[0] + L[1]) + (L[2] + L[3]);
         }
 #pragma unroll
         for (int d = 1; d < kFinLeafLanes; d <<= 1) {

@@ -50,15 +50,11 @@ __device__ __forceinline__ void fin_load_record(const DeferParts& dp, const int6
     for (int j = 0; j < 3; ++j) f.xe[j] = dp.pxe[j][b];
 }
 
-// pairwise sum of 16 consecutive leaves (a perfect subtree of the buffer's tree)
-__device__ __forceinline__ double tree16(const double* L) {
-    double a[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) a[j] = L[2 * j] + L[2 * j + 1];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) a[j] = a[2 * j] + a[2 * j + 1];
-    return (a[0] + a[1]) + (a[2] + a[3]);
-}
+// A lane of the np.sum pass takes 4 consecutive fused blocks of a buffer: each
+// block left the pairwise sum of its four 128-element leaves (a perfect
+// subtree of the buffer's tree), so (b0 + b1) + (b2 + b3) is the lane's
+// 16-leaf subtree.
+static_assert(kSumChunk == 16 * kPartPer, "a buffer is 16 fused blocks, 4 per np.sum lane");
 
 __global__ __launch_bounds__(kFinThreads) void finalize_deferred_kernel(
     const int64_t n, const DeferParts dp, const double* __restrict__ w_un,
@@ -103,12 +99,12 @@ __global__ __launch_bounds__(kFinThreads) void finalize_deferred_kernel(
         for (int j = 0; j < 11; ++j) q[k][j] = dp.ps[j][bb];
     }
     const int part = tid & (kFinLeafLanes - 1);
-    double L[16];
+    double L[4];                                   // fused-block subtree sums
     {
         const int64_t c = tid / kFinLeafLanes;
-        const double* Lp = dp.leaf + 64 * (c < nfull ? c : 0) + 16 * part;
+        const double* Lp = dp.leaf + 16 * (c < nfull ? c : 0) + 4 * part;
 #pragma unroll
-        for (int j = 0; j < 16; ++j) L[j] = Lp[j];
+        for (int j = 0; j < 4; ++j) L[j] = Lp[j];
     }
     // ---- lane partial sums scaled to the lane's max (rescaled to the global
     // max once that is known); q dies here except the totals q[k][0]
@@ -154,11 +150,11 @@ __global__ __launch_bounds__(kFinThreads) void finalize_deferred_kernel(
         double v = 0.0;
         if (tid / kFinLeafLanes < cnt) {
             if (c0 > 0) {
-                const double* Lp = dp.leaf + 64 * c + 16 * part;
+                const double* Lp = dp.leaf + 16 * c + 4 * part;
 #pragma unroll
-                for (int j = 0; j < 16; ++j) L[j] = Lp[j];
+                for (int j = 0; j < 4; ++j) L[j] = Lp[j];
             }
-            v = tree16(L);
+            v = (L[0] + L[1]) + (L[2] + L[3]);
         }
 #pragma unroll
         for (int d = 1; d < kFinLeafLanes; d <<= 1) {

@@ -23,7 +23,8 @@ constexpr int kPartPer = 256 * kDeferPPT;            // particles per fused bloc
 // kPartPer-particle block, its max unnormalised weight M_b with the first index,
 // sums scaled by 1/M_b (sum u, sum u^2, sum u d, sum u d d^T with u = w_un/M_b
 // and d = particle - refp; scaling keeps squares of tiny likelihoods out of
-// the subnormal range) and its four 128-element np.sum leaf sums.
+// the subnormal range) and its np.sum subtree (the pairwise sum of its four
+// 128-element leaves).
 // Per block also: the largest w_un before the first max (-1 if none), so
 // the step end knows without a rescan whether a smaller weight can round to
 // the same normalised maximum, and the particle at the first max (x_est).
@@ -33,7 +34,7 @@ struct DeferParts {
     double* ppre;           // max w_un at indices before pidx (-1: none)
     double* pxe[3];         // particle (x, y, th) at pidx
     double* ps[11];         // sw, sw2, m1[3], m2[6]
-    double* leaf;           // [(kPartPer / 128) * blocks]
+    double* leaf;           // [blocks] the block's np.sum subtree (its kPartPer / 128 leaves, pairwise)
     int64_t* mark;          // [npad] resample-run starts: (RNG step << 32) | source (expand pass)
     int32_t* carry;         // [blocks] source of each fused block's first position
 };

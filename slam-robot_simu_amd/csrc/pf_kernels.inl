@@ -306,9 +306,20 @@ __device__ void defer_epilogue(const int64_t base, const int64_t n, const double
         double acc = s_seg[16 * t];
         for (int mm = 1; mm < 16; ++mm) acc = acc + s_seg[16 * t + mm];
         dp.ps[t][blk] = acc;
-    } else if (t >= 64 && t < 64 + kLeaves) {
-        const double* r = s_acc + 8 * (t - 64);
-        dp.leaf[kLeaves * blk + (t - 64)] = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+    } else if (t >= 64 && t < 128) {
+        // the block's np.sum subtree: its kLeaves leaves, then their pair sums
+        // (wave 1; lane l < kLeaves holds leaf l)
+        double v = 0.0;
+        if (t - 64 < kLeaves) {
+            const double* r = s_acc + 8 * (t - 64);
+            v = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+        }
+#pragma unroll
+        for (int d = 1; d < kLeaves; d <<= 1) {
+            const double o = __shfl_xor(v, d, 64);
+            v = (lane & d) ? (o + v) : (v + o);
+        }
+        if (t == 64) dp.leaf[blk] = v;
     } else if (t == 128) {
         dp.pmax[blk] = M;
         dp.pidx[blk] = bi;
