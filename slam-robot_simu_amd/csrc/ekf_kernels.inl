@@ -267,20 +267,35 @@ __global__ __launch_bounds__(256) void eks_pht_kernel(const double* __restrict__
         return;
     }
     const double p0 = psym(P, ld, i, 0), p1 = psym(P, ld, i, 1), p2 = psym(P, ld, i, 2);
-    for (int t = 0; t < k; ++t) {
-        const int64_t c0 = 3 + 3 * ids[t];
-        const double l0 = psym(P, ld, i, c0), l1 = psym(P, ld, i, c0 + 1),
-                     l2 = psym(P, ld, i, c0 + 2);
-        const double* H = hs + 18 * t;
+    // landmarks in groups of 8: the 24 P entries of a group are requested
+    // together (one memory round trip per group, not per landmark)
+    constexpr int kG = 8;
+    for (int t0 = 0; t0 < k; t0 += kG) {
+        double l[kG][3];
 #pragma unroll
-        for (int a = 0; a < 3; ++a) {
-            double acc = p0 * H[3 * a];
-            acc = fma(p1, H[3 * a + 1], acc);
-            acc = fma(p2, H[3 * a + 2], acc);
-            acc = fma(l0, H[9 + 3 * a], acc);
-            acc = fma(l1, H[9 + 3 * a + 1], acc);
-            acc = fma(l2, H[9 + 3 * a + 2], acc);
-            out[3 * t + a] = acc;
+        for (int g = 0; g < kG; ++g) {
+            if (t0 + g < k) {
+                const int64_t c0 = 3 + 3 * ids[t0 + g];
+#pragma unroll
+                for (int j = 0; j < 3; ++j) l[g][j] = psym(P, ld, i, c0 + j);
+            }
+        }
+#pragma unroll
+        for (int g = 0; g < kG; ++g) {
+            const int t = t0 + g;
+            if (t < k) {
+                const double* H = hs + 18 * t;
+#pragma unroll
+                for (int a = 0; a < 3; ++a) {
+                    double acc = p0 * H[3 * a];
+                    acc = fma(p1, H[3 * a + 1], acc);
+                    acc = fma(p2, H[3 * a + 2], acc);
+                    acc = fma(l[g][0], H[9 + 3 * a], acc);
+                    acc = fma(l[g][1], H[9 + 3 * a + 1], acc);
+                    acc = fma(l[g][2], H[9 + 3 * a + 2], acc);
+                    out[3 * t + a] = acc;
+                }
+            }
         }
     }
     for (int u = 3 * k; u < M; ++u) out[u] = 0.0;
