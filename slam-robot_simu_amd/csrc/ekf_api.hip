@@ -36,6 +36,7 @@ struct slam_ekfslam {
     int32_t kernel_sel = 0;        // 0: fragment-streaming (m <= 64), 1: LDS-staged
     int32_t frag_shape = 0;        // 0: 8 waves of 32 x 64, 1: 16 waves of 32 x 32
     int32_t frag_pf = 0;           // experiment: where the next P block is requested
+    int32_t apply_lds = 0;         // SLAM_EKS_APPLY=lds: the one-wave-per-row K = PH^T S^-1
     hipStream_t stream = nullptr;
     double* P = nullptr;           // n x ld, lower triangle current
     double* mu = nullptr;          // n
@@ -152,8 +153,13 @@ int eks_update(slam_ekfslam* h, int32_t k, const int64_t* ids, const double* obs
                        h->hs, h->rd, k, M, h->sinv);
     SLAM_HIP_TRY(hipEventRecord(h->ev[2], h->stream));
     const int64_t apply_grid = std::min<int64_t>(512, (h->n_pad + 15) / 16);
-    hipLaunchKernelGGL(eks_apply_kernel, dim3((unsigned)apply_grid), dim3(kEksApplyThreads),
-                       sbytes, h->stream, h->pht, h->sinv, h->e, h->n, h->n_pad, M, h->kg, h->mu);
+    if (M <= 64 && !h->apply_lds) {
+        hipLaunchKernelGGL(eks_apply_mfma_kernel, dim3((unsigned)((h->n_pad / 16 + 3) / 4)), dim3(256),
+                           0, h->stream, h->pht, h->sinv, h->e, h->n, h->n_pad, M, h->kg, h->mu);
+    } else {
+        hipLaunchKernelGGL(eks_apply_kernel, dim3((unsigned)apply_grid), dim3(kEksApplyThreads),
+                           sbytes, h->stream, h->pht, h->sinv, h->e, h->n, h->n_pad, M, h->kg, h->mu);
+    }
     SLAM_HIP_TRY(hipEventRecord(h->ev[3], h->stream));
     const int64_t nt = h->n_pad / kEksTile;
     const int64_t tiles = nt * (nt + 1) / 2;
@@ -401,6 +407,8 @@ int slam_ekfslam_create(const slam_ekfslam_config* cfg, int64_t n_landmarks, int
         h->kernel_sel = sel == "pipe" ? 1 : 0;
         h->frag_shape = (sel == "frag16") ? 1 : 0;
         h->frag_pf = sel == "pfmid" ? 1 : sel == "pf0" ? 2 : 0;
+        const char* ap = std::getenv("SLAM_EKS_APPLY");
+        h->apply_lds = (ap && std::string(ap) == "lds") ? 1 : 0;
         const hipError_t oe =
             h->frag_shape == 1
                 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(

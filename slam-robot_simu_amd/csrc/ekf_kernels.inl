@@ -583,6 +583,61 @@ constexpr int kEksPipeBB = 8 / kEksPipeWC;          // 16-column MFMA blocks per
 constexpr int kEksPipeWPE = kEksPipeWC;             // waves per SIMD of the one workgroup per CU
 typedef double eks_d4 __attribute__((ext_vector_type(4)));
 
+// K = PH^T S^-1 and mu += K e for M <= 64 on the fp64 MFMA (the product is a
+// GEMM, n_pad x M x M): one wave per 16-row strip, four 16-column blocks,
+// v_mfma_f64_16x16x4 over the k-quads (entries past M read as 0), then each
+// row's K e from its K entries (a 16-lane butterfly) and the mu update.
+// 62 -> 26 us per C4 update against eks_apply_kernel (which stays for M > 64;
+// SLAM_EKS_APPLY=lds selects it for comparison).
+__global__ __launch_bounds__(256) void eks_apply_mfma_kernel(
+    const double* __restrict__ pht, const double* __restrict__ sinv, const double* __restrict__ e,
+    const int64_t n, const int64_t n_pad, const int32_t M, double* __restrict__ kg,
+    double* __restrict__ mu) {
+    const int lane = threadIdx.x & 63, lr = lane & 15, lk = lane >> 4;
+    const int64_t row0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 16;
+    if (row0 >= n_pad) return;                       // wave-uniform
+    eks_d4 acc[4];
+#pragma unroll
+    for (int cb = 0; cb < 4; ++cb) acc[cb] = eks_d4{0.0, 0.0, 0.0, 0.0};
+    const int nq = (M + 3) / 4;
+    for (int q = 0; q < nq; ++q) {
+        const int v = 4 * q + lk;
+        const double a = (v < M) ? pht[(row0 + lr) * M + v] : 0.0;
+#pragma unroll
+        for (int cb = 0; cb < 4; ++cb) {
+            const int u = 16 * cb + lr;
+            const double b = (v < M && u < M) ? sinv[v * M + u] : 0.0;
+            acc[cb] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc[cb], 0, 0, 0);
+        }
+    }
+    double dm[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int cb = 0; cb < 4; ++cb) {
+        const int u = 16 * cb + lr;
+        const double eu = (u < M) ? e[u] : 0.0;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            if (u < M) kg[(row0 + lk + 4 * r) * M + u] = acc[cb][r];
+            dm[r] = fma(acc[cb][r], eu, dm[r]);
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int d = 1; d < 16; d <<= 1) dm[r] += __shfl_xor(dm[r], d, 64);
+    if (lr == 0) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int64_t i = row0 + lk + 4 * r;
+            if (i < n) {
+                double m = mu[i] + dm[r];
+                if (i == 2) m = wrap_angle(m);
+                mu[i] = m;
+            }
+        }
+    }
+}
+
 __device__ __forceinline__ void eks_tile_rc(const int64_t L, int64_t& ti, int64_t& tj) {
     ti = (int64_t)((sqrt(8.0 * (double)L + 1.0) - 1.0) * 0.5);
     while (ti * (ti + 1) / 2 > L) --ti;
