@@ -1037,9 +1037,22 @@ __device__ void block_scan_array(const T* in, T* out, const int nb, T* total, T*
             return (T)ld_wt_i((const int32_t*)p);
         }
     };
+    // up to kMaxPer words per thread stay in registers between the two passes
+    // (one memory round trip instead of two)
+    constexpr int kMaxPer = 8;
+    const bool cached = per <= kMaxPer;
+    T cv[kMaxPer];
     T loc = T(0);
-    for (int k = 0; k < per; ++k)
-        if (b0 + k < nb) loc = loc + ld(in + b0 + k);
+    if (cached) {
+#pragma unroll
+        for (int k = 0; k < kMaxPer; ++k) {
+            cv[k] = (k < per && b0 + k < nb) ? ld(in + b0 + k) : T(0);
+            loc = loc + cv[k];
+        }
+    } else {
+        for (int k = 0; k < per; ++k)
+            if (b0 + k < nb) loc = loc + ld(in + b0 + k);
+    }
     T tot;
     T ex = block_excl_scan<T, NT>(loc, sh, tot);
     auto st = [wt](T* p, const T v) {
@@ -1053,13 +1066,77 @@ __device__ void block_scan_array(const T* in, T* out, const int nb, T* total, T*
             st_wt_i((int32_t*)p, (int32_t)v);
         }
     };
-    for (int k = 0; k < per; ++k)
-        if (b0 + k < nb) {
-            const T v = ld(in + b0 + k);
-            st(out + b0 + k, ex);
-            ex = ex + v;
-        }
+    if (cached) {
+#pragma unroll
+        for (int k = 0; k < kMaxPer; ++k)
+            if (k < per && b0 + k < nb) {
+                st(out + b0 + k, ex);
+                ex = ex + cv[k];
+            }
+    } else {
+        for (int k = 0; k < per; ++k)
+            if (b0 + k < nb) {
+                const T v = ld(in + b0 + k);
+                st(out + b0 + k, ex);
+                ex = ex + v;
+            }
+    }
     if (threadIdx.x == 0 && total) st(total, tot);
+}
+
+// The two tile-total scans of the exact cumsum (increments k: u64, special
+// counts f: i32) with both arrays' loads issued together (one memory round
+// trip for both); the same sums as two block_scan_array calls.
+template <int NT>
+__device__ void block_scan_pair(const uint64_t* kin, uint64_t* kout, uint64_t* ktotal,
+                                const int32_t* fin, int32_t* fout, int32_t* ftotal, const int nb,
+                                uint64_t* shk, int32_t* shf, int32_t* f_lds = nullptr) {
+    constexpr int kMaxPer = 8;
+    const int per = (nb + NT - 1) / NT;
+    if (per > kMaxPer) {
+        block_scan_array<uint64_t, NT>(kin, kout, nb, ktotal, shk, true);
+        __syncthreads();
+        block_scan_array<int32_t, NT>(fin, fout, nb, ftotal, shf, true);
+        if (f_lds) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            for (int k = threadIdx.x; k < nb; k += NT) f_lds[k] = ld_wt_i(&fout[k]);
+        }
+        return;
+    }
+    const int b0 = threadIdx.x * per;
+    uint64_t kv[kMaxPer];
+    int32_t fv[kMaxPer];
+#pragma unroll
+    for (int k = 0; k < kMaxPer; ++k) {
+        const bool ok = k < per && b0 + k < nb;
+        kv[k] = ok ? ld_wt(kin + b0 + k) : 0;
+        fv[k] = ok ? ld_wt_i(fin + b0 + k) : 0;
+    }
+    uint64_t kloc = 0;
+    int32_t floc = 0;
+#pragma unroll
+    for (int k = 0; k < kMaxPer; ++k) {
+        kloc = kloc + kv[k];
+        floc = floc + fv[k];
+    }
+    uint64_t ktot;
+    int32_t ftot;
+    uint64_t kex = block_excl_scan<uint64_t, NT>(kloc, shk, ktot);
+    int32_t fex = block_excl_scan<int32_t, NT>(floc, shf, ftot);
+#pragma unroll
+    for (int k = 0; k < kMaxPer; ++k)
+        if (k < per && b0 + k < nb) {
+            st_wt(kout + b0 + k, kex);
+            st_wt_i(fout + b0 + k, fex);
+            if (f_lds) f_lds[b0 + k] = fex;
+            kex = kex + kv[k];
+            fex = fex + fv[k];
+        }
+    if (threadIdx.x == 0) {
+        st_wt(ktotal, ktot);
+        st_wt_i(ftotal, ftot);
+    }
 }
 
 // ====================================================================
@@ -1800,12 +1877,12 @@ __device__ void lean_place_fold(const SpecialIn* __restrict__ stage,
                                 const int32_t M, const uint64_t ktot, const int64_t n,
                                 SpecialOut* __restrict__ out, int32_t* __restrict__ flags,
                                 const double* __restrict__ w_un, const double* __restrict__ s_in,
-                                const double np_recip, double* __restrict__ c) {
-    __shared__ int32_t s_off[kFoldTilesLds];
+                                const double np_recip, double* __restrict__ c,
+                                int32_t* __restrict__ s_off) {
+    // s_off: the tiles' special offsets in LDS (kFoldTilesLds words), already
+    // filled by the scan that produced bofff when ntiles fits
     __shared__ int s_bad;
     const bool in_lds = ntiles <= kFoldTilesLds;
-    if (in_lds)
-        for (int k = threadIdx.x; k < ntiles; k += blockDim.x) s_off[k] = ld_wt_i(&bofff[k]);
     if (threadIdx.x == 0) {
         s_bad = 0;
         flags[kFlagNSpecial] = M;
@@ -2009,14 +2086,14 @@ __device__ __forceinline__ void lean_last_block(uint64_t* __restrict__ bk, int32
                                                 const double np_recip, double* __restrict__ c) {
     __shared__ uint64_t shk[kScanThreads / 64 + 1];
     __shared__ int32_t shf[kScanThreads / 64 + 1];
+    __shared__ int32_t s_off[kFoldTilesLds];
     PROBE_AT(1);
-    block_scan_array<uint64_t, kScanThreads>(bk, boffk, nblocks, ktot, shk, true);
-    __syncthreads();
-    block_scan_array<int32_t, kScanThreads>(bf, bofff, nblocks, nspec, shf, true);
+    block_scan_pair<kScanThreads>(bk, boffk, ktot, bf, bofff, nspec, nblocks, shk, shf,
+                                  nblocks <= kFoldTilesLds ? s_off : nullptr);
     __syncthreads();
     PROBE_AT(2);
     lean_place_fold(stage, boffk, bofff, nblocks, ld_wt_i(nspec), ld_wt(ktot), n, spec_out, flags,
-                    w_un, s_in, np_recip, c);
+                    w_un, s_in, np_recip, c, s_off);
     PROBE_AT(4);
 }
 
