@@ -460,6 +460,8 @@ def main():
         # 128-byte RCCL id travels through torch.distributed once).  At
         # world = 1 the single shard runs the same kernels in-process.
         from slamhip.dist import Comm, DistFilter
+        if os.environ.get("SLAM_BENCH_FAIL_RANK") == str(rank):      # tests of the fallback
+            raise RuntimeError("injected sharded-mode failure (SLAM_BENCH_FAIL_RANK)")
         n_global = world * NP_PER_GPU
         comm = None
         kw = dict(dt=dt, motion="velocity", likelihood=likelihood, seed=1234, device=local_rank)
@@ -534,7 +536,34 @@ def main():
         pf.close()
         return el
 
-    elapsed, out, timing = measure(args.likelihood)
+    sharded_error = None
+    if args.mode == "sharded" and dist is not None and world > 1:
+        # the sharded exchange needs every rank's GPU reachable over xGMI; if
+        # any rank fails (every wait in the library is bounded, so a failure
+        # raises rather than hangs), all ranks agree through the harness's
+        # process group and fall back to independent replicas, and the JSON
+        # line says so (config.parallelism, sharded_error)
+        import torch
+        try:
+            result = measure(args.likelihood)
+            ok = 1
+        except Exception as e:                          # noqa: BLE001 - reported below
+            result, ok = None, 0
+            sharded_error = f"rank {rank}: {type(e).__name__}: {e}"[:400]
+            print(f"bench: sharded mode failed on rank {rank}: {e}", file=sys.stderr)
+        flag = torch.tensor([ok], dtype=torch.int32,
+                            device="cpu" if share_gpu else f"cuda:{local_rank}")
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+        if int(flag.item()) == 1:
+            elapsed, out, timing = result
+        else:
+            errs = [None] * world
+            dist.all_gather_object(errs, sharded_error)
+            sharded_error = "; ".join(e for e in errs if e) or "another rank failed"
+            args.mode = "replicas"
+            elapsed, out, timing = measure(args.likelihood)
+    else:
+        elapsed, out, timing = measure(args.likelihood)
     fused_ms, fused_n = timing[0]
     red_ms, red_n = timing[1]
     res_ms, res_n = timing[2]
@@ -626,6 +655,8 @@ def main():
         except Exception as e:            # reported, never silently replaced
             vb = {"error": f"{type(e).__name__}: {e}"}
         line["cpu_baseline_vectorised"] = vb
+    if sharded_error is not None:
+        line["sharded_error"] = sharded_error
     if rank == 0:
         print(json.dumps(line), flush=True)
     if dist is not None:

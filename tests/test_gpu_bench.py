@@ -78,3 +78,20 @@ def test_bench_sharded_two_ranks_share_one_gpu():
     assert d["n_gpus"] == 2 and d["config"]["parallelism"] == "sharded2"
     assert d["value"] > 1e10 and d["resample_steps"] >= 1
     assert abs(d["value"] - 2 * 2 ** 20 * 100 / (d["ms_per_step"] / 1e3)) <= 1e-6 * d["value"]
+
+
+def test_bench_sharded_failure_falls_back_to_replicas():
+    """A rank that cannot run the sharded exchange (injected on rank 1): every
+    rank agrees and measures independent replicas; the line says so."""
+    args = [os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "6", "--warmup", "2",
+            "--no-secondary", "--no-cpu-baseline"]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", "29543"] + args
+    env = dict(os.environ, SLAM_BENCH_SHARE_GPU="1", SLAM_BENCH_FAIL_RANK="1")
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["config"]["parallelism"] == "replicas2"
+    assert "injected" in d["sharded_error"] and d["value"] > 1e10
