@@ -460,8 +460,8 @@ def main():
         # 128-byte RCCL id travels through torch.distributed once).  At
         # world = 1 the single shard runs the same kernels in-process.
         from slamhip.dist import Comm, DistFilter
-        if os.environ.get("SLAM_BENCH_FAIL_RANK") == str(rank):      # tests of the fallback
-            raise RuntimeError("injected sharded-mode failure (SLAM_BENCH_FAIL_RANK)")
+        if os.environ.get("SLAM_BENCH_FAIL_SHARDED") == "1":         # tests of the fallback
+            raise RuntimeError("injected sharded-mode failure (SLAM_BENCH_FAIL_SHARDED)")
         n_global = world * NP_PER_GPU
         comm = None
         kw = dict(dt=dt, motion="velocity", likelihood=likelihood, seed=1234, device=local_rank)

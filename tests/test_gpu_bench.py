@@ -81,13 +81,14 @@ def test_bench_sharded_two_ranks_share_one_gpu():
 
 
 def test_bench_sharded_failure_falls_back_to_replicas():
-    """A rank that cannot run the sharded exchange (injected on rank 1): every
-    rank agrees and measures independent replicas; the line says so."""
+    """Ranks that cannot run the sharded exchange (a failure injected before the
+    exchange is set up): the ranks agree and measure independent replicas, and
+    the line says so."""
     args = [os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "6", "--warmup", "2",
             "--no-secondary", "--no-cpu-baseline"]
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", "29543"] + args
-    env = dict(os.environ, SLAM_BENCH_SHARE_GPU="1", SLAM_BENCH_FAIL_RANK="1")
+    env = dict(os.environ, SLAM_BENCH_SHARE_GPU="1", SLAM_BENCH_FAIL_SHARDED="1")
     r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=110)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
