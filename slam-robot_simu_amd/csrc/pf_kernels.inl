@@ -196,7 +196,8 @@ __device__ __forceinline__ void max_first(double& v, int64_t& i, const double ov
 // right, then the 16 segments.
 __device__ void defer_epilogue(const int64_t base, const int64_t n, const double* wv,
                                const double* xv, const double* yv, const double* tv,
-                               const double* __restrict__ refp, const DeferParts& dp) {
+                               const double* __restrict__ refp, const DeferParts& dp,
+                               const int wave_s) {
     constexpr int kQ = 11;
     constexpr int kLeaves = kPartPer / 128;
     __shared__ double s_w[kPartPer];
@@ -205,7 +206,9 @@ __device__ void defer_epilogue(const int64_t base, const int64_t n, const double
     __shared__ double s_acc[8 * kLeaves];
     __shared__ double s_mv[4], s_pre[4];
     __shared__ int64_t s_mi[4];
-    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    // the thread index from the wave's SGPR index and the lane id (both
+    // rematerialised: threadIdx.x itself would be held across the kernel)
+    const int lane = (int)__lane_id(), wave = wave_s, t = (wave << 6) | lane;
     const int blk = blockIdx.x;
     // lane max and its first particle, then the wave max
     double m = -1.0;
@@ -488,7 +491,7 @@ __device__ SLAM_SLOW_ATTR double logsum_slow(const double xn, const double yn, c
                                            const double cp, const double* __restrict__ lm,
                                            const double* __restrict__ z, const LikConst& lc) {
     const int nl = lc.nl;
-    const int lane = threadIdx.x & 63;
+    const int lane = (int)__lane_id();
     double ch = 0.0, cl = 0.0;               // sum of q over the landmarks before this chunk
     double s_prev = 0.0;                     // log prefix before j0 (0: empty product = 1)
     int j0 = nl;
@@ -554,7 +557,7 @@ __device__ __forceinline__ void likelihood_lanes(const double* xn, const double*
                                                  const double* __restrict__ lm,
                                                  const double* __restrict__ z,
                                                  const double* __restrict__ zc, const LikConst& lc,
-                                                 double* bn) {
+                                                 double* bn, const int wave_s) {
     const int nl = lc.nl;
     if (LIK == SLAM_LIK_PRODUCT) {
         double acc[P];
@@ -661,7 +664,8 @@ __device__ __forceinline__ void likelihood_lanes(const double* xn, const double*
         __shared__ int s_nslow;
         __shared__ double s_pt[4][kMax];
         __shared__ double s_bn[kMax];
-        if (threadIdx.x == 0) s_nslow = 0;
+        const int tl = (wave_s << 6) | (int)__lane_id();
+        if (tl == 0) s_nslow = 0;
         __syncthreads();
         int slot[P];
 #pragma unroll
@@ -678,15 +682,15 @@ __device__ __forceinline__ void likelihood_lanes(const double* xn, const double*
         __syncthreads();
         const int ns = s_nslow;
 #ifdef SLAM_PROBE_COUNT_SLOW                               // probe builds only
-        if (threadIdx.x == 0) {
+        if (tl == 0) {
             atomicAdd(&g_probe_slow[0], (unsigned long long)ns);
             atomicAdd(&g_probe_slow[1], 1ull);
         }
 #endif
         // one slow particle per wave, all 64 lanes on it (wave-uniform loop)
-        for (int t = (int)(threadIdx.x >> 6); t < ns; t += (int)(blockDim.x >> 6)) {
+        for (int t = wave_s; t < ns; t += (int)(blockDim.x >> 6)) {
             const double r = logsum_slow(s_pt[0][t], s_pt[1][t], s_pt[2][t], s_pt[3][t], lm, z, lc);
-            if ((threadIdx.x & 63) == 0) s_bn[t] = r;
+            if ((tl & 63) == 0) s_bn[t] = r;
         }
         __syncthreads();
 #pragma unroll
@@ -728,6 +732,7 @@ __global__ __launch_bounds__(256) SLAM_FUSED_ATTR void pf_fused_kernel(
     constexpr int P = DEFER ? kDeferPPT : 1;
     const int64_t base = (int64_t)blockIdx.x * (256 * P);
     const int64_t i0 = base + P * (int64_t)threadIdx.x;
+    const int wave_s = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
     bool valid[P];
     int64_t idx[P];
 #pragma unroll
@@ -912,7 +917,8 @@ __global__ __launch_bounds__(256) SLAM_FUSED_ATTR void pf_fused_kernel(
 
     // ---- likelihood and weight (particle_filter.py:170-198)
     double bn[P];
-    likelihood_lanes<LIK, P>(xv, yv, sp, cp, lm, zs, io.zc + (size_t)st * kClosedWords, lc, bn);
+    likelihood_lanes<LIK, P>(xv, yv, sp, cp, lm, zs, io.zc + (size_t)st * kClosedWords, lc, bn,
+                             wave_s);
     // previous weights: particle_filter.py:222 (a resampled step starts from
     // 1/NP) / :235-236 (deferred: w_un / s, NaN -> 1/NP)
     double wv[P];
@@ -928,7 +934,7 @@ __global__ __launch_bounds__(256) SLAM_FUSED_ATTR void pf_fused_kernel(
         for (int h = 0; h < P; h += 2)
             *reinterpret_cast<double2*>(w_un + i0 + h) = double2{wv[h], wv[h + 1]};
 #ifndef SLAM_NO_EPILOGUE
-        defer_epilogue(base, n, wv, xv, yv, tv, refp, dp);
+        defer_epilogue(base, n, wv, xv, yv, tv, refp, dp, wave_s);
 #endif
     } else if (valid[0]) {
         w_un[i0] = wv[0];
