@@ -19,7 +19,15 @@ particles, per-rank reduction records) are pushes into peer memory over xGMI
 with device-side signalling, bootstrapped over an RCCL communicator; 8 steps
 per hipGraph, no host decision per step.  --mode replicas runs independent
 Monte-Carlo realisations (no data-path exchange; the N = 1 default).  At N = 1
-the line also carries "sharded1": the sharded step's kernels on one shard.
+the line also carries "sharded1": the sharded step's kernels on one shard, and
+"strong_single": one handle of 2^23 particles (the strong-scaling reference).
+
+    --total-particles T   strong scaling: one filter of T particles split over
+                          the N ranks (T / N per GPU; "scaling": "strong")
+
+The sharded setup and run agree across ranks at fixed points (every rank
+reaches the same collectives whether or not it failed locally), so one rank's
+failure sends every rank to the replica fallback together.
 """
 from __future__ import annotations
 
@@ -36,10 +44,15 @@ sys.path.insert(0, os.path.join(ROOT, "slam-robot_simu_amd"))
 
 METRIC = "particle-observation updates/sec @1M particles×100 landmarks; 1/2/4/8-GPU scaling"
 NP_PER_GPU = 1 << 20
+STRONG_TOTAL = 1 << 23          # BASELINE configs[2]'s total particles
 NL = 100
 FP64_PEAK_TFLOPS = 78.6          # MI355X FP64 (vector = matrix), spec
 HBM_PEAK_GBS = 8000.0
-# algorithmic fp64 operations per particle-landmark update (fma = 2, exp = div = 1):
+VALU_SLOTS_PER_S = 1024 * 2.4e9 / 4   # wave64 VALU instructions/s: 1,024 SIMDs, 4 cycles each, 2.4 GHz
+# The reference algorithm's fp64 operations per particle-landmark update (fma =
+# 2, exp = div = 1) -- reported as "reference_equivalent_tflops" only: the
+# log-sum kernel evaluates the landmark sum in closed form and does not execute
+# them; roofline.achieved is the kernel's EXECUTED fp64 work (PMC).
 #   product (particle_filter.py:187-192 + mlab.bivariate_normal, factor by factor):
 #     diff 2, rotate 6, residual 2, q = dx^2/sx^2 + dy^2/sy^2 5, -q/2 1, exp 1,
 #     /den 1, running product 1  -> 19
@@ -197,12 +210,14 @@ def pf_sources_sha():
     return h.hexdigest()[:16]
 
 
-def load_pmc_traffic():
-    """HBM bytes per launch of the fused kernel from the rocprofv3 PMC passes of
-    tools/pmc.sh (profiles/pmc_traffic.json, FETCH_SIZE x2 + WRITE_SIZE per the
-    microarch guide).  The counters cannot be read from inside this process;
-    the file records the sources it was measured on, and a figure measured on
-    other sources is reported as null (stale), never as this kernel's."""
+def load_pmc_traffic(likelihood="logsum"):
+    """Per-launch counters of the fused kernel from the rocprofv3 PMC passes of
+    tools/pmc.sh (profiles/pmc_traffic.json): HBM bytes (FETCH_SIZE x2 +
+    WRITE_SIZE per the microarch guide), executed fp64 flops
+    (SQ_INSTS_VALU_{ADD,MUL,FMA,TRANS}_F64 x 64 lanes, fma = 2) and VALU
+    wave-instructions.  The counters cannot be read from inside this process;
+    the file records the sources it was measured on, and figures measured on
+    other sources are reported as null (stale), never as this kernel's."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(path) as f:
@@ -212,8 +227,53 @@ def load_pmc_traffic():
     cur = pf_sources_sha()
     if d.get("sources_sha") != cur:
         return None, f"stale: measured on sources {d.get('sources_sha')}, current {cur}", {}
+    if likelihood != "logsum":
+        k = d.get("kernels", {}).get(likelihood, {})
+        return k.get("hbm_bytes"), f"rocprofv3 PMC ({d.get('source')}), sources {cur}", k
     return d.get("fused_kernel_hbm_bytes_per_launch"), \
         f"rocprofv3 PMC ({d.get('source')}), sources {cur}", d.get("fused_kernel", {})
+
+
+def fused_roofline(likelihood, n_particles, fused_avg_s):
+    """Roofline of the fused predict + likelihood kernel from EXECUTED work
+    (VERDICT r2): executed fp64 flops (PMC) / the live average launch against
+    the fp64 peak, and HBM bytes / launch against 8 TB/s -- the binding one of
+    the two is `bound` / `achieved` / `frac`; the VALU issue fraction (the
+    kernel's actual limiter) and the reference algorithm's flop-equivalent rate
+    are reported beside them."""
+    traffic, src, pmc = load_pmc_traffic(likelihood)
+    alg_bytes = BYTES_PER_PARTICLE * n_particles
+    hbm_alg_gbs = alg_bytes / fused_avg_s / 1e9
+    hbm = {"achieved": hbm_alg_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+           "frac": hbm_alg_gbs / HBM_PEAK_GBS, "algorithmic_bytes": alg_bytes,
+           "note": "64 B/particle: x, y, th (24) + w (8) read and written"}
+    if traffic:
+        hbm["traffic_gbs"] = traffic / fused_avg_s / 1e9
+        hbm["traffic_frac"] = hbm["traffic_gbs"] / HBM_PEAK_GBS
+    fp = {"achieved": None, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": None}
+    if pmc.get("fp64_flops"):
+        fp["achieved"] = pmc["fp64_flops"] / fused_avg_s / 1e12
+        fp["frac"] = fp["achieved"] / FP64_PEAK_TFLOPS
+        fp["executed_flops_per_launch"] = pmc["fp64_flops"]
+    fp_frac = fp["frac"] if fp["frac"] is not None else -1.0
+    main = fp if fp_frac >= hbm["frac"] else hbm
+    rf = {"bound": "valu_fp64" if main is fp else "hbm",
+          "kernel": f"pf_fused_kernel<velocity, {likelihood}> (predict + likelihood + block epilogue)",
+          "achieved": main["achieved"], "peak": main["peak"], "unit": main["unit"],
+          "frac": main["frac"], "traffic": traffic, "traffic_source": src,
+          "avg_launch_ms": fused_avg_s * 1e3, "fp64": fp, "hbm": hbm,
+          "reference_equivalent_tflops":
+              FLOPS_PER_UPDATE[likelihood] * n_particles * NL / fused_avg_s / 1e12,
+          "note": "achieved/frac: the binding one of executed fp64 (PMC flops / live launch "
+                  "time / 78.6 TF) and HBM (algorithmic bytes / live launch time / 8 TB/s); "
+                  "the kernel is VALU-issue bound (valu_issue_frac: PMC wave64 VALU "
+                  "instructions x 4 cycles over 1,024 SIMDs x 2.4 GHz); "
+                  "reference_equivalent_tflops counts the reference's per-landmark flops "
+                  "(SURVEY 8(d)), which the closed-form log-sum does not execute"}
+    if pmc.get("SQ_INSTS_VALU"):
+        rf["valu_issue_frac"] = pmc["SQ_INSTS_VALU"] / (VALU_SLOTS_PER_S * fused_avg_s)
+        rf["valu_insts_per_launch"] = pmc["SQ_INSTS_VALU"]
+    return rf
 
 
 # ----------------------------------------------------------- secondary rows
@@ -295,7 +355,7 @@ def bench_ekfslam(n_lm=10000, k=20, steps=6, device=0):
     return {"workload": "EKF-SLAM C4: 10,000 landmarks (n = 30,003, P = 7.2 GB), 20 observed "
                         "per step", "value": 1.0 / float(np.mean(times)), "unit": "updates/s",
             "ms_per_update": float(np.mean(times)) * 1e3, "last_update_breakdown_ms": tm,
-            "roofline": {"bound": "hbm", "kernel": "eks_rank_update_pipelined_kernel (fp64 MFMA)",
+            "roofline": {"bound": "hbm", "kernel": "eks_rank_update_frag_kernel (fp64 MFMA)",
                          "achieved": byt / rk / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": byt / rk / 1e9 / HBM_PEAK_GBS,
                          "tflops": flops / rk / 1e12, "avg_launch_ms": rk * 1e3}}
@@ -412,6 +472,37 @@ def secondary(device=0, cpu=True):
     return out
 
 
+class ShardedFailure(RuntimeError):
+    """The sharded mode failed on some rank (every rank raises it together)."""
+
+
+class Agreement:
+    """Fixed agreement points for a multi-rank phase sequence: every rank runs
+    the same collectives in the same order whether or not its own work failed
+    (a failed rank skips the work, not the collectives), and at each
+    checkpoint all ranks learn -- through one MIN all-reduce of an ok flag --
+    whether any rank failed, and then raise ShardedFailure together.
+
+    agree(ok: bool) -> bool is the all-reduce (True when every rank is ok)."""
+
+    def __init__(self, agree, rank=0):
+        self.agree, self.rank, self.err = agree, rank, None
+
+    def attempt(self, fn, *a, **kw):
+        if self.err is not None:
+            return None
+        try:
+            return fn(*a, **kw)
+        except Exception as e:                      # noqa: BLE001 - agreed on below
+            self.err = e
+            return None
+
+    def checkpoint(self, phase):
+        if not self.agree(self.err is None):
+            mine = None if self.err is None else f"rank {self.rank}: {type(self.err).__name__}: {self.err}"
+            raise ShardedFailure(phase, mine)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -421,6 +512,8 @@ def main():
     ap.add_argument("--mode", default=None, choices=["replicas", "sharded"],
                     help="sharded (default for N > 1): one filter over N x 2^20 particles "
                          "(BASELINE configs[2]); replicas (default for N = 1): independent filters")
+    ap.add_argument("--total-particles", type=int, default=None,
+                    help="strong scaling: one filter of this many particles over the N ranks")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-secondary", action="store_true",
                     help="skip the EKF / EKF-SLAM / graph-SLAM rows (rank 0, N = 1 only)")
@@ -431,6 +524,11 @@ def main():
         args.mode = "sharded" if world > 1 else "replicas"
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    strong = args.total_particles is not None
+    n_total = args.total_particles if strong else world * NP_PER_GPU
+    if strong and (n_total % world or (n_total // world) % 8192):
+        raise SystemExit("--total-particles: need T / N to be a whole number of 8192-particle buffers")
+    n_per_rank = n_total // world
     # SLAM_BENCH_SHARE_GPU=1 (tests on a one-GPU box): every rank on device 0,
     # gloo for the harness, the exchange regions bootstrapped through gloo
     # (RCCL refuses two ranks on one GPU)
@@ -443,6 +541,16 @@ def main():
         import torch.distributed as dist
         torch.cuda.set_device(local_rank)
         dist.init_process_group("nccl" if torch.cuda.is_available() and not share_gpu else "gloo")
+    multi = dist is not None and world > 1
+    tdev = "cpu" if share_gpu else f"cuda:{local_rank}"
+
+    def agree(ok):
+        if not multi:
+            return ok
+        import torch
+        t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=tdev)
+        dist.all_reduce(t, op=dist.ReduceOp.MIN)
+        return int(t.item()) == 1
 
     from slamhip.pf import DeviceParticleFilter
     total_steps = args.warmup + 2 * args.steps
@@ -455,34 +563,10 @@ def main():
             dist.barrier()
             torch.cuda.synchronize()
 
-    def measure_sharded(likelihood):
-        # one filter over world x 2^20 particles (BASELINE configs[2]): this
-        # rank's shard through slamhip.dist.DistFilter -- the device-resident
-        # step (peer-memory exchanges over xGMI inside the step's kernels, no
-        # host decision, 8 steps per hipGraph); the exchange regions are
-        # bootstrapped over an RCCL communicator created by the library (the
-        # 128-byte RCCL id travels through torch.distributed once).  At
-        # world = 1 the single shard runs the same kernels in-process.
-        from slamhip.dist import Comm, DistFilter
-        if os.environ.get("SLAM_BENCH_FAIL_SHARDED") == "1":         # tests of the fallback
-            raise RuntimeError("injected sharded-mode failure (SLAM_BENCH_FAIL_SHARDED)")
-        n_global = world * NP_PER_GPU
-        comm = None
-        kw = dict(dt=dt, motion="velocity", likelihood=likelihood, seed=1234, device=local_rank)
-        if dist is not None and world > 1 and share_gpu:
-            def all_gather(b):
-                out = [None] * world
-                dist.all_gather_object(out, b)
-                return out
-            filt = DistFilter(n_global, lm, world=world, rank=rank, all_gather=all_gather, **kw)
-        elif dist is not None and world > 1:
-            obj = [Comm.unique_id() if rank == 0 else None]
-            dist.broadcast_object_list(obj, src=0)
-            comm = Comm(obj[0], world, rank, local_rank)
-            filt = DistFilter(n_global, lm, world=world, rank=rank, comm=comm, **kw)
-        else:
-            filt = DistFilter(n_global, lm, world=1, **kw)
-        filt.load_observations(zs)
+    def timed_runs(filt):
+        # W untimed warm-up steps (they also capture the step graphs), K timed
+        # steps between barrier + synchronize, then a kernel-timing pass over K
+        # more steps (HIP events on the filter's stream around every launch)
         if args.warmup:
             filt.run(0, ctl[:args.warmup], want_results=False)
         barrier_sync()
@@ -494,33 +578,66 @@ def main():
         filt.run(args.warmup + args.steps, ctl[args.warmup + args.steps:])
         timing = {k: filt.timing(k) for k in range(4)}
         filt.enable_timing(False)
-        filt.close()
-        if comm is not None:
-            comm.close()
         return elapsed, out, timing
 
-    def measure(likelihood):
+    def measure_sharded(likelihood, n_global):
+        # one filter over n_global particles (BASELINE configs[2]): this rank's
+        # shard through slamhip.dist.DistFilter -- the device-resident step
+        # (peer-memory exchanges over xGMI inside the step's kernels, no host
+        # decision, 8 steps per hipGraph); the exchange regions are bootstrapped
+        # over an RCCL communicator created by the library (the 128-byte RCCL id
+        # travels through torch.distributed once).  At world = 1 the single
+        # shard runs the same kernels in-process.
+        from slamhip.dist import Comm, DistFilter
+        if os.environ.get("SLAM_BENCH_FAIL_SHARDED") == "1":         # tests: every rank, before setup
+            raise ShardedFailure("setup", f"rank {rank}: injected sharded-mode failure")
+        fail_rank = os.environ.get("SLAM_BENCH_FAIL_SHARDED_RANK")   # tests: one rank, after setup
+        kw = dict(dt=dt, motion="velocity", likelihood=likelihood, seed=1234, device=local_rank)
+        ag = Agreement(agree, rank)
+        comm = filt = None
+        try:
+            if not multi:
+                filt = DistFilter(n_global, lm, world=1, **kw)
+            else:
+                if not share_gpu:
+                    obj = [ag.attempt(Comm.unique_id) if rank == 0 else None]
+                    dist.broadcast_object_list(obj, src=0)
+                    ag.checkpoint("rccl id")
+                    comm = Comm(obj[0], world, rank, local_rank)       # collective (RCCL init)
+                filt = ag.attempt(DistFilter, n_global, lm, world=world, rank=rank, connect=False, **kw)
+                ag.checkpoint("shard create")
+                blob = ag.attempt(filt.export_handle)
+                if share_gpu:
+                    blobs = [None] * world
+                    dist.all_gather_object(blobs, blob)
+                else:
+                    blobs = comm.all_gather_bytes(blob if blob is not None else bytes(len_blob(filt)))
+                ag.checkpoint("handle exchange")
+                ag.attempt(filt.connect, blobs)
+                if fail_rank is not None and int(fail_rank) == rank:
+                    ag.attempt(_raise, RuntimeError(f"injected failure on rank {rank} after connect"))
+                ag.checkpoint("connect")
+            ag.attempt(filt.load_observations, zs)
+            ag.checkpoint("load")
+            res = ag.attempt(timed_runs, filt)
+            ag.checkpoint("run")
+            return res
+        finally:
+            if filt is not None:
+                filt.close()
+            if comm is not None:
+                comm.close()
+
+    def measure(likelihood, n_part=None):
         if args.mode == "sharded":
-            return measure_sharded(likelihood)
-        pf = DeviceParticleFilter(NP_PER_GPU, lm, dt=dt, motion="velocity",
+            return measure_sharded(likelihood, n_total)
+        pf = DeviceParticleFilter(n_part or n_per_rank, lm, dt=dt, motion="velocity",
                                   likelihood=likelihood, seed=1234 + rank, device=local_rank)
-        pf.load_observations(zs)
-        if args.warmup:
-            pf.run(0, ctl[:args.warmup], want_results=False)       # also captures the step graphs
-        # timed region: K steps, one hipGraph replay per step, no host sync inside
-        barrier_sync()
-        t0 = time.perf_counter()
-        out = pf.run(args.warmup, ctl[args.warmup:args.warmup + args.steps])
-        barrier_sync()
-        elapsed = time.perf_counter() - t0
-        # kernel-timing pass over the next K steps: HIP events on the filter's
-        # stream around every launch (direct launches, same kernels)
-        pf.enable_timing(True)
-        pf.run(args.warmup + args.steps, ctl[args.warmup + args.steps:])
-        timing = {k: pf.timing(k) for k in range(4)}
-        pf.enable_timing(False)
-        pf.close()
-        return elapsed, out, timing
+        try:
+            pf.load_observations(zs)
+            return timed_runs(pf)
+        finally:
+            pf.close()
 
     def measure_numpy_stream(likelihood):
         # parity mode on the device: NumPy's RandomState stream drawn there
@@ -528,42 +645,34 @@ def main():
         # reference's draws) and the observations simulated from the true pose
         pf = DeviceParticleFilter(NP_PER_GPU, lm, dt=dt, motion="velocity",
                                   likelihood=likelihood, seed=1234, device=local_rank)
-        pf.use_numpy_stream(np.random.RandomState(1234))
-        pf.load_truth(simulate_world.poses)
-        if args.warmup:
-            pf.run(0, ctl[:args.warmup], want_results=False)
-        barrier_sync()
-        t0 = time.perf_counter()
-        pf.run(args.warmup, ctl[args.warmup:args.warmup + args.steps])
-        barrier_sync()
-        el = time.perf_counter() - t0
-        pf.close()
-        return el
+        try:
+            pf.use_numpy_stream(np.random.RandomState(1234))
+            pf.load_truth(simulate_world.poses)
+            if args.warmup:
+                pf.run(0, ctl[:args.warmup], want_results=False)
+            barrier_sync()
+            t0 = time.perf_counter()
+            pf.run(args.warmup, ctl[args.warmup:args.warmup + args.steps])
+            barrier_sync()
+            return time.perf_counter() - t0
+        finally:
+            pf.close()
 
     sharded_error = None
-    if args.mode == "sharded" and dist is not None and world > 1:
+    if args.mode == "sharded" and multi:
         # the sharded exchange needs every rank's GPU reachable over xGMI; if
-        # any rank fails (every wait in the library is bounded, so a failure
-        # raises rather than hangs), all ranks agree through the harness's
-        # process group and fall back to independent replicas, and the JSON
-        # line says so (config.parallelism, sharded_error)
-        import torch
+        # any rank fails, every rank leaves measure_sharded at the same
+        # agreement point with ShardedFailure, the ranks share their errors and
+        # measure independent replicas instead, and the line says so
+        # (config.parallelism, sharded_error)
         try:
-            result = measure(args.likelihood)
-            ok = 1
-        except Exception as e:                          # noqa: BLE001 - reported below
-            result, ok = None, 0
-            sharded_error = f"rank {rank}: {type(e).__name__}: {e}"[:400]
-            print(f"bench: sharded mode failed on rank {rank}: {e}", file=sys.stderr)
-        flag = torch.tensor([ok], dtype=torch.int32,
-                            device="cpu" if share_gpu else f"cuda:{local_rank}")
-        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
-        if int(flag.item()) == 1:
-            elapsed, out, timing = result
-        else:
+            elapsed, out, timing = measure(args.likelihood)
+        except ShardedFailure as e:
+            phase, mine = e.args
+            print(f"bench: sharded mode failed at {phase} ({mine or 'another rank'})", file=sys.stderr)
             errs = [None] * world
-            dist.all_gather_object(errs, sharded_error)
-            sharded_error = "; ".join(e for e in errs if e) or "another rank failed"
+            dist.all_gather_object(errs, mine)
+            sharded_error = f"{phase}: " + ("; ".join(x for x in errs if x) or "another rank failed")
             args.mode = "replicas"
             elapsed, out, timing = measure(args.likelihood)
     else:
@@ -575,16 +684,23 @@ def main():
 
     if dist is not None:
         import torch
-        t = torch.tensor([elapsed], dtype=torch.float64,
-                         device="cpu" if share_gpu else f"cuda:{local_rank}")
+        t = torch.tensor([elapsed], dtype=torch.float64, device=tdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    updates = world * NP_PER_GPU * NL * args.steps
+    # particles processed per step by the whole job
+    n_job = n_total if args.mode == "sharded" else world * n_per_rank
+    n_rank = n_total // world if args.mode == "sharded" else n_per_rank
+    updates = n_job * NL * args.steps
     value = updates / elapsed
     fused_avg_s = fused_ms / 1e3 / max(fused_n, 1)
-    achieved_tf = FLOPS_PER_UPDATE[args.likelihood] * NP_PER_GPU * NL / fused_avg_s / 1e12
-    traffic, traffic_src, pmc = load_pmc_traffic()
+    if args.mode == "replicas":
+        workload = (f"PF C2: {n_rank:,} particles/GPU x 100 landmarks, velocity motion model, "
+                    "systematic resample")
+    else:
+        workload = (f"PF C3 form: one filter of {n_job:,} particles sharded {n_rank:,}/GPU x 100 "
+                    "landmarks, velocity motion model, exact systematic resample across shards; "
+                    "global np.sum-order normalisation")
     line = {
         "metric": METRIC,
         "value": value,
@@ -594,63 +710,52 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": elapsed * 1e3 / args.steps,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if strong else "weak",
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic (simulated circular trajectory, 100 landmarks ~ U(-10,10)^2, "
                 "on-device Philox noise)",
-        "config": {"workload": ("PF C2: 1,048,576 particles/GPU x 100 landmarks, velocity "
-                                "motion model, systematic resample") if args.mode == "replicas" else
-                               (f"PF C3 form: one filter of {world} x 1,048,576 particles sharded "
-                                "1M/GPU x 100 landmarks, velocity motion model, exact systematic "
-                                "resample across shards; global np.sum-order normalisation"),
-                   "particles_per_gpu": NP_PER_GPU, "landmarks": NL,
-                   "likelihood": args.likelihood, "parallelism": f"{args.mode}{world}"},
-        "roofline": {"bound": "valu_fp64", "kernel": "pf_fused_kernel (predict+likelihood)",
-                     "achieved": achieved_tf, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
-                     "frac": achieved_tf / FP64_PEAK_TFLOPS, "traffic": traffic,
-                     "traffic_source": traffic_src,
-                     "note": "fp64-VALU bound (not HBM, not MFMA); peak = MI355X fp64 vector "
-                             "78.6 TF; achieved counts the reference algorithm's "
-                             f"{FLOPS_PER_UPDATE[args.likelihood]} flops per particle-landmark update "
-                             "(SURVEY 8(d); fma = 2, exp = div = 1)" +
-                             ("; the kernel evaluates the iso log-sum in closed form (O(NP + NL) per "
-                              "step, DESIGN 4.3): its executed fp64 work is executed_fp64_tflops"
-                              if args.likelihood == "logsum" else ""),
-                     "avg_launch_ms": fused_avg_s * 1e3,
-                     "hbm_gbs_algorithmic": BYTES_PER_PARTICLE * NP_PER_GPU / fused_avg_s / 1e9},
+        "config": {"workload": workload, "particles_per_gpu": n_rank, "particles_total": n_job,
+                   "landmarks": NL, "likelihood": args.likelihood,
+                   "parallelism": f"{args.mode}{world}"},
+        "roofline": fused_roofline(args.likelihood, n_rank, fused_avg_s),
         "breakdown_ms_per_step": {"fused": fused_ms / max(fused_n, 1),
                                   "reduce": red_ms / max(red_n, 1),
                                   "resample": res_ms / max(res_n, 1),
                                   "step_events": step_ms / max(step_n, 1)},
         "resample_steps": int(sum(o["resampled"] for o in out)),
+        "ess_near_steps": int(sum(o.get("ess_near", False) for o in out)),
+        "closed_form_fallback_waves": int(sum(o.get("dd_waves", 0) for o in out)),
     }
-    if pmc.get("fp64_flops") and args.likelihood == "logsum":
-        # executed fp64 flops (PMC SQ_INSTS_VALU_{ADD,MUL,FMA,TRANS}_F64 x 64 lanes, fma = 2)
-        # over this run's live launch time, and the VALU issue utilisation: every wave64
-        # VALU instruction occupies a 16-lane SIMD for 4 cycles (256 CUs x 4 SIMDs, 2.4 GHz)
-        rf = line["roofline"]
-        rf["executed_fp64_tflops"] = pmc["fp64_flops"] / fused_avg_s / 1e12
-        if pmc.get("SQ_INSTS_VALU"):
-            rf["valu_issue_frac"] = pmc["SQ_INSTS_VALU"] * 4 / (1024 * 2.4e9 * fused_avg_s)
-    if world == 1 and args.likelihood != "product":
+    if world == 1 and args.likelihood != "product" and not strong:
         e2, _, t2 = measure("product")
-        line["alt_modes"] = {"product": {"value": NP_PER_GPU * NL * args.steps / e2,
-                                         "fused_avg_ms": t2[0][0] / max(t2[0][1], 1)}}
+        f2 = t2[0][0] / 1e3 / max(t2[0][1], 1)
+        line["alt_modes"] = {"product": {"value": n_rank * NL * args.steps / e2,
+                                         "ms_per_step": e2 * 1e3 / args.steps,
+                                         "fused_avg_ms": f2 * 1e3,
+                                         "roofline": fused_roofline("product", n_rank, f2)}}
         e4 = measure_numpy_stream(args.likelihood)
         line["alt_modes"]["numpy_stream"] = {
             "value": NP_PER_GPU * NL * args.steps / e4, "ms_per_step": e4 * 1e3 / args.steps,
             "note": "the reference's own noise stream (MT19937 + polar normals, bit-identical to "
                     "np.random) drawn on the device with the observations simulated there"}
-    if world == 1 and args.mode == "replicas":
+    if world == 1 and args.mode == "replicas" and not strong:
         # the sharded step's kernels on one shard (its overhead over the single handle)
-        e3, _, t3 = measure_sharded(args.likelihood)
+        e3, _, t3 = measure_sharded(args.likelihood, NP_PER_GPU)
         line["sharded1"] = {"ms_per_step": e3 * 1e3 / args.steps,
                             "over_single": e3 / elapsed,
                             "fused_avg_ms": t3[0][0] / max(t3[0][1], 1)}
-    if rank == 0 and world == 1 and not args.no_secondary:
+        # strong-scaling reference: one handle of 2^23 particles (BASELINE configs[2]'s
+        # total) -- the single-GPU line that `--total-particles 8388608 --gpus N` divides
+        e5, o5, t5 = measure(args.likelihood, STRONG_TOTAL)
+        line["strong_single"] = {"particles": STRONG_TOTAL,
+                                 "value": STRONG_TOTAL * NL * args.steps / e5,
+                                 "ms_per_step": e5 * 1e3 / args.steps,
+                                 "fused_avg_ms": t5[0][0] / max(t5[0][1], 1),
+                                 "resample_steps": int(sum(o["resampled"] for o in o5))}
+    if rank == 0 and world == 1 and not args.no_secondary and not strong:
         line["secondary"] = secondary(local_rank, cpu=not args.no_cpu_baseline)
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not strong:
         line["cpu_baseline"] = cpu_baseline()
         line["cpu_baseline"]["gpu_over_cpu"] = value / line["cpu_baseline"]["value"]
         try:
@@ -665,6 +770,17 @@ def main():
         print(json.dumps(line), flush=True)
     if dist is not None:
         dist.destroy_process_group()
+
+
+def _raise(e):
+    raise e
+
+
+def len_blob(filt):
+    import ctypes as C
+    size = C.c_int64(0)
+    filt._lib.slam_dist_handle_size(C.byref(size))
+    return size.value
 
 
 if __name__ == "__main__":

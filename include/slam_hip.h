@@ -75,6 +75,10 @@ typedef struct {
     int32_t resample_next;/* ess < ESS_TH: the next step will resample */
     int32_t status;       /* bit0: resample clamp (reference IndexError); bit1: exact-scan fallback */
     int32_t n_special;    /* exact-cumsum diagnostics: sequentially folded elements */
+    int32_t ess_near;     /* |ess - ESS_TH| <= band * ESS_TH: the reference's `1 / (pw @ pw.T)`
+                             (particle_filter.py:210, BLAS order) could decide resample_next
+                             differently; the drop-in confirms such steps on the host */
+    int32_t dd_waves;     /* closed-form log-sum: wavefronts that took the double-double form */
 } slam_pf_result;
 
 /* ParticleFilter.__init__ (particle_filter.py:21-84).  landmarks: n_landmarks x 2 row-major. */
@@ -130,6 +134,10 @@ int slam_pf_set_scan_merged(slam_pf* h, int32_t on);
  * on the host's BLAS, when the device's ESS lies within rounding of the
  * threshold (the device sums in its own fixed order).  Single-GPU handles. */
 int slam_pf_set_resample_next(slam_pf* h, int32_t on);
+/* Band of slam_pf_result.ess_near, relative to ESS_TH (default 1e-9): the steps
+ * whose device ESS lies this close to the threshold, where the reference's BLAS
+ * dot (particle_filter.py:210) could order the sum differently. */
+int slam_pf_set_ess_band(slam_pf* h, double band);
 /* external != 0: run on the caller's HIP stream (e.g. torch.cuda.current_stream();
  * NULL = the default stream).  external == 0: a private stream again. */
 int slam_pf_set_stream(slam_pf* h, void* hip_stream, int32_t external);
@@ -160,39 +168,6 @@ int slam_comm_info(slam_comm* comm, int32_t* world, int32_t* rank);
 int slam_comm_all_gather_host(slam_comm* comm, const void* send, void* recv, int64_t bytes);
 
 /* ====================================================================
- * Sharded particle filter (BASELINE config 3): one handle per GPU holds
- * particles [gbase, gbase + n_local) of a filter of n_global particles.
- * The caller runs the phases in order and exchanges the small device
- * buffers between ranks (slamhip/shard.py: torch.distributed / RCCL):
- *   begin -> [scan_local -> A -> classify -> B(meta) -> export_specials ->
- *   B(lists) -> fold -> plan -> export_items -> C -> import_items] ->
- *   predict_update -> D -> normalize -> E -> finish
- * Every rank ends with the same result, bit-identical to one GPU holding
- * all n_global particles.  d_* arguments are device pointers.
- * ==================================================================== */
-int slam_pf_create_shard(const slam_pf_config* cfg, int64_t n_local, int64_t n_global,
-                         int64_t gbase, int32_t n_landmarks, const double* landmarks, int device,
-                         slam_pf** out);
-/* out[4] = {np.sum buffers held locally, record bytes, special bytes, item bytes} */
-int slam_pf_shard_sizes(slam_pf* h, int64_t* out);
-int slam_pf_shard_begin(slam_pf* h, const double* control, const double* z, const double* noise,
-                        double u_resample, int32_t resample);
-int slam_pf_shard_scan_local(slam_pf* h, double* d_total);
-int slam_pf_shard_classify(slam_pf* h, const double* d_totals, int32_t rank, int32_t world,
-                           int64_t* d_meta);
-int slam_pf_shard_export_specials(slam_pf* h, int64_t count, void* d_dst);
-int slam_pf_shard_fold(slam_pf* h, const void* d_lists, int64_t cap, const int64_t* meta,
-                       int32_t world, int32_t rank);
-int slam_pf_shard_plan(slam_pf* h, const int64_t* gb, int32_t world, int64_t* send_counts);
-int slam_pf_shard_export_items(slam_pf* h, void* d_send);
-int slam_pf_shard_import_items(slam_pf* h, const void* d_recv, int64_t n_items);
-int slam_pf_shard_predict_update(slam_pf* h, double* d_partials);
-int slam_pf_shard_normalize(slam_pf* h, const double* d_all_partials, int64_t nparts,
-                            void* d_record);
-int slam_pf_shard_finish(slam_pf* h, const void* d_all_records, int32_t world,
-                         slam_pf_result* res);
-
-/* ====================================================================
  * Sharded particle filter, device-resident step (BASELINE config 3).
  * One filter of n_global particles split into contiguous shards; a
  * slam_dist groups the shards this process holds -- all of them (LOCAL:
@@ -217,9 +192,12 @@ int slam_pf_create_dist_shard(const slam_pf_config* cfg, int64_t n_local, int64_
  * n_held == 1: rank rank0, connect before stepping).  The shards must outlive it. */
 int slam_dist_create(slam_pf** shards, int32_t n_held, int32_t world, int32_t rank0, slam_dist** out);
 int slam_dist_destroy(slam_dist* d);
+/* bootstrap blob per rank: the exchange region's IPC handle and the GPU's PCI bus id */
 int slam_dist_handle_size(int64_t* bytes);
 int slam_dist_export(slam_dist* d, void* blob);                 /* n_held x handle size */
-int slam_dist_connect(slam_dist* d, const void* all_blobs);     /* world x handle size, rank order */
+/* world x handle size, rank order.  Preflight: every peer GPU must be visible and
+ * reachable (hipDeviceCanAccessPeer), else SLAM_ERR_COMM before any IPC mapping. */
+int slam_dist_connect(slam_dist* d, const void* all_blobs);
 int slam_dist_connect_comm(slam_dist* d, slam_comm* comm);      /* export + RCCL all-gather + connect */
 /* one step from host inputs (observations staged in slot 0, device RNG) */
 int slam_dist_step(slam_dist* d, const double* control, const double* z, slam_pf_result* res);
@@ -246,6 +224,13 @@ typedef struct {
     double r[4];          /* :68-70  R (observation noise, 2x2) */
     double x0[3];         /* :74-79  initial estimate */
     double p0[9];         /* :81-84  initial covariance */
+    int32_t motion;       /* SLAM_MOTION_LINEAR: the reference's __f / jacobF / Q (:160-194);
+                             SLAM_MOTION_VELOCITY: prediction driven by motion_model.py --
+                             f = moveWithoutNoise (:64-86), its Jacobian G, and
+                             Q = V M V^T from a1..a6 (M = diag(sv^4, sw^4): the std handed
+                             to np.random.normal is sigma**2, :43-48) + the gamma yaw term */
+    int32_t pad0;
+    double alphas[6];     /* motion_model.py:20-29 a1..a6 (VELOCITY) */
 } slam_ekf_config;
 
 /* ExtendedKalmanFilter.__init__: every filter starts at (x0, p0). */
@@ -291,6 +276,10 @@ typedef struct {
     double r_dist;        /* ScanSensor range noise fraction  (graph_based_slam.py:187-192) */
     double r_dir;         /* bearing noise (rad) */
     double r_orient;      /* orientation noise (rad) */
+    int32_t motion;       /* robot motion: SLAM_MOTION_LINEAR (+ q_robot) or SLAM_MOTION_VELOCITY
+                             (motion_model.py, as slam_ekf_config.motion; q_robot unused) */
+    int32_t pad0;
+    double alphas[6];     /* motion_model.py a1..a6 (VELOCITY) */
 } slam_ekfslam_config;
 
 int slam_ekfslam_create(const slam_ekfslam_config* cfg, int64_t n_landmarks, int device,

@@ -16,7 +16,7 @@ from __future__ import annotations
 
 import numpy as np
 
-from pf_oracle import HALF_PI, to_world_frame, wrap_angle
+from pf_oracle import HALF_PI, motion_velocity_exact, to_world_frame, wrap_angle
 
 
 class EKFParams:
@@ -45,6 +45,87 @@ def ekf_jacobian(x, dt, vel):
     return np.array([[1.0, 0.0, -dt * vel * np.sin(x[2])],
                      [0.0, 1.0, dt * vel * np.cos(x[2])],
                      [0.0, 0.0, 1.0]])
+
+
+# ----------------------------------------------- velocity motion model (N1)
+def velocity_motion(x, v, om, dt):
+    """f = MotionModel.moveWithoutNoise (motion_model.py:64-86) for one (3,)
+    state -- pf_oracle.motion_velocity_exact, pinned to tests/golden/motion.npz."""
+    return np.array(motion_velocity_exact(x, v, om, dt))
+
+
+def velocity_jacobians(x, v, om, dt):
+    """Jacobians of moveWithoutNoise (Thrun, Probabilistic Robotics, eq. 7.8 /
+    7.11) at the previous estimate: G = d f / d(x, y, yaw) (only column 2 is
+    not the identity's) and V = d f / d(v, omega).  t1 = the wrapped heading
+    motion_model.py:79-80 forms (sin / cos are 2 pi periodic, so the wrap
+    does not change them)."""
+    a = v / om
+    b = wrap_angle(om * dt)
+    t0 = x[2]
+    t1 = wrap_angle(t0 + b)
+    s0, c0, s1, c1 = np.sin(t0), np.cos(t0), np.sin(t1), np.cos(t1)
+    g02 = a * (-c0 + c1)
+    g12 = a * (-s0 + s1)
+    v00 = (-s0 + s1) / om
+    v10 = (c0 - c1) / om
+    v01 = (v * (s0 - s1)) / (om * om) + ((v * c1) * dt) / om
+    v11 = (-(v * (c0 - c1))) / (om * om) + ((v * s1) * dt) / om
+    G = np.array([[1.0, 0.0, g02], [0.0, 1.0, g12], [0.0, 0.0, 1.0]])
+    V = np.array([[v00, v01], [v10, v11], [0.0, dt]])
+    return G, V
+
+
+def velocity_process_noise(v, om, dt, alphas):
+    """The state-space process noise of moveWithNoise (motion_model.py:31-62):
+    V M V^T with M = diag(sv^4, sw^4) -- the reference hands sigma**2 to
+    np.random.normal as the STANDARD DEVIATION (:46-47), so the variances are
+    sigma^4 -- plus the heading noise of gamma-hat, std sg^2, entering as
+    gamma dt (:48, :56): variance (sg^2 dt)^2 on the yaw."""
+    a1, a2, a3, a4, a5, a6 = alphas
+    v2, w2 = v ** 2, om ** 2
+    sv = (a1 * v2) + (a2 * w2)
+    sw = (a3 * v2) + (a4 * w2)
+    sg = (a5 * v2) + (a6 * w2)
+    mv, mw = (sv ** 2) ** 2, (sw ** 2) ** 2
+    mg = ((sg ** 2) * dt) ** 2
+    return mv, mw, mg
+
+
+def velocity_predict(x, P, v, om, dt, alphas):
+    """EKF prediction driven by motion_model.py: x_m = f(x), P_m = G P G^T +
+    V M V^T (+ the gamma term).  Operation order of ekf_kernels.inl."""
+    xm = velocity_motion(x, v, om, dt)
+    G, V = velocity_jacobians(x, v, om, dt)
+    mv, mw, mg = velocity_process_noise(v, om, dt, alphas)
+    Qv = np.array([[V[0, 0] * V[0, 0] * mv + V[0, 1] * V[0, 1] * mw,
+                    V[0, 0] * V[1, 0] * mv + V[0, 1] * V[1, 1] * mw, V[0, 1] * dt * mw],
+                   [0.0, V[1, 0] * V[1, 0] * mv + V[1, 1] * V[1, 1] * mw, V[1, 1] * dt * mw],
+                   [0.0, 0.0, dt * dt * mw + mg]])
+    Qv[1, 0], Qv[2, 0], Qv[2, 1] = Qv[0, 1], Qv[0, 2], Qv[1, 2]
+    Pm = (G @ P @ G.T) + Qv
+    return xm, Pm, G, Qv
+
+
+def ekf_velocity_update(x_hat, P, z, p: EKFParams, control, alphas):
+    """N1: the reference's EKF step (extended_kalman_filter.py:108-128) with
+    the prediction taken from motion_model.py (velocity_predict) instead of
+    the linear __f / jacobF / Q; the update (position fix C, inv(S), (I - G C)
+    P_m) is the reference's.  Returns (x_hat_m, x_hat, P).  No reference run
+    combines the two: parity unpinned except f (motion.npz)."""
+    v, om = control
+    xm, Pm, _, _ = velocity_predict(x_hat, P, v, om, p.dt, alphas)
+    return _ekf_correct(xm.reshape(3, 1), Pm, z, p)
+
+
+def _ekf_correct(xm, Pm, z, p):
+    e = z.reshape(2, 1) - (p.c @ xm)
+    S = (p.c @ Pm @ p.c.T) + p.r
+    G = (Pm @ p.c.T) @ np.linalg.inv(S)
+    xh = xm + (G @ e)
+    xh[2, 0] = wrap_angle(xh[2, 0])
+    Pn = (np.identity(3) - G @ p.c) @ Pm
+    return xm[:, 0], xh[:, 0], Pn
 
 
 def ekf_update(x_hat, P, z, p: EKFParams, control=None):
@@ -127,23 +208,37 @@ def scan_jacobian(xr, lm):
     return Hr, Hl
 
 
-def ekfslam_step(mu, P, control, obs_ids, obs, dt, q_robot, noise):
+def ekfslam_predict(mu, P, control, dt, q_robot, alphas=None):
+    """EKF-SLAM prediction on the robot rows / columns: the reference EKF's
+    linear model (:160-194, + q_robot), or with ``alphas`` the velocity model
+    of motion_model.py (moveWithoutNoise, G, V M V^T: velocity_predict)."""
+    v, om = control
+    mu = mu.copy()
+    xr = mu[:3].copy()
+    P = P.copy()
+    if alphas is None:
+        F = ekf_jacobian(xr, dt, v)
+        mu[:3] = ekf_motion(xr, dt, v, om)
+        Q = q_robot
+    else:
+        _, _, F, Q = velocity_predict(xr, P[:3, :3], v, om, dt, alphas)
+        mu[:3] = velocity_motion(xr, v, om, dt)
+    P[:3, :] = F @ P[:3, :]
+    P[:, :3] = P[:, :3] @ F.T
+    P[:3, :3] += Q
+    return mu, P
+
+
+def ekfslam_step(mu, P, control, obs_ids, obs, dt, q_robot, noise, alphas=None):
     """One EKF-SLAM predict + batched update.
 
     mu (n,), P (n,n) with n = 3 + 3*NLM; robot motion = the reference EKF's
-    linear model (:160-194); ``obs`` (k,3) range/bearing/orientation of the
-    landmarks ``obs_ids``; ``noise`` = (r_dist, r_dir, r_orient).  The
+    linear model (:160-194), or motion_model.py's velocity model with
+    ``alphas`` (ekfslam_predict); ``obs`` (k,3) range/bearing/orientation of
+    the landmarks ``obs_ids``; ``noise`` = (r_dist, r_dir, r_orient).  The
     update is P <- P - K S K^T with K = P H^T S^-1 (rank-3k)."""
-    v, om = control
     n = mu.size
-    mu = mu.copy()
-    xr = mu[:3].copy()
-    F = ekf_jacobian(xr, dt, v)
-    mu[:3] = ekf_motion(xr, dt, v, om)
-    P = P.copy()
-    P[:3, :] = F @ P[:3, :]
-    P[:, :3] = P[:, :3] @ F.T
-    P[:3, :3] += q_robot
+    mu, P = ekfslam_predict(mu, P, control, dt, q_robot, alphas)
     k = len(obs_ids)
     H = np.zeros((3 * k, n))
     innov = np.zeros(3 * k)

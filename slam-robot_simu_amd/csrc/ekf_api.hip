@@ -63,6 +63,8 @@ EKFConst ekf_const(const slam_ekf_config& c) {
     k.omega = c.omega;
     for (int i = 0; i < 9; ++i) k.q[i] = c.q[i];
     for (int i = 0; i < 4; ++i) k.r[i] = c.r[i];
+    k.motion = c.motion;
+    for (int i = 0; i < 6; ++i) k.alphas[i] = c.alphas[i];
     return k;
 }
 
@@ -117,6 +119,8 @@ EksConst eks_const(const slam_ekfslam_config& c) {
     k.r_dist = c.r_dist;
     k.r_dir = c.r_dir;
     k.r_orient = c.r_orient;
+    k.motion = c.motion;
+    for (int i = 0; i < 6; ++i) k.alphas[i] = c.alphas[i];
     return k;
 }
 
@@ -125,7 +129,7 @@ int eks_predict(slam_ekfslam* h, const double* control) {
     const int64_t rows = h->n - 3;
     if (rows > 0)
         hipLaunchKernelGGL(eks_predict_rows_kernel, dim3((unsigned)((rows + 255) / 256)), dim3(256),
-                           0, h->stream, h->P, h->n, h->ld, h->mu, h->cfg.dt, v);
+                           0, h->stream, h->P, h->n, h->ld, h->mu, eks_const(h->cfg), v, om);
     hipLaunchKernelGGL(eks_predict_pose_kernel, dim3(1), dim3(64), 0, h->stream, h->P, h->ld,
                        h->mu, eks_const(h->cfg), v, om);
     SLAM_HIP_TRY(hipGetLastError());
@@ -225,6 +229,8 @@ extern "C" {
 // ------------------------------------------------------------------ EKF
 int slam_ekf_create(const slam_ekf_config* cfg, int64_t batch, int device, slam_ekf** out) {
     SLAM_ARG_CHECK(cfg && out && batch >= 1, "slam_ekf_create: bad arguments");
+    SLAM_ARG_CHECK(cfg->motion == SLAM_MOTION_LINEAR || cfg->motion == SLAM_MOTION_VELOCITY,
+                   "slam_ekf_create: bad motion model");
     *out = nullptr;
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev)
@@ -370,6 +376,8 @@ int slam_ekf_synchronize(slam_ekf* h) {
 int slam_ekfslam_create(const slam_ekfslam_config* cfg, int64_t n_landmarks, int device,
                         slam_ekfslam** out) {
     SLAM_ARG_CHECK(cfg && out && n_landmarks >= 1, "slam_ekfslam_create: bad arguments");
+    SLAM_ARG_CHECK(cfg->motion == SLAM_MOTION_LINEAR || cfg->motion == SLAM_MOTION_VELOCITY,
+                   "slam_ekfslam_create: bad motion model");
     *out = nullptr;
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev)

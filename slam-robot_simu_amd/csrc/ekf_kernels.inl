@@ -22,25 +22,94 @@ struct EKFConst {
     double dt, vel, omega;
     double q[9];
     double r[4];
+    int32_t motion;          // SLAM_MOTION_LINEAR (the reference's __f) or _VELOCITY (motion_model.py)
+    double alphas[6];        // motion_model.py:20-29 a1..a6 (velocity model)
 };
+
+// The prediction of an EKF driven by motion_model.py (north_star; oracle
+// ekf_oracle.velocity_predict, same operation order):
+//   f = moveWithoutNoise (motion_model.py:64-86): a = v / w, b = limit(w dt),
+//       t1 = limit(t + b), x' = x + a (-sin t + sin t1), y' = y + a (cos t - cos t1);
+//   G = d f / d(x, y, t): column 2 = (a (-cos t + cos t1), a (-sin t + sin t1), 1);
+//   V = d f / d(v, w) (Thrun eq. 7.11), M = diag(sv^4, sw^4): moveWithNoise
+//       hands sigma**2 to np.random.normal as the standard deviation (:46-47);
+//   the yaw noise of gamma-hat (std sg^2, entering as gamma dt, :48, :56).
+// Q = V M V^T + diag(0, 0, (sg^2 dt)^2) replaces the linear model's Q.
+struct VelPredict {
+    double xm, ym, tm, g02, g12;
+    double q[9];
+};
+
+__device__ __forceinline__ VelPredict velocity_predict(const double x, const double y,
+                                                       const double t, const double v,
+                                                       const double om, const double dt,
+                                                       const double* al) {
+    VelPredict r;
+    const double a = v / om;
+    const double b = wrap_angle(om * dt);
+    const double t1 = wrap_angle(t + b);
+    double s0, c0, s1, c1;
+    sincos(t, &s0, &c0);
+    sincos(t1, &s1, &c1);
+    r.xm = x + a * (-s0 + s1);
+    r.ym = y + a * (c0 - c1);
+    r.tm = t1;
+    r.g02 = a * (-c0 + c1);
+    r.g12 = a * (-s0 + s1);
+    const double v00 = (-s0 + s1) / om, v10 = (c0 - c1) / om;
+    const double v01 = (v * (s0 - s1)) / (om * om) + ((v * c1) * dt) / om;
+    const double v11 = (-(v * (c0 - c1))) / (om * om) + ((v * s1) * dt) / om;
+    const double v2 = v * v, w2 = om * om;
+    const double sv = (al[0] * v2) + (al[1] * w2);
+    const double sw = (al[2] * v2) + (al[3] * w2);
+    const double sg = (al[4] * v2) + (al[5] * w2);
+    const double mv = (sv * sv) * (sv * sv), mw = (sw * sw) * (sw * sw);
+    const double gd = (sg * sg) * dt;
+    const double mg = gd * gd;
+    r.q[0] = ((v00 * v00) * mv) + ((v01 * v01) * mw);
+    r.q[1] = ((v00 * v10) * mv) + ((v01 * v11) * mw);
+    r.q[2] = (v01 * dt) * mw;
+    r.q[4] = ((v10 * v10) * mv) + ((v11 * v11) * mw);
+    r.q[5] = (v11 * dt) * mw;
+    r.q[8] = ((dt * dt) * mw) + mg;
+    r.q[3] = r.q[1];
+    r.q[6] = r.q[2];
+    r.q[7] = r.q[5];
+    return r;
+}
 
 // One step of extended_kalman_filter.py:108-128 on a register-resident filter.
 // Products with the structural 0/1 entries of A, B, C, jacobF are exact in the
 // reference's BLAS calls; the remaining two-term sums follow OpenBLAS dgemm's
-// accumulation (fma into a running sum, k ascending).
+// accumulation (fma into a running sum, k ascending).  With c.motion =
+// VELOCITY the prediction is velocity_predict's (G in place of jacobF, its Q).
 __device__ __forceinline__ void ekf_filter_step(double& x, double& y, double& t, double* P,
                                                 const double zx, const double zy, const double v,
                                                 const double om, const EKFConst& c, double* xm_out) {
-    double sy, cy;
-    sincos(t, &sy, &cy);
-    // __f (:160-178): a = DT cos(yaw), b = DT sin(yaw); x' = A x + B u
-    const double a = c.dt * cy, b = c.dt * sy;
-    const double xm = x + v * a;
-    const double ym = y + v * b;
-    const double tm = wrap_angle(t + om * c.dt);
-    // jacobF (:180-194) at the previous estimate
-    const double f02 = (-c.dt) * v * sy;
-    const double f12 = c.dt * v * cy;
+    double xm, ym, tm, f02, f12, q[9];
+    if (c.motion == SLAM_MOTION_VELOCITY) {
+        const VelPredict vp = velocity_predict(x, y, t, v, om, c.dt, c.alphas);
+        xm = vp.xm;
+        ym = vp.ym;
+        tm = vp.tm;
+        f02 = vp.g02;
+        f12 = vp.g12;
+#pragma unroll
+        for (int k = 0; k < 9; ++k) q[k] = vp.q[k];
+    } else {
+        double sy, cy;
+        sincos(t, &sy, &cy);
+        // __f (:160-178): a = DT cos(yaw), b = DT sin(yaw); x' = A x + B u
+        const double a = c.dt * cy, b = c.dt * sy;
+        xm = x + v * a;
+        ym = y + v * b;
+        tm = wrap_angle(t + om * c.dt);
+        // jacobF (:180-194) at the previous estimate
+        f02 = (-c.dt) * v * sy;
+        f12 = c.dt * v * cy;
+#pragma unroll
+        for (int k = 0; k < 9; ++k) q[k] = c.q[k];
+    }
     // P_m = F P F^T + Q  (:117-118)
     double FP[9];
 #pragma unroll
@@ -52,9 +121,9 @@ __device__ __forceinline__ void ekf_filter_step(double& x, double& y, double& t,
     double Pm[9];
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
-        Pm[3 * i + 0] = fma(FP[3 * i + 2], f02, FP[3 * i + 0]) + c.q[3 * i + 0];
-        Pm[3 * i + 1] = fma(FP[3 * i + 2], f12, FP[3 * i + 1]) + c.q[3 * i + 1];
-        Pm[3 * i + 2] = FP[3 * i + 2] + c.q[3 * i + 2];
+        Pm[3 * i + 0] = fma(FP[3 * i + 2], f02, FP[3 * i + 0]) + q[3 * i + 0];
+        Pm[3 * i + 1] = fma(FP[3 * i + 2], f12, FP[3 * i + 1]) + q[3 * i + 1];
+        Pm[3 * i + 2] = FP[3 * i + 2] + q[3 * i + 2];
     }
     // S = C P_m C^T + R; G = P_m C^T S^-1  (:149-158)
     const double s00 = Pm[0] + c.r[0], s01 = Pm[1] + c.r[1];
@@ -141,6 +210,8 @@ struct EksConst {
     double dt;
     double q[9];
     double r_dist, r_dir, r_orient;
+    int32_t motion;          // SLAM_MOTION_LINEAR / _VELOCITY (velocity_predict)
+    double alphas[6];
 };
 
 // symmetric read from the lower-triangle storage
@@ -153,12 +224,21 @@ __device__ __forceinline__ double psym(const double* P, const int64_t ld, const 
 __global__ __launch_bounds__(256) void eks_predict_rows_kernel(double* __restrict__ P,
                                                                const int64_t n, const int64_t ld,
                                                                const double* __restrict__ mu,
-                                                               const double dt, const double v) {
+                                                               const EksConst c, const double v,
+                                                               const double om) {
     const int64_t i = 3 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    double sy, cy;
-    sincos(mu[2], &sy, &cy);
-    const double f02 = (-dt) * v * sy, f12 = dt * v * cy;
+    double f02, f12;
+    if (c.motion == SLAM_MOTION_VELOCITY) {
+        const VelPredict vp = velocity_predict(mu[0], mu[1], mu[2], v, om, c.dt, c.alphas);
+        f02 = vp.g02;
+        f12 = vp.g12;
+    } else {
+        double sy, cy;
+        sincos(mu[2], &sy, &cy);
+        f02 = (-c.dt) * v * sy;
+        f12 = c.dt * v * cy;
+    }
     double* r = P + i * ld;
     const double p2 = r[2];
     r[0] = fma(p2, f02, r[0]);
@@ -171,9 +251,20 @@ __global__ void eks_predict_pose_kernel(double* __restrict__ P, const int64_t ld
                                         const double om) {
     if (threadIdx.x != 0) return;
     const double x = mu[0], y = mu[1], t = mu[2];
-    double sy, cy;
-    sincos(t, &sy, &cy);
-    const double f02 = (-c.dt) * v * sy, f12 = c.dt * v * cy;
+    const bool vel = c.motion == SLAM_MOTION_VELOCITY;
+    VelPredict vp{};
+    double sy = 0.0, cy = 0.0, f02, f12;
+    const double* q = c.q;
+    if (vel) {
+        vp = velocity_predict(x, y, t, v, om, c.dt, c.alphas);
+        f02 = vp.g02;
+        f12 = vp.g12;
+        q = vp.q;
+    } else {
+        sincos(t, &sy, &cy);
+        f02 = (-c.dt) * v * sy;
+        f12 = c.dt * v * cy;
+    }
     double p[9];
     for (int i = 0; i < 3; ++i)
         for (int j = 0; j < 3; ++j) p[3 * i + j] = psym(P, ld, i, j);
@@ -184,9 +275,15 @@ __global__ void eks_predict_pose_kernel(double* __restrict__ P, const int64_t ld
         FP[6 + j] = p[6 + j];
     }
     for (int i = 0; i < 3; ++i) {
-        P[i * ld + 0] = fma(FP[3 * i + 2], f02, FP[3 * i + 0]) + c.q[3 * i + 0];
-        P[i * ld + 1] = fma(FP[3 * i + 2], f12, FP[3 * i + 1]) + c.q[3 * i + 1];
-        P[i * ld + 2] = FP[3 * i + 2] + c.q[3 * i + 2];
+        P[i * ld + 0] = fma(FP[3 * i + 2], f02, FP[3 * i + 0]) + q[3 * i + 0];
+        P[i * ld + 1] = fma(FP[3 * i + 2], f12, FP[3 * i + 1]) + q[3 * i + 1];
+        P[i * ld + 2] = FP[3 * i + 2] + q[3 * i + 2];
+    }
+    if (vel) {
+        mu[0] = vp.xm;
+        mu[1] = vp.ym;
+        mu[2] = vp.tm;
+        return;
     }
     const double a = c.dt * cy, b = c.dt * sy;
     mu[0] = x + v * a;

@@ -12,7 +12,6 @@
 
 #include "mt_stream.hpp"
 #include "pf_kernels.inl"
-#include "pf_shard.inl"
 #include "pf_dist.inl"
 
 namespace slam {
@@ -89,9 +88,7 @@ struct slam_pf {
     int32_t cap = 0;                // steps the StepIO arrays hold
     double* ctl = nullptr;
     double* z_all = nullptr;
-    double* zc = nullptr;                 // [cap][kClosedWords] closed-form log-sum sums
-    std::vector<double> lm_host;          // landmarks (closed-form sums)
-    std::vector<double> z_host;           // the loaded batch's observations (closed-form sums)
+    double* zc = nullptr;                 // [cap][kZcWords] closed-form words (device-formed per step)
     double* ofs = nullptr;
     slam_pf_result* res_dev = nullptr;
     slam_pf_result* res_host = nullptr;   // pinned
@@ -106,7 +103,7 @@ struct slam_pf {
     hipGraphExec_t graph[2] = {nullptr, nullptr};
     hipGraphExec_t graph_multi[2] = {nullptr, nullptr};
     Timer tm;
-    ShardScratch sh;
+    double ofs_host = 0.0;          // pinned-free staging of one step's resample offset
     // deferred normalisation (single-GPU handles): current weights = w_un / s_cur
     bool deferred = false;
     bool scan_merged = false;   // exact cumsum in one launch (co-resident grid)
@@ -121,6 +118,7 @@ struct slam_pf {
     double* truth = nullptr;             // [cap][4] true pose (x, y, cos, sin) per step
     int32_t truth_steps = 0;
     const double* noise_src = nullptr;   // fused kernel's host-noise input (default h->noise)
+    double ess_band = 1e-9;              // result.ess_near band (relative to ESS_TH)
 };
 
 namespace {
@@ -175,6 +173,13 @@ int make_lik_const(slam_pf* h) {
     lc.neg_ln_den = -std::log(lc.den);
     lc.fast_min_l = climb > 700.0 ? std::numeric_limits<double>::infinity()
                                   : lc.normal_min_l + climb;
+    // closed form: the fp64 expansion while its rounding bound 11 u V stays
+    // within |dL| <= 1e-13 (dL = dF / (2 sx2), 1 % of the 1e-12 parity bar):
+    // V rsx2 <= 160; SLAM_PF_EXPAND_VMAX=<factor> scales the
+    // bound (0: double-double only)
+    const char* ve = std::getenv("SLAM_PF_EXPAND_VMAX");
+    const double vf = ve ? std::atof(ve) : 1.0;
+    lc.expand_vmax = vf * 160.0 * lc.sx2;
     return SLAM_OK;
 }
 
@@ -198,6 +203,9 @@ StepIO step_io(slam_pf* h) {
     io.ofs = h->ofs;
     io.res = h->res_dev;
     io.ctr = h->ctr;
+    io.cap = h->cap;
+    io.motion = h->cfg.motion;
+    io.ess_band = h->ess_band;
     return io;
 }
 
@@ -354,13 +362,7 @@ int launch_fused(slam_pf* h, int motion, bool host_noise) {
                                                    h->w_un, h->c, h->flags, nsrc, h->lm, io,     \
                                                    h->pc, h->lc, h->cfg.seed, h->s_cur, h->refp, \
                                                    h->dp)
-#define SLAM_FUSED(M, L, HN)                 \
-    do {                                     \
-        if (h->deferred)                     \
-            SLAM_FUSED_D(M, L, HN, true);    \
-        else                                 \
-            SLAM_FUSED_D(M, L, HN, false);   \
-    } while (0)
+#define SLAM_FUSED(M, L, HN) SLAM_FUSED_D(M, L, HN, true)     /* every handle is deferred */
     if (motion == kMotionNone) {
         if (lik == SLAM_LIK_PRODUCT) SLAM_FUSED(2, 0, false); else SLAM_FUSED(2, 1, false);
     } else if (motion == SLAM_MOTION_LINEAR) {
@@ -394,7 +396,7 @@ int launch_reduce(slam_pf* h, int32_t resampled_known) {
         finalize_deferred_kernel<<<1, kFinThreads, 0, s>>>(
             n, h->dp, h->w_un, h->s_cur, h->tail_leaves, h->tail_ops, h->n_tail_leaves,
             h->n_tail_ops, h->x[c], h->y[c], h->th[c], h->refp, h->flags, h->cfg.ess_threshold,
-            step_io(h), resampled_known, h->pc.np_recip, h->boff);
+            step_io(h), resampled_known, h->pc.np_recip, h->boff, h->lm, h->lc, h->pc.dt);
         toc(h, 1);
         SLAM_HIP_TRY(hipGetLastError());
         return SLAM_OK;
@@ -418,12 +420,13 @@ int launch_reduce(slam_pf* h, int32_t resampled_known) {
 // __observation (particle_filter.py:144-154) of step ctr[0] from the true pose:
 // world2robot (mylib/transform.py:31-35: the 2x2 rotation through OpenBLAS's
 // fused dgemm) plus the mvn(0, R) noise of normals [n3, n3 + 2 NL) (x @ M,
-// dgemm order); then the step's closed-form log-sum sums (iso handles).
+// dgemm order); then the step's closed-form words (iso handles).
 __global__ __launch_bounds__(512) void pf_mt_observe_kernel(
     const double* __restrict__ normals, const int64_t n3, const double* __restrict__ lm,
     const int32_t nl, const double* __restrict__ truth, const int32_t* __restrict__ ctr,
     const double r0, const double r1, const double r2, const double r3, double* __restrict__ z_all,
-    double* __restrict__ zc, const int32_t closed) {
+    double* __restrict__ zc, const int32_t closed, const double* __restrict__ refp,
+    const double* __restrict__ ctl, const double dt, const int32_t motion) {
     extern __shared__ double s_z[];
     const int32_t st = ctr[0];
     const double* t = truth + 4 * (size_t)st;
@@ -443,25 +446,33 @@ __global__ __launch_bounds__(512) void pf_mt_observe_kernel(
         s_z[2 * (nl + l) + 1] = lm[2 * l + 1];
     }
     __syncthreads();
-    // one component per wave: lane partials, then the butterfly of
-    // closed_sums (pf_kernels.hpp), so host and device sums are the same bits
-    const int k = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    if (closed && k < 8) {
-        DDSum S = closed_lane_partial(k, lane, s_z + 2 * nl, s_z, nl);
-#pragma unroll
-        for (int d = 1; d < kClosedLanes; d <<= 1) {
-            DDSum o;
-            o.h = __shfl_xor(S.h, d, 64);
-            o.l = __shfl_xor(S.l, d, 64);
-            // partner with the lower index is the left operand
-            if ((lane & d) == 0) S = dd_join(S, o);
-            else S = dd_join(o, S);
-        }
-        if (lane == 0) {
-            zc[(size_t)st * kClosedWords + 2 * k] = S.h;
-            zc[(size_t)st * kClosedWords + 2 * k + 1] = S.l;
-        }
-    }
+    if (closed)
+        closed_prep_block(s_z + 2 * nl, s_z, nl, refp, ctl[2 * st], ctl[2 * st + 1], dt, motion,
+                          zc + (size_t)st * kZcWords);
+}
+
+// The step ctr[0]'s closed-form words from its loaded observations (sync-mode
+// steps and the first step of a device-resident batch; later steps of a batch
+// are prepared by the previous step's end).
+__global__ __launch_bounds__(512) void pf_prestep_kernel(const double* __restrict__ lm,
+                                                         const double* __restrict__ z_all,
+                                                         const int32_t nl,
+                                                         const int32_t* __restrict__ ctr,
+                                                         const double* __restrict__ refp,
+                                                         const double* __restrict__ ctl,
+                                                         const double dt, const int32_t motion,
+                                                         double* __restrict__ zc) {
+    const int32_t st = ctr[0];
+    closed_prep_block(lm, z_all + (size_t)st * 2 * nl, nl, refp, ctl[2 * st], ctl[2 * st + 1], dt,
+                      motion, zc + (size_t)st * kZcWords);
+}
+
+int launch_prestep(slam_pf* h) {
+    if (!h->lc.closed) return SLAM_OK;
+    pf_prestep_kernel<<<1, 512, 0, h->stream>>>(h->lm, h->z_all, h->nl, h->ctr, h->refp, h->ctl,
+                                                h->pc.dt, h->cfg.motion, h->zc);
+    SLAM_HIP_TRY(hipGetLastError());
+    return SLAM_OK;
 }
 
 // mvn(0, Q, NP) (particle_filter.py:165): noise = normals @ M, OpenBLAS's order
@@ -486,7 +497,7 @@ int launch_mt(slam_pf* h) {
     if (h->nl > 0)
         pf_mt_observe_kernel<<<1, 512, 32 * (size_t)h->nl, h->stream>>>(
             h->mtb.normals, n3, h->lm, h->nl, h->truth, h->ctr, h->mr[0], h->mr[1], h->mr[2],
-            h->mr[3], h->z_all, h->zc, h->lc.closed);
+            h->mr[3], h->z_all, h->zc, h->lc.closed, h->refp, h->ctl, h->pc.dt, h->cfg.motion);
     if (h->cfg.motion == SLAM_MOTION_LINEAR)
         pf_mt_noise_kernel<<<grid_for(h->n, 256), 256, 0, h->stream>>>(h->n, h->mtb.normals, h->pc,
                                                                      h->noise);
@@ -634,7 +645,9 @@ int create_impl(const slam_pf_config* cfg, int64_t n_local, int64_t n_global, in
     A(h->part, h->nchunks);
     A(h->bp, h->nb_norm);
     A(h->wsum, 1);
-    A(h->refp, 4);
+    // [0..2] last estimate, [4..6] the one before, [7] moves of the first
+    // expansion reference, [8..10] last weighted mean pose, [12..14] the one before
+    A(h->refp, 16);
     A(h->flags, kFlagWords);
     A(h->tk, 4 * kTicketWords);
     A(h->lm, 2 * std::max<int32_t>(n_landmarks, 1));
@@ -667,14 +680,17 @@ int create_impl(const slam_pf_config* cfg, int64_t n_local, int64_t n_global, in
     SLAM_HIP_TRY(hipMemcpy(h->w_un, tmp.data(), n * sizeof(double), hipMemcpyHostToDevice));
     const double one = 1.0;
     SLAM_HIP_TRY(hipMemcpy(h->s_cur, &one, sizeof(double), hipMemcpyHostToDevice));
-    SLAM_HIP_TRY(hipMemcpy(h->refp, cfg->x0, 3 * sizeof(double), hipMemcpyHostToDevice));
+    {
+        const double rp[16] = {cfg->x0[0], cfg->x0[1], cfg->x0[2], 0.0, cfg->x0[0], cfg->x0[1],
+                               cfg->x0[2], 1.0, cfg->x0[0], cfg->x0[1], cfg->x0[2], 0.0,
+                               cfg->x0[0], cfg->x0[1], cfg->x0[2], 0.0};
+        SLAM_HIP_TRY(hipMemcpy(h->refp, rp, sizeof(rp), hipMemcpyHostToDevice));
+    }
     SLAM_HIP_TRY(hipMemset(h->flags, 0, kFlagWords * sizeof(int32_t)));
     SLAM_HIP_TRY(hipMemset(h->tk, 0, 4 * kTicketWords * sizeof(unsigned)));
     SLAM_HIP_TRY(hipMemset(h->ctr, 0, 4 * sizeof(int32_t)));
-    if (n_landmarks > 0) {
+    if (n_landmarks > 0)
         SLAM_HIP_TRY(hipMemcpy(h->lm, landmarks, 2 * n_landmarks * sizeof(double), hipMemcpyHostToDevice));
-        h->lm_host.assign(landmarks, landmarks + 2 * (size_t)n_landmarks);
-    }
     *out = h;
     return SLAM_OK;
 }
@@ -696,39 +712,26 @@ int set_s_one(slam_pf* h) {
     return SLAM_OK;
 }
 
-// the closed-form sums of steps [0, n_steps) of z_host (or of one staged z) into zc
-int upload_closed(slam_pf* h, const double* z, const int32_t n_steps) {
-    if (!h->nl || !h->lc.iso) return SLAM_OK;
-    std::vector<double> zc((size_t)kClosedWords * n_steps);
-    for (int32_t t = 0; t < n_steps; ++t)
-        closed_sums(h->lm_host.data(), z + (size_t)t * 2 * h->nl, h->nl, zc.data() + (size_t)t * kClosedWords);
-    SLAM_HIP_TRY(hipMemcpyAsync(h->zc, zc.data(), zc.size() * sizeof(double), hipMemcpyHostToDevice,
-                                h->stream));
-    return SLAM_OK;
-}
-
 // stage one sync-mode step's inputs into StepIO slot 0
 int stage_inputs(slam_pf* h, const double* control, const double* z, const double* noise,
                  double u) {
-    if (h->nl && z) {
+    if (h->nl && z)
         SLAM_HIP_TRY(hipMemcpyAsync(h->z_all, z, 2 * h->nl * sizeof(double), hipMemcpyHostToDevice,
                                     h->stream));
-        const int rc = upload_closed(h, z, 1);
-        if (rc) return rc;
-    }
     SLAM_HIP_TRY(hipMemcpyAsync(h->ctl, control, 2 * sizeof(double), hipMemcpyHostToDevice, h->stream));
-    h->sh.ofs_host = std::isnan(u) ? u : u * h->pc.np_recip;           // particle_filter.py:214
-    SLAM_HIP_TRY(hipMemcpyAsync(h->ofs, &h->sh.ofs_host, sizeof(double), hipMemcpyHostToDevice, h->stream));
+    h->ofs_host = std::isnan(u) ? u : u * h->pc.np_recip;           // particle_filter.py:214
+    SLAM_HIP_TRY(hipMemcpyAsync(h->ofs, &h->ofs_host, sizeof(double), hipMemcpyHostToDevice, h->stream));
     if (noise)
         SLAM_HIP_TRY(hipMemcpyAsync(h->noise, noise, 3 * h->n * sizeof(double),
                                     hipMemcpyHostToDevice, h->stream));
     h->z_steps = 0;   // slot 0 now holds a single staged step
-    return set_ctr(h, 0);
+    const int rc = set_ctr(h, 0);
+    if (rc || !z) return rc;
+    return launch_prestep(h);
 }
 
 }  // namespace
 
-#include "pf_shard_api.inl"
 #include "pf_dist_api.inl"
 
 #ifdef SLAM_PROBE_COUNT_SLOW
@@ -752,15 +755,6 @@ extern "C" {
 int slam_pf_create(const slam_pf_config* cfg, int64_t n_particles, int32_t n_landmarks,
                    const double* landmarks, int device, slam_pf** out) {
     return create_impl(cfg, n_particles, n_particles, 0, n_landmarks, landmarks, device, out, true);
-}
-
-int slam_pf_create_shard(const slam_pf_config* cfg, int64_t n_local, int64_t n_global,
-                         int64_t gbase, int32_t n_landmarks, const double* landmarks, int device,
-                         slam_pf** out) {
-    SLAM_ARG_CHECK(n_local % kSumChunk == 0 || gbase + n_local == n_global,
-                   "slam_pf_create_shard: every shard but the last must hold a multiple of 8192 "
-                   "particles (np.sum buffer alignment)");
-    return create_impl(cfg, n_local, n_global, gbase, n_landmarks, landmarks, device, out, false);
 }
 
 int slam_pf_destroy(slam_pf* h) {
@@ -803,12 +797,6 @@ int slam_pf_set_landmarks(slam_pf* h, const double* landmarks) {
     if (h->nl) {
         SLAM_HIP_TRY(hipMemcpyAsync(h->lm, landmarks, 2 * h->nl * sizeof(double),
                                     hipMemcpyHostToDevice, h->stream));
-        h->lm_host.assign(landmarks, landmarks + 2 * (size_t)h->nl);
-        // the loaded batch's closed-form sums depend on the landmarks
-        if (h->z_steps > 0) {
-            const int rc = upload_closed(h, h->z_host.data(), h->z_steps);
-            if (rc) return rc;
-        }
     }
     SLAM_HIP_TRY(hipStreamSynchronize(h->stream));
     return SLAM_OK;
@@ -1003,8 +991,6 @@ int slam_pf_load_observations(slam_pf* h, int32_t n_steps, const double* z_all) 
     if (h->nl) {
         SLAM_HIP_TRY(hipMemcpyAsync(h->z_all, z_all, (size_t)n_steps * 2 * h->nl * sizeof(double),
                                     hipMemcpyHostToDevice, h->stream));
-        if (h->lc.iso) h->z_host.assign(z_all, z_all + (size_t)n_steps * 2 * h->nl);
-        if ((rc = upload_closed(h, z_all, n_steps))) return rc;
     }
     std::vector<double> nan((size_t)n_steps, std::nan(""));
     SLAM_HIP_TRY(hipMemcpyAsync(h->ofs, nan.data(), n_steps * sizeof(double), hipMemcpyHostToDevice,
@@ -1026,6 +1012,7 @@ int slam_pf_run(slam_pf* h, int32_t first_step, int32_t n_steps, const double* c
     SLAM_HIP_TRY(hipMemcpyAsync(h->ctl + 2 * first_step, controls, 2 * n_steps * sizeof(double),
                                 hipMemcpyHostToDevice, h->stream));
     if ((rc = set_ctr(h, first_step)) || (rc = set_flag(h, kFlagResample, h->resample_next))) return rc;
+    if (!h->mt && (rc = launch_prestep(h))) return rc;         // the first step's closed-form words
     if (h->resample_next && (rc = launch_bsum(h))) return rc;   // prefix for the first step's scan
     const bool graphs = h->use_graph && !h->timing;
     // one captured hipGraph per ping-pong parity for kGraphSteps steps (even:
@@ -1164,6 +1151,13 @@ int slam_pf_set_resample_next(slam_pf* h, int32_t on) {
     int rc = set_flag(h, kFlagResample, h->resample_next);
     if (rc) return rc;
     SLAM_HIP_TRY(hipStreamSynchronize(h->stream));
+    return SLAM_OK;
+}
+
+int slam_pf_set_ess_band(slam_pf* h, double band) {
+    SLAM_ARG_CHECK(h && band >= 0.0, "slam_pf_set_ess_band: bad argument");
+    h->ess_band = band;
+    drop_graphs(h);                  // captured step kernels carry the band
     return SLAM_OK;
 }
 

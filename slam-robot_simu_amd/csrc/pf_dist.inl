@@ -120,19 +120,48 @@ __device__ __forceinline__ void dist_signal(const DistPeers& P, const int kind, 
     }
 }
 
+// #{i in [0, N): fl(fl(i*step) + ofs) <= x}  (resample positions are monotone)
+__device__ __forceinline__ int64_t count_positions(const double x, const int64_t N,
+                                                   const double step, const double ofs) {
+    int64_t lo = 0, hi = N;
+    while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        const double pos = (double)mid * step + ofs;
+        if (pos <= x) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+
+// A wait that expired marks the shard dead (flags[kFlagDistDead], never reset
+// on this handle): every later wait reports kDistStWait at once instead of
+// polling again, so a dead peer costs one bounded wait per handle, not one per
+// wait of every replayed step.
+__device__ __forceinline__ bool dist_dead(int32_t* flags) {
+    return __hip_atomic_load(&flags[kFlagDistDead], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+}
+__device__ __forceinline__ void dist_mark_dead(int32_t* flags) {
+    atomicOr(&flags[kFlagStatus], kDistStWait);
+    __hip_atomic_store(&flags[kFlagDistDead], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // wait until every peer published `epoch` in my flag words [kind][q]
 // (bounded: ~2^24 polls, ~20 s, then status bit kDistStWait and proceed)
 __device__ __forceinline__ void dist_wait(const DistPeers& P, const int kind, const uint64_t epoch,
                                           int32_t* flags) {
     if ((int)threadIdx.x < P.world) {
         const uint64_t* f = dist_flags(P, P.rank) + kind * kDistMaxWorld + threadIdx.x;
-        int64_t polls = 0;
-        while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < epoch) {
-            if (++polls > (int64_t(1) << 24)) {
-                atomicOr(&flags[kFlagStatus], kDistStWait);
-                break;
+        if (dist_dead(flags)) {
+            atomicOr(&flags[kFlagStatus], kDistStWait);
+        } else {
+            int64_t polls = 0;
+            while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < epoch) {
+                if (++polls > (int64_t(1) << 24)) {
+                    dist_mark_dead(flags);
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(2);
             }
-            __builtin_amdgcn_s_sleep(2);
         }
     }
     __syncthreads();
@@ -447,7 +476,9 @@ __device__ __forceinline__ void dist_item_offsets(const DistPeers& P, int64_t* s
     int64_t o = 0;
     for (int q = 0; q < P.world; ++q) {
         s_off[q] = o;
-        o += (int64_t)ld_sys(reinterpret_cast<const int64_t*>(mine + P.L.item_hdr) + 2 * q);
+        // a count outside [0, cap] (a peer that never published) reads no slot past the region
+        const int64_t c = (int64_t)ld_sys(reinterpret_cast<const int64_t*>(mine + P.L.item_hdr) + 2 * q);
+        o += c < 0 ? 0 : (c > P.L.cap_item ? P.L.cap_item : c);
     }
     s_off[P.world] = o;
 }
@@ -560,14 +591,15 @@ __device__ __forceinline__ bool dist_token_wait(const int32_t* word, const int32
     __shared__ int s_go;
     if (threadIdx.x == 0) {
         int go = 0;
-        for (int it = 0; it < kDistTokenWait; ++it) {
+        const int bound = dist_dead(flags) ? 1 : kDistTokenWait;   // dead: one look, no poll
+        for (int it = 0; it < bound; ++it) {
             if (ld_wt_i(word) == token) {
                 go = 1;
                 break;
             }
             __builtin_amdgcn_s_sleep(2);
         }
-        if (!go) atomicOr(&flags[kFlagStatus], kDistStWait);
+        if (!go) dist_mark_dead(flags);
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         s_go = go;
     }
@@ -1319,7 +1351,7 @@ __device__ __forceinline__ void dist_finalize(const int64_t n, const DeferParts&
         }
         flags[kFlagStatus] |= st;
         const int32_t stp = io.ctr[0];
-        write_result_xe(tot, xe, refp, s, flags, ess_th, io.res + stp, -1);
+        write_result_xe(tot, xe, refp, s, flags, ess_th, io.ess_band, io.res + stp, -1);
         io.ctr[0] = stp + 1;
         io.ctr[1] = io.ctr[1] + 1;
         *s_cur = s;
@@ -1364,15 +1396,34 @@ __global__ __launch_bounds__(kFinThreads) void dist_reduce_kernel(
     const double* __restrict__ ys, const double* __restrict__ ts, double* __restrict__ s_cur,
     double* __restrict__ refp, int32_t* __restrict__ flags, const double ess_th, StepIO io,
     const double np_recip, double* __restrict__ boff, DistScratch* __restrict__ scr,
-    const DistPeers P) {
+    const DistPeers P, const double* __restrict__ lm, const LikConst lc, const double dt) {
     __shared__ double sh[2048];                             // buffer partials (nch <= 2048)
+    __shared__ double s_prep[16];                           // the next step's closed-form sums
     const uint64_t epoch = dist_epoch(io);
     PROBE_AT(27);
+    // the next step's closed-form words (as finalize_deferred_kernel): its sums
+    // here, its expansion about this step's refp (read before the finalize
+    // replaces it) by the last wave before the global fold
+    const int32_t st_now = io.ctr[0];
+    const bool prep = FINALIZE && lc.closed && st_now + 1 < io.cap;
+    double prep_rp[3];
+    if (prep) {
+        closed_prep_sums(lm, io.z + (size_t)(st_now + 1) * 2 * lc.nl, lc.nl,
+                         (int)(threadIdx.x >> 6), kFinWaves, s_prep);
+        for (int k = 0; k < 3; ++k) prep_rp[k] = refp[8 + k];     // the mean pose (write_result)
+    }
     if (RECORD)
         dist_record(n, dp, w_un, tail_leaves, tail_ops, n_tail_leaves, n_tail_ops, xs, ys, ts, P,
                     epoch, sh);
     if (FINALIZE) {
-        if (RECORD) __syncthreads();
+        __syncthreads();
+        if (prep && threadIdx.x == kFinThreads - 64) {
+            const int32_t sn = st_now + 1;
+            double px, py, pth;
+            closed_prep_reference(prep_rp, 2, io.ctl[2 * sn], io.ctl[2 * sn + 1], dt, io.motion, px,
+                                  py, pth);
+            closed_prep_constants(s_prep, lc.nl, px, py, pth, io.zc + (size_t)sn * kZcWords);
+        }
         dist_finalize(n, dp, s_cur, refp, flags, ess_th, io, np_recip, boff, scr, P, epoch, sh);
         PROBE_AT(31);
     }

@@ -115,7 +115,7 @@ int dist_enqueue_step(slam_dist* d) {
         kern<<<1, kFinThreads, 0, h->stream>>>(
             h->n, h->dp, h->w_un, h->tail_leaves, h->tail_ops, h->n_tail_leaves, h->n_tail_ops,
             h->x[c], h->y[c], h->th[c], h->s_cur, h->refp, h->flags, h->cfg.ess_threshold,
-            step_io(h), h->pc.np_recip, h->boff, d->scr[i], d->peers[i]);
+            step_io(h), h->pc.np_recip, h->boff, d->scr[i], d->peers[i], h->lm, h->lc, h->pc.dt);
     };
     if (m == 1) {                                         // record + push, wait, global finalize
         reduce(0, dist_reduce_kernel<true, true>);
@@ -195,11 +195,18 @@ int slam_dist_create(slam_pf** shards, int32_t n_held, int32_t world, int32_t ra
     d->local = (n_held == world);
     d->device = shards[0]->device;
     d->sh.assign(shards, shards + n_held);
-    SLAM_HIP_TRY(hipSetDevice(d->device));
+    // every failure from here on releases d and what it holds (slam_dist_destroy)
     auto bail = [&](int rc) {
         slam_dist_destroy(d);
         return rc;
     };
+#define DIST_TRY(expr)                                                                    \
+    do {                                                                                  \
+        const hipError_t e_ = (expr);                                                     \
+        if (e_ != hipSuccess)                                                             \
+            return bail(fail(SLAM_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_))); \
+    } while (0)
+    DIST_TRY(hipSetDevice(d->device));
     // the largest shard sets the slot sizes (shards are equal but the last)
     int64_t nmax = 0;
     for (auto* h : d->sh) nmax = std::max(nmax, h->n);
@@ -234,7 +241,7 @@ int slam_dist_create(slam_pf** shards, int32_t n_held, int32_t world, int32_t ra
         if (hipExtMallocWithFlags(&xb, (size_t)L.total, hipDeviceMallocFinegrained) != hipSuccess)
             return bail(fail(SLAM_ERR_HIP, "slam_dist_create: fine-grained exchange region allocation failed"));
         d->xbuf.push_back((char*)xb);
-        SLAM_HIP_TRY(hipMemset(xb, 0, (size_t)L.flags + 3 * kDistMaxWorld * 8));
+        DIST_TRY(hipMemset(xb, 0, (size_t)L.flags + 3 * kDistMaxWorld * 8));
         void *p1, *p2, *p3, *p4, *p5, *p6, *p7, *p8, *p9;
         const int32_t nbs = h->nb_scan;
         if ((rc = dist_alloc(d, &p1, sizeof(DistScratch))) ||
@@ -247,8 +254,8 @@ int slam_dist_create(slam_pf** shards, int32_t n_held, int32_t world, int32_t ra
             (rc = dist_alloc(d, &p8, sizeof(DistItem) * (size_t)L.cap_item)) ||
             (rc = dist_alloc(d, &p9, sizeof(int32_t) * 2 * kDistMaxWorld * (size_t)nbs)))
             return bail(rc);
-        SLAM_HIP_TRY(hipMemset(p1, 0, sizeof(DistScratch)));
-        SLAM_HIP_TRY(hipMemset(p7, 0, sizeof(unsigned) * 4 * kTicketWords));
+        DIST_TRY(hipMemset(p1, 0, sizeof(DistScratch)));
+        DIST_TRY(hipMemset(p7, 0, sizeof(unsigned) * 4 * kTicketWords));
         d->scr.push_back((DistScratch*)p1);
         d->spec_g.push_back((SpecialIn*)p2);
         d->spec_go.push_back((SpecialOut*)p3);
@@ -295,7 +302,8 @@ int slam_dist_create(slam_pf** shards, int32_t n_held, int32_t world, int32_t ra
     }
     for (auto& P : d->peers)
         for (int q = 0; q <= world; ++q) P.gb[q] = gb[q];
-    SLAM_HIP_TRY(hipDeviceSynchronize());
+    DIST_TRY(hipDeviceSynchronize());
+#undef DIST_TRY
     if (d->local) {
         for (auto& P : d->peers)
             for (int q = 0; q < world; ++q) P.base[q] = d->xbuf[q];
@@ -305,20 +313,30 @@ int slam_dist_create(slam_pf** shards, int32_t n_held, int32_t world, int32_t ra
     return SLAM_OK;
 }
 
+// A rank's bootstrap blob: the IPC handle of its exchange region and the PCI
+// bus id of its GPU (the peer-access preflight of slam_dist_connect).
+constexpr int kDistBusId = 32;
+constexpr size_t kDistBlob = sizeof(hipIpcMemHandle_t) + kDistBusId;
+
 int slam_dist_handle_size(int64_t* bytes) {
     SLAM_ARG_CHECK(bytes, "slam_dist_handle_size: NULL argument");
-    *bytes = (int64_t)sizeof(hipIpcMemHandle_t);
+    *bytes = (int64_t)kDistBlob;
     return SLAM_OK;
 }
 
-// IPC handles of the held shards' exchange regions (n_held x handle size)
+// bootstrap blobs of the held shards (n_held x slam_dist_handle_size bytes)
 int slam_dist_export(slam_dist* d, void* blob) {
     SLAM_ARG_CHECK(d && blob, "slam_dist_export: NULL argument");
     SLAM_HIP_TRY(hipSetDevice(d->device));
+    char bus[kDistBusId];
+    std::memset(bus, 0, sizeof(bus));
+    SLAM_HIP_TRY(hipDeviceGetPCIBusId(bus, kDistBusId - 1, d->device));
     for (int i = 0; i < d->nloc; ++i) {
         hipIpcMemHandle_t hd;
         SLAM_HIP_TRY(hipIpcGetMemHandle(&hd, d->xbuf[i]));
-        std::memcpy((char*)blob + i * sizeof(hd), &hd, sizeof(hd));
+        char* b = (char*)blob + i * kDistBlob;
+        std::memcpy(b, &hd, sizeof(hd));
+        std::memcpy(b + sizeof(hd), bus, kDistBusId);
     }
     return SLAM_OK;
 }
@@ -328,6 +346,25 @@ int slam_dist_connect(slam_dist* d, const void* all_blobs) {
     SLAM_ARG_CHECK(d && all_blobs, "slam_dist_connect: NULL argument");
     if (d->connected) return SLAM_OK;
     SLAM_HIP_TRY(hipSetDevice(d->device));
+    // preflight: every peer's GPU reachable from this one (the exchange stores
+    // into peer memory over xGMI); fail loudly instead of in the first wait
+    for (int q = 0; q < d->world; ++q) {
+        if (q >= d->rank0 && q < d->rank0 + d->nloc) continue;
+        char bus[kDistBusId];
+        std::memcpy(bus, (const char*)all_blobs + q * kDistBlob + sizeof(hipIpcMemHandle_t), kDistBusId);
+        bus[kDistBusId - 1] = 0;
+        int dev = -1;
+        if (hipDeviceGetByPCIBusId(&dev, bus) != hipSuccess || dev < 0)
+            return fail(SLAM_ERR_COMM, std::string("slam_dist_connect: rank ") + std::to_string(q) +
+                                           "'s GPU (PCI " + bus + ") is not visible to this process");
+        if (dev == d->device) continue;                  // ranks sharing one GPU
+        int can = 0;
+        SLAM_HIP_TRY(hipDeviceCanAccessPeer(&can, d->device, dev));
+        if (!can)
+            return fail(SLAM_ERR_COMM, std::string("slam_dist_connect: no peer access from device ") +
+                                           std::to_string(d->device) + " to rank " + std::to_string(q) +
+                                           "'s device " + std::to_string(dev) + " (PCI " + bus + ")");
+    }
     std::vector<char*> base(d->world, nullptr);
     for (int q = 0; q < d->world; ++q) {
         if (q >= d->rank0 && q < d->rank0 + d->nloc) {
@@ -335,7 +372,7 @@ int slam_dist_connect(slam_dist* d, const void* all_blobs) {
             continue;
         }
         hipIpcMemHandle_t hd;
-        std::memcpy(&hd, (const char*)all_blobs + q * sizeof(hd), sizeof(hd));
+        std::memcpy(&hd, (const char*)all_blobs + q * kDistBlob, sizeof(hd));
         void* p = nullptr;
         const hipError_t e = hipIpcOpenMemHandle(&p, hd, hipIpcMemLazyEnablePeerAccess);
         if (e != hipSuccess)
@@ -357,7 +394,7 @@ int slam_dist_connect_comm(slam_dist* d, slam_comm* comm) {
     int rc = slam_comm_info(comm, &w, &r);
     if (rc) return rc;
     SLAM_ARG_CHECK(w == d->world && r == d->rank0, "slam_dist_connect_comm: communicator rank mismatch");
-    const size_t hs = sizeof(hipIpcMemHandle_t);
+    const size_t hs = kDistBlob;
     std::vector<char> mine(hs), all(hs * w);
     if ((rc = slam_dist_export(d, mine.data()))) return rc;
     if ((rc = slam_comm_all_gather_host(comm, mine.data(), all.data(), (int64_t)hs))) return rc;
@@ -431,8 +468,8 @@ int slam_dist_run(slam_dist* d, int32_t first_step, int32_t n_steps, const doubl
                        "slam_dist_run: steps outside the loaded observations");
         SLAM_HIP_TRY(hipMemcpyAsync(h->ctl + 2 * first_step, controls, 2 * n_steps * sizeof(double),
                                     hipMemcpyHostToDevice, h->stream));
-        const int rc = set_ctr(h, first_step);
-        if (rc) return rc;
+        int rc = set_ctr(h, first_step);
+        if (rc || (rc = launch_prestep(h))) return rc;       // the first step's closed-form words
     }
     const bool graphs = d->sh[0]->use_graph && !d->sh[0]->timing;
     hipStream_t s = d->sh[0]->stream;          // LOCAL: the shared stream; else the shard's

@@ -5,7 +5,27 @@
 namespace slam {
 
 constexpr int kMotionNone = 2;     // internal: likelihood-only pass
-constexpr int kClosedWords = 16;   // S_ll, S_lx, S_ly, S_zz, S_zx, S_zy, D, E (hi, lo each)
+
+// Per-step closed-form words of the iso log-sum likelihood (StepIO.zc, one
+// slot of kZcWords doubles per step), formed on the device at the start of
+// every step (closed_prep_*):
+//  * kZcSum + 2k, k < 8: S_ll, S_lx, S_ly, S_zz, S_zx, S_zy, D, E as
+//    double-double (hi, lo) pairs -- the sums of landmarks / observations of
+//    the step (the double-double form of likelihood_lanes);
+//  * the expansion about the step's reference pose (p^, c^, s^): F^ = the
+//    exact sum of squared residuals at it, A, B (gradient in the rotation)
+//    and L2 (landmark second moment about p^) as double-doubles (hi, lo),
+//    S_r (residual sum) and L1 (landmark sum about p^) rounded, and the
+//    coefficients K3..K5 of the per-particle rounding bound.
+enum : int {
+    kZcSum = 0,
+    kZcPx = 16, kZcPy, kZcC, kZcS,
+    kZcFh, kZcFl, kZcA, kZcAl, kZcB, kZcBl, kZcL2, kZcL2l,
+    kZcSrx, kZcSry, kZcL1x, kZcL1y,
+    kZcK1, kZcK2, kZcK3, kZcK4, kZcK5,
+    kZcWords = 40,
+};
+constexpr int kClosedWords = kZcWords;
 constexpr int kSumChunk = 8192;     // np.sum buffer size (particle_filter.py:234 order)
 constexpr int kScanBlock = 2048;    // elements per block of the exact-cumsum passes
 constexpr int kScanThreads = 256;
@@ -53,6 +73,9 @@ struct LikConst {
                             // (every partial product provably stays normal above it)
     double normal_min_l;    // ln(DBL_MIN) + 1: a log prefix above it is a normal partial product
     double neg_ln_den;      // -log(den): log-prefix increment per landmark
+    double expand_vmax;     // closed form: the expansion about the step's reference
+                            // pose is taken when the particle's bound V <= this
+                            // (|dL| <= 1e-14); beyond it the double-double form
     int32_t has_rho;
     int32_t iso;            // sx2 == sy2 and rho == 0 (log-sum shortcut)
     int32_t nl;
@@ -75,10 +98,13 @@ struct PredictConst {
 struct StepIO {
     const double* ctl;      // [cap][2] control (v, omega)
     const double* z;        // [cap][2*NL] robot-frame observations
-    const double* zc;       // [cap][kClosedWords] closed-form log-sum sums (double-double pairs)
+    double* zc;             // [cap][kZcWords] closed-form words (formed on the device per step)
     const double* ofs;      // [cap] host resample offset (NaN: device RNG)
     slam_pf_result* res;    // [cap] result records
     int32_t* ctr;           // [0] step within the batch, [1] global RNG step
+    int32_t cap;            // steps the arrays hold (the step end prepares step ctr[0] + 1 < cap)
+    int32_t motion;         // the handle's motion model (reference pose of the expansion)
+    double ess_band;        // result.ess_near: |ess - ESS_TH| <= ess_band * ESS_TH
 };
 
 struct BlockPartial {
@@ -112,6 +138,8 @@ enum : int {
     kFlagFallback = 3,
     kFlagMarkGen = 4,       // tag of the resample-run marks, advanced by every step end
     kFlagScanToken = 5,     // release token of the merged exact-cumsum launch
+    kFlagDistDead = 6,      // sharded step: a peer wait expired once (sticky: later waits are skipped)
+    kFlagDDWaves = 7,       // closed form: wavefronts of this step that took the double-double form
     kFlagWords = 8,
 };
 
@@ -168,17 +196,6 @@ __host__ __device__ inline DDSum closed_lane_partial(const int k, const int lane
     for (int32_t j = lane; j < nl; j += kClosedLanes)
         closed_term(S, k, lm[2 * j], lm[2 * j + 1], z[2 * j], z[2 * j + 1]);
     return S;
-}
-
-inline void closed_sums(const double* lm, const double* z, const int32_t nl, double* out) {
-    for (int k = 0; k < 8; ++k) {
-        DDSum v[kClosedLanes];
-        for (int t = 0; t < kClosedLanes; ++t) v[t] = closed_lane_partial(k, t, lm, z, nl);
-        for (int d = 1; d < kClosedLanes; d <<= 1)
-            for (int t = 0; t < kClosedLanes; t += 2 * d) v[t] = dd_join(v[t], v[t + d]);
-        out[2 * k] = v[0].h;
-        out[2 * k + 1] = v[0].l;
-    }
 }
 
 }  // namespace slam

@@ -425,6 +425,138 @@ __device__ __forceinline__ dd_t dd_mul(const dd_t a, const dd_t b) {
 __device__ __forceinline__ dd_t dd_scale(const dd_t a, const double p2) {   // p2 = +-2^k: exact
     return {a.h * p2, a.l * p2};
 }
+__device__ __forceinline__ dd_t dd_neg(const dd_t a) { return {-a.h, -a.l}; }
+
+// ====================================================================
+// per-step closed-form words (StepIO.zc slot, pf_kernels.hpp kZc*)
+// ====================================================================
+// Part 1 (every wave of a block, one sum per wave): the eight landmark /
+// observation sums of the step as double-doubles in the fixed order of
+// closed_lane_partial (64 lane partials, then a butterfly with the lower lane
+// on the left), into sdd[16] (LDS).  The caller barriers before part 2.
+__device__ void closed_prep_sums(const double* __restrict__ lm, const double* __restrict__ z,
+                                 const int32_t nl, const int wave, const int nwaves, double* sdd) {
+    const int lane = (int)__lane_id();
+    for (int k = wave; k < 8; k += nwaves) {
+        DDSum S = closed_lane_partial(k, lane, lm, z, nl);
+#pragma unroll
+        for (int d = 1; d < kClosedLanes; d <<= 1) {
+            DDSum o;
+            o.h = __shfl_xor(S.h, d, 64);
+            o.l = __shfl_xor(S.l, d, 64);
+            if ((lane & d) == 0) S = dd_join(S, o);
+            else S = dd_join(o, S);
+        }
+        if (lane == 0) {
+            sdd[2 * k] = S.h;
+            sdd[2 * k + 1] = S.l;
+        }
+    }
+}
+
+// The expansion's reference pose for a step: the weighted mean pose two steps
+// back (rp: x, y, th; refp[12..14] at the step's start, refp[8..10] at the
+// previous step's end) moved `moves` times by the step's control, noise free
+// (motion_model.py:64-86 / particle_filter.py:129-140): twice, or once for the
+// first step after the handle's creation (refp[7] = 1: the initial pose is the
+// particles' state before that step's predict).  Any finite pose gives exact
+// constants; a close one keeps every particle on the fp64 expansion.
+__device__ void closed_prep_reference(const double* rp, const int moves, const double v,
+                                      const double om, const double dt, const int motion,
+                                      double& px, double& py, double& pth) {
+    px = rp[0];
+    py = rp[1];
+    pth = rp[2];
+    if (!(isfinite(px) && isfinite(py) && fabs(pth) < 1e6)) px = py = pth = 0.0;
+    for (int k = 0; k < moves; ++k) {
+        double s0, c0;
+        fast_sincos(pth, &s0, &c0);
+        const double t1 = wrap_angle(pth + om * dt);
+        const double a = v / om;
+        if (motion == SLAM_MOTION_VELOCITY && om != 0.0 && isfinite(a)) {
+            double s1, c1;
+            fast_sincos(t1, &s1, &c1);
+            px = (px - a * s0) + a * s1;
+            py = (py + a * c0) - a * c1;
+        } else if (isfinite(v)) {
+            px = px + v * (dt * c0);
+            py = py + v * (dt * s0);
+        }
+        if (isfinite(t1)) pth = t1;
+    }
+}
+
+// Part 2 (one lane): the constants of the expansion about (p^, c^, s^) from the
+// eight sums, each formed in double-double from the exact identities
+//   l^ = l - p^:  L1 = S_l - NL p^,  L2 = S_ll - 2 p^.S_l + NL |p^|^2,
+//   D^ = D - p^.S_z,  E^ = E - (p^_x S_zy - p^_y S_zx),
+//   A = c^ L2 - D^,  B = s^ L2 - E^,  S_r = R^ L1 - S_z,
+//   F^ = (c^^2 + s^^2) L2 - 2 (c^ D^ + s^ E^) + S_zz
+// (F^ = sum_j |R^(l_j - p^) - z_j|^2, A = sum r^.l^, B = sum r^ x l^), then
+// rounded (F^ kept as a double-double).
+__device__ void closed_prep_constants(const double* sdd, const int32_t nl, const double px,
+                                      const double py, const double pth, double* __restrict__ zc) {
+    double sh, ch;
+    fast_sincos(kHalfPi - pth, &sh, &ch);                 // mylib/transform.py:31
+    const dd_t Sll{sdd[0], sdd[1]}, Slx{sdd[2], sdd[3]}, Sly{sdd[4], sdd[5]}, Szz{sdd[6], sdd[7]};
+    const dd_t Szx{sdd[8], sdd[9]}, Szy{sdd[10], sdd[11]}, Dd{sdd[12], sdd[13]}, Ed{sdd[14], sdd[15]};
+    const double fnl = (double)nl;
+    const dd_t L1x = dd_add2(Slx, dd_neg(dd_two_prod(fnl, px)));
+    const dd_t L1y = dd_add2(Sly, dd_neg(dd_two_prod(fnl, py)));
+    const dd_t r2 = dd_add2(dd_two_prod(px, px), dd_two_prod(py, py));
+    const dd_t t1 = dd_add2(dd_mul_d(Slx, px), dd_mul_d(Sly, py));
+    const dd_t L2 = dd_add2(dd_add2(Sll, dd_scale(t1, -2.0)), dd_mul_d(r2, fnl));
+    const dd_t Dh = dd_add2(Dd, dd_neg(dd_add2(dd_mul_d(Szx, px), dd_mul_d(Szy, py))));
+    const dd_t Eh = dd_add2(Ed, dd_neg(dd_add2(dd_mul_d(Szy, px), dd_mul_d(Szx, -py))));
+    const dd_t A = dd_add2(dd_mul_d(L2, ch), dd_neg(Dh));
+    const dd_t B = dd_add2(dd_mul_d(L2, sh), dd_neg(Eh));
+    const dd_t Srx = dd_add2(dd_add2(dd_mul_d(L1x, ch), dd_neg(dd_mul_d(L1y, sh))), dd_neg(Szx));
+    const dd_t Sry = dd_add2(dd_add2(dd_mul_d(L1x, sh), dd_mul_d(L1y, ch)), dd_neg(Szy));
+    const dd_t kk = dd_add2(dd_two_prod(ch, ch), dd_two_prod(sh, sh));
+    const dd_t rr = dd_add2(dd_mul_d(Dh, ch), dd_mul_d(Eh, sh));
+    const dd_t F = dd_add2(dd_add2(dd_mul(kk, L2), dd_scale(rr, -2.0)), Szz);
+    for (int k = 0; k < 16; ++k) zc[kZcSum + k] = sdd[k];
+    zc[kZcPx] = px;
+    zc[kZcPy] = py;
+    zc[kZcC] = ch;
+    zc[kZcS] = sh;
+    zc[kZcFh] = F.h;
+    zc[kZcFl] = F.l;
+    zc[kZcA] = A.h;
+    zc[kZcAl] = A.l;
+    zc[kZcB] = B.h;
+    zc[kZcBl] = B.l;
+    zc[kZcSrx] = Srx.h;
+    zc[kZcSry] = Sry.h;
+    zc[kZcL2] = L2.h;
+    zc[kZcL2l] = L2.l;
+    zc[kZcL1x] = L1x.h;
+    zc[kZcL1y] = L1y.h;
+    // bound coefficients (likelihood_lanes): K3..K5 weigh the fp64 terms,
+    // K1, K2 the rounding of dc, ds when they are not exact (weight 1/11)
+    zc[kZcK1] = 2.0 * (fabs(A.h) + fabs(B.h)) / 11.0;
+    zc[kZcK2] = 2.0 * L2.h / 11.0;
+    zc[kZcK3] = 2.0 * (fabs(L1x.h) + fabs(L1y.h));
+    zc[kZcK4] = 2.0 * (fabs(Srx.h) + fabs(Sry.h));
+    zc[kZcK5] = fnl;
+}
+
+// Both parts by one block (prestep / observation kernels): refp[12..14] = the
+// mean pose two steps back, refp[7] the moves from it (2; 1 after creation),
+// (v, om) the step's control.
+__device__ void closed_prep_block(const double* __restrict__ lm, const double* __restrict__ z,
+                                  const int32_t nl, const double* refp, const double v,
+                                  const double om, const double dt, const int motion,
+                                  double* __restrict__ zc) {
+    __shared__ double sdd[16];
+    closed_prep_sums(lm, z, nl, (int)(threadIdx.x >> 6), (int)(blockDim.x >> 6), sdd);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double px, py, pth;
+        closed_prep_reference(refp + 12, refp[7] == 1.0 ? 1 : 2, v, om, dt, motion, px, py, pth);
+        closed_prep_constants(sdd, nl, px, py, pth, zc);
+    }
+}
 
 // One landmark factor in the reference's rounding order
 // (particle_filter.py:187-191: mylib/transform.py:31-35 then mlab.bivariate_normal).
@@ -551,8 +683,10 @@ __device__ SLAM_SLOW_ATTR double logsum_slow(const double xn, const double yn, c
 // sequential loop could have left the normal range (subnormal or zero) --
 // takes logsum_slow instead, so the zero set and the subnormal roundings are
 // the reference's (identical zero sets, <= 1e-12 relative).
+// Returns 1 when one of the lane's particles took the closed form's
+// double-double evaluation.
 template <int LIK, int P>
-__device__ __forceinline__ void likelihood_lanes(const double* xn, const double* yn,
+__device__ __forceinline__ int likelihood_lanes(const double* xn, const double* yn,
                                                  const double* sp, const double* cp,
                                                  const double* __restrict__ lm,
                                                  const double* __restrict__ z,
@@ -571,31 +705,106 @@ __device__ __forceinline__ void likelihood_lanes(const double* xn, const double*
         }
 #pragma unroll
         for (int k = 0; k < P; ++k) bn[k] = acc[k];
-        return;
+        return 0;
     }
     double L[P];
+    int lane_dd = 0;
     if (lc.closed) {
-        // sum_j |R(l_j - p) - z_j|^2 in closed form (iso: q_j = that / sx2):
-        //   k |l - p|^2 summed - 2 sum z.R(l - p) + sum |z|^2,  k = c^2 + s^2,
-        // from the step's landmark / observation sums, in double-double (the
-        // terms are ~1e4, the sum ~NL sx2: fp64 would lose ~1e-12 in L).  The
-        // exact value of the reference's sum: the difference to the reference
-        // is its own rounding (~1e-14 relative of the weight).
-        const dd_t Sll{zc[0], zc[1]}, Slx{zc[2], zc[3]}, Sly{zc[4], zc[5]}, Szz{zc[6], zc[7]};
-        const dd_t Szx{zc[8], zc[9]}, Szy{zc[10], zc[11]}, Dd{zc[12], zc[13]}, Ed{zc[14], zc[15]};
+        // sum_j |R(l_j - p) - z_j|^2 in closed form (iso: q_j = that / sx2).
+        // Fast form: the expansion about the step's reference pose (p^, c^, s^),
+        // exact as a polynomial identity for any particle (x, y, c, s):
+        //   d = p - p^, dc = c - c^, ds = s - s^, (u, v) = R(c, s) d,
+        //   F = F^ + 2 (dc A + ds B) + (dc^2 + ds^2) L2            [rotation terms]
+        //          - 2 S_r.(u, v) - 2 (dR L1).(u, v) + NL (u^2 + v^2),  dR = [[dc, -ds], [ds, dc]]
+        // (DESIGN 4.3).  The rotation terms, which carry the cloud's heading
+        // spread (|dc A| and dc^2 L2 reach ~10 while F ~ NL sx2), are formed to
+        // ~u^2 from double-double A, B, L2 (exact products, TwoSum) and summed
+        // with F^ in double-double; dc, ds are exact when c, c^ (s, s^) are
+        // within a factor 2 (Sterbenz), else off by u|dc|; the remaining
+        // terms round in fp64.  All of it stays within 11 u V,
+        //   V = b (a K3 + K4 + b K5) + a (K1 + a K2),  a = |dc| + |ds|, b = |u| + |v|,
+        // so V <= expand_vmax keeps |dL| <= 1e-13.  Beyond it (a particle far from the reference pose) the
+        // double-double form of the same sum from the eight sums.  Either way
+        // the exact value of the sum for the particle's rounded c, s up to that
+        // bound and one final rounding: the difference to the reference is its
+        // own rounding (~1e-14 relative of the weight).
         const double fnl = (double)nl;
+        const double phx = zc[kZcPx], phy = zc[kZcPy], chh = zc[kZcC], shh = zc[kZcS];
+        const double Fh = zc[kZcFh], Fl = zc[kZcFl];
+        const double Ah = zc[kZcA], Al = zc[kZcAl], Bh = zc[kZcB], Bl = zc[kZcBl];
+        const double L2h = zc[kZcL2], L2l = zc[kZcL2l];
+        const double Srx = zc[kZcSrx], Sry = zc[kZcSry];
+        const double L1x = zc[kZcL1x], L1y = zc[kZcL1y];
+        const double K1 = zc[kZcK1], K2 = zc[kZcK2], K3 = zc[kZcK3], K4 = zc[kZcK4];
+        const double K5 = zc[kZcK5];
+        bool dd[P];
+        int any_dd = 0;
 #pragma unroll
         for (int k = 0; k < P; ++k) {
-            const double x = xn[k], y = yn[k], c = cp[k], sn = sp[k];
-            const dd_t r2 = dd_add2(dd_two_prod(x, x), dd_two_prod(y, y));          // |p|^2
-            const dd_t t1 = dd_add2(dd_mul_d(Slx, x), dd_mul_d(Sly, y));            // p . S_l
-            const dd_t p1 = dd_add2(dd_add2(Sll, dd_scale(t1, -2.0)), dd_mul_d(r2, fnl));
-            const dd_t kk = dd_add2(dd_two_prod(c, c), dd_two_prod(sn, sn));
-            const dd_t q1 = dd_add2(Dd, dd_scale(dd_add2(dd_mul_d(Szx, x), dd_mul_d(Szy, y)), -1.0));
-            const dd_t q2 = dd_add2(Ed, dd_scale(dd_add2(dd_mul_d(Szy, x), dd_mul_d(Szx, -y)), -1.0));
-            const dd_t rr = dd_add2(dd_mul_d(q1, c), dd_mul_d(q2, sn));
-            const dd_t acc = dd_add2(dd_add2(dd_mul(kk, p1), dd_scale(rr, -2.0)), Szz);
-            L[k] = nl ? fma(-0.5, acc.h * lc.rsx2, lc.neg_nl_ln_den) : lc.neg_nl_ln_den;
+            const double c = cp[k], sn = sp[k];
+            const double dx = xn[k] - phx, dy = yn[k] - phy;
+            const double dc = c - chh, ds = sn - shh;
+            // rotation terms to ~u^2: 2 t1 = 2 (dc A + ds B), t3 = (dc^2 + ds^2) L2
+            const double p1 = dc * Ah, e1 = fma(dc, Ah, -p1);
+            const double p2 = ds * Bh, e2 = fma(ds, Bh, -p2);
+            const double q1 = dc * dc, f1 = fma(dc, dc, -q1);
+            const double q2 = ds * ds, f2 = fma(ds, ds, -q2);
+            const double a2 = q1 + q2;
+            const double a2b = a2 - q1;
+            const double a2e = ((q1 - (a2 - a2b)) + (q2 - a2b)) + (f1 + f2);
+            const double p3 = a2 * L2h;
+            const double e3 = fma(a2, L2h, -p3) + fma(a2e, L2h, a2 * L2l);
+            // translation terms in fp64: t2 = S_r . R d, t4 = dR L1 . R d, t5 = NL |R d|^2
+            const double u = fma(c, dx, -(sn * dy));
+            const double v = fma(sn, dx, c * dy);
+            const double t2 = fma(Srx, u, Sry * v);
+            const double gx = fma(dc, L1x, -(ds * L1y)), gy = fma(ds, L1x, dc * L1y);
+            const double t4 = fma(gx, u, gy * v);
+            const double t5 = fma(u, u, v * v) * fnl;
+            // F^h + 2 p1 + 2 p2 + p3 by TwoSum, then every low part
+            double h = Fh, lo;
+            {
+                const double b = 2.0 * p1, t = h + b, bb = t - h;
+                lo = (h - (t - bb)) + (b - bb);
+                h = t;
+            }
+            {
+                const double b = 2.0 * p2, t = h + b, bb = t - h;
+                lo += (h - (t - bb)) + (b - bb);
+                h = t;
+            }
+            {
+                const double t = h + p3, bb = t - h;
+                lo += (h - (t - bb)) + (p3 - bb);
+                h = t;
+            }
+            const double rot_lo = fma(2.0, (e1 + e2) + fma(dc, Al, ds * Bl), e3);
+            lo = lo + ((Fl + rot_lo) + (fma(-2.0, t2 + t4, t5)));
+            const double F = h + lo;
+            const double a = fabs(dc) + fabs(ds), b = fabs(u) + fabs(v);
+            const double V = fma(b, fma(a, K3, fma(b, K5, K4)), a * fma(a, K2, K1));
+            dd[k] = !(V <= lc.expand_vmax);                                  // also NaN
+            any_dd |= dd[k] ? 1 : 0;
+            L[k] = nl ? fma(-0.5, F * lc.rsx2, lc.neg_nl_ln_den) : lc.neg_nl_ln_den;
+        }
+        lane_dd = any_dd;
+        if (any_dd) {
+            const dd_t Sll{zc[0], zc[1]}, Slx{zc[2], zc[3]}, Sly{zc[4], zc[5]}, Szz{zc[6], zc[7]};
+            const dd_t Szx{zc[8], zc[9]}, Szy{zc[10], zc[11]}, Dd{zc[12], zc[13]}, Ed{zc[14], zc[15]};
+#pragma unroll
+            for (int k = 0; k < P; ++k) {
+                if (!dd[k]) continue;
+                const double x = xn[k], y = yn[k], c = cp[k], sn = sp[k];
+                const dd_t r2 = dd_add2(dd_two_prod(x, x), dd_two_prod(y, y));          // |p|^2
+                const dd_t t1 = dd_add2(dd_mul_d(Slx, x), dd_mul_d(Sly, y));            // p . S_l
+                const dd_t p1 = dd_add2(dd_add2(Sll, dd_scale(t1, -2.0)), dd_mul_d(r2, fnl));
+                const dd_t kk = dd_add2(dd_two_prod(c, c), dd_two_prod(sn, sn));
+                const dd_t q1 = dd_add2(Dd, dd_scale(dd_add2(dd_mul_d(Szx, x), dd_mul_d(Szy, y)), -1.0));
+                const dd_t q2 = dd_add2(Ed, dd_scale(dd_add2(dd_mul_d(Szy, x), dd_mul_d(Szx, -y)), -1.0));
+                const dd_t rr = dd_add2(dd_mul_d(q1, c), dd_mul_d(q2, sn));
+                const dd_t acc = dd_add2(dd_add2(dd_mul(kk, p1), dd_scale(rr, -2.0)), Szz);
+                L[k] = nl ? fma(-0.5, acc.h * lc.rsx2, lc.neg_nl_ln_den) : lc.neg_nl_ln_den;
+            }
         }
     } else if (lc.iso) {
         double a[P][2];
@@ -697,6 +906,7 @@ __device__ __forceinline__ void likelihood_lanes(const double* xn, const double*
         for (int k = 0; k < P; ++k)
             if (slot[k] >= 0) bn[k] = s_bn[slot[k]];
     }
+    return lane_dd;
 }
 
 // The fused step kernel: [resample gather +] predict + likelihood + weight.
@@ -917,8 +1127,9 @@ __global__ __launch_bounds__(256) SLAM_FUSED_ATTR void pf_fused_kernel(
 
     // ---- likelihood and weight (particle_filter.py:170-198)
     double bn[P];
-    likelihood_lanes<LIK, P>(xv, yv, sp, cp, lm, zs, io.zc + (size_t)st * kClosedWords, lc, bn,
-                             wave_s);
+    const int lane_dd = likelihood_lanes<LIK, P>(xv, yv, sp, cp, lm, zs,
+                                                 io.zc + (size_t)st * kZcWords, lc, bn, wave_s);
+    if (__ballot(lane_dd) != 0 && __lane_id() == 0) atomicAdd(&flags[kFlagDDWaves], 1);
     // previous weights: particle_filter.py:222 (a resampled step starts from
     // 1/NP) / :235-236 (deferred: w_un / s, NaN -> 1/NP)
     double wv[P];
@@ -1214,7 +1425,8 @@ __device__ __forceinline__ BlockPartial bp_block_reduce(BlockPartial a, BlockPar
 __device__ void write_result(const BlockPartial& r, const double* xs, const double* ys,
                              const double* ts, const int64_t gbase, double* refp,
                              const double s, int32_t* flags, const double ess_th,
-                             slam_pf_result* res, const int32_t resampled_known) {
+                             const double ess_band, slam_pf_result* res,
+                             const int32_t resampled_known) {
     slam_pf_result o;
     const int64_t mi = r.maxi;
     o.max_idx = mi;
@@ -1231,21 +1443,33 @@ __device__ void write_result(const BlockPartial& r, const double* xs, const doub
     o.weight_sum = s;
     o.resampled = resampled_known >= 0 ? resampled_known : (flags[kFlagResample] != 0);
     o.resample_next = (o.ess < ess_th) ? 1 : 0;
+    o.ess_near = (fabs(o.ess - ess_th) <= ess_band * ess_th) ? 1 : 0;
     o.status = flags[kFlagStatus];
     o.n_special = flags[kFlagNSpecial];
+    o.dd_waves = flags[kFlagDDWaves];
+    flags[kFlagDDWaves] = 0;
     flags[kFlagResample] = o.resample_next;
     flags[kFlagMarkGen] = flags[kFlagMarkGen] + 1;
     flags[kFlagStatus] = 0;
-    refp[0] = o.x_est[0];
-    refp[1] = o.x_est[1];
-    refp[2] = o.x_est[2];
+    // the weighted mean pose (the moments' origin is the old refp), kept two
+    // steps deep as the expansion's reference (closed_prep_reference): the
+    // centre of the cloud the next steps' particles are resampled from
+    for (int k = 0; k < 3; ++k) {
+        const double m = refp[k] + mu[k];
+        refp[12 + k] = refp[8 + k];
+        refp[8 + k] = isfinite(m) ? m : o.x_est[k];
+        refp[4 + k] = refp[k];
+        refp[k] = o.x_est[k];
+    }
+    refp[7] = 2.0;
     *res = o;
 }
 
 // result record with x_est given (deferred path: taken from the block partials)
 __device__ void write_result_xe(const BlockPartial& r, const double* xe, double* refp,
                                 const double s, int32_t* flags, const double ess_th,
-                                slam_pf_result* res, const int32_t resampled_known) {
+                                const double ess_band, slam_pf_result* res,
+                                const int32_t resampled_known) {
     slam_pf_result o;
     o.max_idx = r.maxi;
     o.max_val = r.maxv;
@@ -1261,14 +1485,25 @@ __device__ void write_result_xe(const BlockPartial& r, const double* xe, double*
     o.weight_sum = s;
     o.resampled = resampled_known >= 0 ? resampled_known : (flags[kFlagResample] != 0);
     o.resample_next = (o.ess < ess_th) ? 1 : 0;
+    o.ess_near = (fabs(o.ess - ess_th) <= ess_band * ess_th) ? 1 : 0;
     o.status = flags[kFlagStatus];
     o.n_special = flags[kFlagNSpecial];
+    o.dd_waves = flags[kFlagDDWaves];
+    flags[kFlagDDWaves] = 0;
     flags[kFlagResample] = o.resample_next;
     flags[kFlagMarkGen] = flags[kFlagMarkGen] + 1;
     flags[kFlagStatus] = 0;
-    refp[0] = o.x_est[0];
-    refp[1] = o.x_est[1];
-    refp[2] = o.x_est[2];
+    // the weighted mean pose (the moments' origin is the old refp), kept two
+    // steps deep as the expansion's reference (closed_prep_reference): the
+    // centre of the cloud the next steps' particles are resampled from
+    for (int k = 0; k < 3; ++k) {
+        const double m = refp[k] + mu[k];
+        refp[12 + k] = refp[8 + k];
+        refp[8 + k] = isfinite(m) ? m : o.x_est[k];
+        refp[4 + k] = refp[k];
+        refp[k] = o.x_est[k];
+    }
+    refp[7] = 2.0;
     *res = o;
 }
 
@@ -1360,7 +1595,7 @@ __global__ __launch_bounds__(1024) void finalize_kernel(
     const BlockPartial tot = bp_block_reduce(c, shp);
     if (threadIdx.x == 0) {
         const int32_t st = io.ctr[0];
-        write_result(tot, xs, ys, ts, gbase, refp, *s_in, flags, ess_th, io.res + st,
+        write_result(tot, xs, ys, ts, gbase, refp, *s_in, flags, ess_th, io.ess_band, io.res + st,
                      resampled_known);
         want_scan = flags[kFlagResample];
         io.ctr[0] = st + 1;                              // advance the step context

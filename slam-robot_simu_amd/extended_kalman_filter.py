@@ -21,7 +21,11 @@ from slamhip.ekf import DeviceEKF, reference_ekf_config
 class ExtendedKalmanFilter(object):
     """EKF localisation with a world-position sensor (GPU filter)."""
 
-    def __init__(self, period_ms, *, device=0):
+    def __init__(self, period_ms, *, device=0, motion="linear", alphas=None):
+        """motion="velocity": the filter's prediction is driven by motion_model.py
+        (MotionModel.moveWithoutNoise, its Jacobian and moveWithNoise's noise
+        from ``alphas`` a1..a6, default 0.1 each); "linear" is the reference's
+        own __f / jacobF / Q.  The simulated truth stays the reference's."""
         p = reference_ekf_config(period_ms)
         self.dt = p["dt"]                                          # :29
         self.omega = p["omega"]                                    # :46
@@ -33,7 +37,8 @@ class ExtendedKalmanFilter(object):
         self.R_act = self.R                                        # :71
         self.x_true = p["x0"].reshape(3, 1).copy()                 # :74-79
         self.x_dr = self.x_true.copy()
-        self.dev = DeviceEKF(1, device=device, **p)
+        kw = {} if alphas is None else {"alphas": alphas}
+        self.dev = DeviceEKF(1, device=device, motion=motion, **kw, **p)
 
     def _f(self, x, v=None, om=None):
         """extended_kalman_filter.py:160-178 (host copy for truth / dead reckoning)."""

@@ -36,18 +36,20 @@ class PFResult(C.Structure):
     _fields_ = [("x_est", C.c_double * 3), ("cov", C.c_double * 9), ("max_val", C.c_double),
                 ("ess", C.c_double), ("weight_sum", C.c_double), ("max_idx", C.c_int64),
                 ("resampled", C.c_int32), ("resample_next", C.c_int32), ("status", C.c_int32),
-                ("n_special", C.c_int32)]
+                ("n_special", C.c_int32), ("ess_near", C.c_int32), ("dd_waves", C.c_int32)]
 
 
 class EKFConfig(C.Structure):
     _fields_ = [("dt", C.c_double), ("vel", C.c_double), ("omega", C.c_double),
                 ("q", C.c_double * 9), ("r", C.c_double * 4), ("x0", C.c_double * 3),
-                ("p0", C.c_double * 9)]
+                ("p0", C.c_double * 9), ("motion", C.c_int32), ("pad0", C.c_int32),
+                ("alphas", C.c_double * 6)]
 
 
 class EKFSLAMConfig(C.Structure):
     _fields_ = [("dt", C.c_double), ("q_robot", C.c_double * 9), ("r_dist", C.c_double),
-                ("r_dir", C.c_double), ("r_orient", C.c_double)]
+                ("r_dir", C.c_double), ("r_orient", C.c_double), ("motion", C.c_int32),
+                ("pad0", C.c_int32), ("alphas", C.c_double * 6)]
 
 
 class GraphEdge(C.Structure):
@@ -92,6 +94,7 @@ SIGNATURES = {
     "slam_pf_timing": (C.c_int, [_P, C.c_int32, _D, _I64]),
     "slam_pf_set_graphs": (C.c_int, [_P, C.c_int32]),
     "slam_pf_set_scan_merged": (C.c_int, [_P, C.c_int32]),
+    "slam_pf_set_ess_band": (C.c_int, [_P, C.c_double]),
     "slam_pf_set_resample_next": (C.c_int, [_P, C.c_int32]),
     "slam_pf_set_stream": (C.c_int, [_P, _P, C.c_int32]),
     "slam_motion_velocity": (C.c_int, [_D, C.c_int64, _D, C.c_double, C.c_double, _D, _D,
@@ -130,20 +133,6 @@ SIGNATURES = {
     "slam_dist_load_observations": (C.c_int, [_P, C.c_int32, _D]),
     "slam_dist_run": (C.c_int, [_P, C.c_int32, C.c_int32, _D, C.POINTER(PFResult)]),
     "slam_dist_set_merged": (C.c_int, [_P, C.c_int32, C.POINTER(C.c_int32)]),
-    "slam_pf_create_shard": (C.c_int, [C.POINTER(PFConfig), C.c_int64, C.c_int64, C.c_int64,
-                                       C.c_int32, _D, C.c_int, C.POINTER(_P)]),
-    "slam_pf_shard_sizes": (C.c_int, [_P, _I64]),
-    "slam_pf_shard_begin": (C.c_int, [_P, _D, _D, _D, C.c_double, C.c_int32]),
-    "slam_pf_shard_scan_local": (C.c_int, [_P, _P]),
-    "slam_pf_shard_classify": (C.c_int, [_P, _P, C.c_int32, C.c_int32, _P]),
-    "slam_pf_shard_export_specials": (C.c_int, [_P, C.c_int64, _P]),
-    "slam_pf_shard_fold": (C.c_int, [_P, _P, C.c_int64, _I64, C.c_int32, C.c_int32]),
-    "slam_pf_shard_plan": (C.c_int, [_P, _I64, C.c_int32, _I64]),
-    "slam_pf_shard_export_items": (C.c_int, [_P, _P]),
-    "slam_pf_shard_import_items": (C.c_int, [_P, _P, C.c_int64]),
-    "slam_pf_shard_predict_update": (C.c_int, [_P, _P]),
-    "slam_pf_shard_normalize": (C.c_int, [_P, _P, C.c_int64, _P]),
-    "slam_pf_shard_finish": (C.c_int, [_P, _P, C.c_int32, C.POINTER(PFResult)]),
     "slam_ekf_create": (C.c_int, [C.POINTER(EKFConfig), C.c_int64, C.c_int, C.POINTER(_P)]),
     "slam_ekf_destroy": (C.c_int, [_P]),
     "slam_ekf_set_state": (C.c_int, [_P, _D, _D]),

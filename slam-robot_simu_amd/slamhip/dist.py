@@ -69,7 +69,11 @@ class DistFilter:
     """One particle filter over ``world`` shards."""
 
     def __init__(self, n_global, landmarks, *, world, rank=None, comm=None, all_gather=None,
-                 device=0, **cfg_kw):
+                 device=0, connect=True, **cfg_kw):
+        """connect=False (one rank per process): create the shard and its
+        exchange region only; the caller then gathers ``export_handle()`` from
+        every rank and calls ``connect(blobs)`` -- so a harness can agree on
+        every rank's local success before and after the one collective."""
         lib = _lib.load()
         self._lib = lib
         self.n_global, self.world = int(n_global), int(world)
@@ -93,7 +97,7 @@ class DistFilter:
             check(lib.slam_dist_create(arr, len(self._shards), self.world, self.ranks[0], C.byref(d)),
                   "slam_dist_create")
             self._d = d
-            if rank is not None:
+            if rank is not None and connect:
                 if comm is not None:
                     check(lib.slam_dist_connect_comm(d, comm._h), "slam_dist_connect_comm")
                 else:
@@ -108,6 +112,21 @@ class DistFilter:
             self.close()
             raise
         self.resample_next = False
+
+    def export_handle(self) -> bytes:
+        """This rank's exchange-region IPC handle (slam_dist_export)."""
+        size = C.c_int64(0)
+        check(self._lib.slam_dist_handle_size(C.byref(size)), "slam_dist_handle_size")
+        mine = C.create_string_buffer(size.value)
+        check(self._lib.slam_dist_export(self._d, mine), "slam_dist_export")
+        return mine.raw
+
+    def connect(self, blobs):
+        """Open every peer's exchange region (blobs: every rank's
+        export_handle(), rank order; slam_dist_connect preflights peer access)."""
+        size = len(blobs[0])
+        allb = C.create_string_buffer(b"".join(blobs), size * self.world)
+        check(self._lib.slam_dist_connect(self._d, allb), "slam_dist_connect")
 
     def close(self):
         if getattr(self, "_d", None):

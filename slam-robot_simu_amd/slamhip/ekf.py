@@ -27,13 +27,25 @@ def reference_ekf_config(period_ms=100):
                 p0=np.diag([0.01, 0.01, np.deg2rad(30.0)]) ** 2)
 
 
-class DeviceEKF:
-    """``batch`` independent 3-state EKFs on one GPU (batch=1: the reference's filter)."""
+_MOTIONS = {"linear": 0, "velocity": 1}
+DEFAULT_ALPHAS = (0.1, 0.1, 0.1, 0.1, 0.1, 0.1)     # graph_based_slam.py:605 MotionModel(2.0, 0.1 x 6)
 
-    def __init__(self, batch=1, *, device=0, **params):
+
+class DeviceEKF:
+    """``batch`` independent 3-state EKFs on one GPU (batch=1: the reference's filter).
+
+    ``motion="linear"``: the reference's prediction (extended_kalman_filter.py
+    :160-194, Q).  ``motion="velocity"``: the prediction driven by
+    motion_model.py (north_star) -- f = MotionModel.moveWithoutNoise, its
+    Jacobian, and the process noise of moveWithNoise from ``alphas`` (a1..a6)."""
+
+    def __init__(self, batch=1, *, device=0, motion="linear", alphas=DEFAULT_ALPHAS, **params):
         p = reference_ekf_config()
         p.update(params)
         cfg = EKFConfig()
+        cfg.motion = _MOTIONS[motion]
+        cfg.alphas[:] = [float(a) for a in alphas]
+        self.motion = motion
         cfg.dt, cfg.vel, cfg.omega = float(p["dt"]), float(p["vel"]), float(p["omega"])
         cfg.q[:] = [float(v) for v in np.asarray(p["q"], float).ravel()]
         cfg.r[:] = [float(v) for v in np.asarray(p["r"], float).ravel()]
@@ -116,9 +128,13 @@ class DeviceEKFSLAM:
     """EKF-SLAM over ``n_landmarks`` landmarks (x, y, phi); covariance in HBM."""
 
     def __init__(self, n_landmarks, *, dt=0.1, q_robot=None, noise=(0.05, np.deg2rad(2.0),
-                                                                         np.deg2rad(2.0)), device=0):
+                                                                         np.deg2rad(2.0)), device=0,
+                 motion="linear", alphas=DEFAULT_ALPHAS):
         cfg = EKFSLAMConfig()
         cfg.dt = float(dt)
+        cfg.motion = _MOTIONS[motion]
+        cfg.alphas[:] = [float(a) for a in alphas]
+        self.motion = motion
         q = np.diag([0.1, 0.1, np.deg2rad(0.1)]) ** 2 if q_robot is None else np.asarray(q_robot)
         cfg.q_robot[:] = [float(v) for v in q.ravel()]
         cfg.r_dist, cfg.r_dir, cfg.r_orient = (float(v) for v in noise)

@@ -151,7 +151,7 @@ class DeviceParticleFilter:
                 "max_val": r.max_val, "max_idx": int(r.max_idx), "ess": r.ess,
                 "weight_sum": r.weight_sum, "resampled": bool(r.resampled),
                 "resample_next": bool(r.resample_next), "status": r.status,
-                "n_special": r.n_special}
+                "n_special": r.n_special, "ess_near": bool(r.ess_near), "dd_waves": r.dd_waves}
 
     def step(self, control, z, noise=None, u_resample=float("nan")):
         ctl = _f64(control, (2,))
@@ -208,14 +208,44 @@ class DeviceParticleFilter:
               "slam_pf_load_observations")
         self._z_steps = z_all.shape[0]
 
-    def run(self, first_step, controls, want_results=True):
+    def run(self, first_step, controls, want_results=True, confirm_ess=False):
+        """Device-resident steps [first_step, first_step + len(controls)) from
+        the loaded observations (hipGraph replays, no host decision).  Each
+        result carries ``ess_near``: the device's ESS fell within
+        ESS_CONFIRM_BAND of ESS_TH, where the reference's `1 / (pw @ pw.T)`
+        (BLAS order) could decide the next resample differently.
+
+        ``confirm_ess=True`` (parity batches): one replayed step at a time, and
+        every ess_near step's decision re-formed on the host by the reference's
+        own expression before the next step runs (as ``step`` does); results
+        then carry ``ess_confirmed`` / ``ess_host`` like ``step``'s."""
         controls = _f64(controls).reshape(-1, 2)
         k = controls.shape[0]
+        if confirm_ess:
+            outs = []
+            for i in range(k):
+                res = (PFResult * 1)()
+                check(self._lib.slam_pf_run(self._h, int(first_step) + i, 1, dptr(controls[i:i + 1]),
+                                            res), "slam_pf_run")
+                out = self._res(res[0])
+                self.resample_next = out["resample_next"]
+                if out["ess_near"]:
+                    self._confirm_ess(out)
+                else:
+                    out["ess_confirmed"] = False
+                outs.append(out)
+            return outs if want_results else None
         res = (PFResult * k)()
         check(self._lib.slam_pf_run(self._h, int(first_step), k, dptr(controls), res),
               "slam_pf_run")
         self.resample_next = bool(res[k - 1].resample_next)
         return [self._res(r) for r in res] if want_results else None
+
+    def set_ess_band(self, band):
+        """Relative band of result['ess_near'] (and of the drop-in's host
+        confirmation); default 1e-9."""
+        check(self._lib.slam_pf_set_ess_band(self._h, float(band)), "slam_pf_set_ess_band")
+        self.ESS_CONFIRM_BAND = float(band)
 
     # ------------------------------------------------ NumPy stream on device
     def use_numpy_stream(self, state=None):

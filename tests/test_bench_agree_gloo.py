@@ -1,0 +1,97 @@
+"""bench.py's multi-rank agreement protocol on CPU (world size 2, gloo): the
+sharded setup and run phases of measure_sharded use bench.Agreement, so that a
+failure on ONE rank -- after the communicator exists, e.g. a peer GPU that
+cannot be mapped in slam_dist_connect -- sends every rank to the replica
+fallback at the same checkpoint, with every collective still paired.  The GPU
+work is replaced by plain functions; the collectives are the real ones
+(all_reduce MIN of the ok flags, barrier, all_gather_object of the errors)."""
+import os
+import sys
+
+import pytest
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _agree(ok):
+    import torch
+    t = torch.tensor([1 if ok else 0], dtype=torch.int32)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    return int(t.item()) == 1
+
+
+def _worker(rank, world, port, fail_rank, fail_phase, q):
+    sys.path.insert(0, ROOT)
+    import bench
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    log = []
+
+    def work(phase):
+        log.append(phase)
+        if rank == fail_rank and phase == fail_phase:
+            raise RuntimeError(f"injected {phase}")
+        return phase
+
+    def sharded():
+        ag = bench.Agreement(_agree, rank)
+        ag.attempt(work, "create")
+        ag.checkpoint("shard create")
+        blob = ag.attempt(work, "export")
+        blobs = [None] * world
+        dist.all_gather_object(blobs, blob)                 # the handle exchange collective
+        ag.checkpoint("handle exchange")
+        ag.attempt(work, "connect")
+        ag.checkpoint("connect")
+        ag.attempt(work, "warmup")
+        dist.barrier()                                      # timed region: barrier on every rank
+        ag.attempt(work, "timed")
+        dist.barrier()
+        ag.checkpoint("run")
+        return "sharded"
+
+    try:
+        mode, phase = sharded(), None
+    except bench.ShardedFailure as e:
+        phase, mine = e.args
+        errs = [None] * world
+        dist.all_gather_object(errs, mine)
+        mode = "replicas"
+        phase = phase + " | " + "; ".join(x for x in errs if x)
+    dist.barrier()
+    dist.destroy_process_group()
+    q.put((rank, mode, phase, log))
+
+
+@pytest.mark.parametrize("fail_rank,fail_phase,expect_phase",
+                         [(None, None, None), (1, "connect", "connect"), (0, "export", "handle exchange"),
+                          (1, "timed", "run"), (0, "create", "shard create")])
+def test_one_rank_failure_agreed(fail_rank, fail_phase, expect_phase):
+    import socket
+    world = 2
+    with socket.socket() as sk:                          # a free local port
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, fail_rank, fail_phase, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    modes = {m for _, m, _, _ in res}
+    if fail_rank is None:
+        assert modes == {"sharded"}
+        return
+    assert modes == {"replicas"}, res
+    for _, _, phase, log in res:
+        assert phase.startswith(expect_phase), phase
+        assert f"rank {fail_rank}" in phase and f"injected {fail_phase}" in phase
+    # the failing rank did no work after its failure; the others stopped at the checkpoint
+    flog = res[fail_rank][3]
+    assert flog[-1] == fail_phase

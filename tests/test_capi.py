@@ -44,7 +44,7 @@ def test_version_and_device_query_without_gpu():
 def test_struct_layouts():
     from slamhip import _lib
     assert ctypes.sizeof(_lib.PFConfig) == 8 * (1 + 1 + 4 + 9 + 6 + 3 + 1) + 8
-    assert ctypes.sizeof(_lib.PFResult) == 8 * (3 + 9 + 3 + 1) + 16
+    assert ctypes.sizeof(_lib.PFResult) == 8 * (3 + 9 + 3 + 1) + 24
 
 
 def test_create_without_device_fails_loudly():

@@ -30,8 +30,13 @@ def test_bench_json_contract():
     assert d["unit"] == "particle-observation updates/s" and d["value"] > 1e10
     assert abs(d["value"] - 2 ** 20 * 100 / (d["ms_per_step"] / 1e3)) <= 1e-6 * d["value"]
     rf = d["roofline"]
-    assert rf["bound"] == "valu_fp64" and 0 < rf["frac"] <= 1
+    assert rf["bound"] in ("valu_fp64", "hbm") and 0 < rf["frac"] <= 1
     assert abs(rf["frac"] - rf["achieved"] / rf["peak"]) < 1e-12
+    # the binding one of executed fp64 and HBM bytes
+    assert rf["frac"] >= rf["hbm"]["frac"] - 1e-15
+    if rf["fp64"]["frac"] is not None:
+        assert rf["frac"] >= rf["fp64"]["frac"] - 1e-15
+    assert d["closed_form_fallback_waves"] == 0 and d["ess_near_steps"] >= 0
     assert d["config"]["particles_per_gpu"] == 2 ** 20 and d["config"]["landmarks"] == 100
 
 
@@ -46,8 +51,8 @@ def _bench_line(cmd):
 
 @pytest.mark.parametrize("launcher", ["direct", "torchrun"])
 def test_bench_sharded_mode(launcher):
-    # --mode sharded: the ShardedFilter orchestration over one shard, in-process
-    # (LocalComm) or as a 1-rank RCCL group (TorchComm over nccl)
+    # --mode sharded: the device-resident sharded step over one shard, in-process
+    # or as a 1-rank group under torch.distributed.run
     args = [os.path.join(ROOT, "bench.py"), "--mode", "sharded", "--steps", "6", "--warmup", "2",
             "--no-secondary", "--no-cpu-baseline"]
     if launcher == "torchrun":
@@ -96,3 +101,38 @@ def test_bench_sharded_failure_falls_back_to_replicas():
     d = json.loads(lines[0])
     assert d["config"]["parallelism"] == "replicas2"
     assert "injected" in d["sharded_error"] and d["value"] > 1e10
+
+
+def test_bench_sharded_one_rank_failure_falls_back_together():
+    """A failure on ONE rank after the exchange regions are set up (as a peer
+    GPU that cannot be mapped would raise in slam_dist_connect): the ranks meet
+    at the same agreement point, fall back to replicas together, and the line
+    names the phase and the failing rank."""
+    args = [os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "6", "--warmup", "2",
+            "--no-secondary", "--no-cpu-baseline"]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", "29547"] + args
+    env = dict(os.environ, SLAM_BENCH_SHARE_GPU="1", SLAM_BENCH_FAIL_SHARDED_RANK="1")
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["config"]["parallelism"] == "replicas2"
+    assert d["sharded_error"].startswith("connect") and "rank 1" in d["sharded_error"]
+
+
+def test_bench_strong_scaling_mode():
+    """--total-particles: one filter of T particles over the ranks (here two
+    ranks on one GPU, T = 2^21: 2^20 per rank), scaling 'strong'."""
+    args = [os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "6", "--warmup", "2",
+            "--no-secondary", "--no-cpu-baseline", "--total-particles", str(1 << 21)]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", "29549"] + args
+    env = dict(os.environ, SLAM_BENCH_SHARE_GPU="1")
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])
+    assert d["scaling"] == "strong" and d["config"]["particles_total"] == 1 << 21
+    assert d["config"]["particles_per_gpu"] == 1 << 20
+    assert abs(d["value"] - (1 << 21) * 100 / (d["ms_per_step"] / 1e3)) <= 1e-6 * d["value"]
