@@ -174,12 +174,12 @@ int make_lik_const(slam_pf* h) {
     lc.fast_min_l = climb > 700.0 ? std::numeric_limits<double>::infinity()
                                   : lc.normal_min_l + climb;
     // closed form: the fp64 expansion while its rounding bound 11 u V stays
-    // within |dL| <= 1e-13 (dL = dF / (2 sx2), 1 % of the 1e-12 parity bar):
-    // V rsx2 <= 160; SLAM_PF_EXPAND_VMAX=<factor> scales the
-    // bound (0: double-double only)
+    // within |dL| <= 3e-13 (dL = dF / (2 sx2), under a third of the 1e-12
+    // parity bar): V rsx2 <= 480; SLAM_PF_EXPAND_VMAX=<factor>
+    // scales the bound (0: double-double only)
     const char* ve = std::getenv("SLAM_PF_EXPAND_VMAX");
     const double vf = ve ? std::atof(ve) : 1.0;
-    lc.expand_vmax = vf * 160.0 * lc.sx2;
+    lc.expand_vmax = vf * 480.0 * lc.sx2;
     return SLAM_OK;
 }
 
@@ -396,7 +396,7 @@ int launch_reduce(slam_pf* h, int32_t resampled_known) {
         finalize_deferred_kernel<<<1, kFinThreads, 0, s>>>(
             n, h->dp, h->w_un, h->s_cur, h->tail_leaves, h->tail_ops, h->n_tail_leaves,
             h->n_tail_ops, h->x[c], h->y[c], h->th[c], h->refp, h->flags, h->cfg.ess_threshold,
-            step_io(h), resampled_known, h->pc.np_recip, h->boff, h->lm, h->lc, h->pc.dt);
+            step_io(h), resampled_known, h->pc.np_recip, h->boff);
         toc(h, 1);
         SLAM_HIP_TRY(hipGetLastError());
         return SLAM_OK;
@@ -646,8 +646,8 @@ int create_impl(const slam_pf_config* cfg, int64_t n_local, int64_t n_global, in
     A(h->bp, h->nb_norm);
     A(h->wsum, 1);
     // [0..2] last estimate, [4..6] the one before, [7] moves of the first
-    // expansion reference, [8..10] last weighted mean pose, [12..14] the one before
-    A(h->refp, 16);
+    // expansion reference (closed_prep_reference)
+    A(h->refp, 8);
     A(h->flags, kFlagWords);
     A(h->tk, 4 * kTicketWords);
     A(h->lm, 2 * std::max<int32_t>(n_landmarks, 1));
@@ -681,9 +681,8 @@ int create_impl(const slam_pf_config* cfg, int64_t n_local, int64_t n_global, in
     const double one = 1.0;
     SLAM_HIP_TRY(hipMemcpy(h->s_cur, &one, sizeof(double), hipMemcpyHostToDevice));
     {
-        const double rp[16] = {cfg->x0[0], cfg->x0[1], cfg->x0[2], 0.0, cfg->x0[0], cfg->x0[1],
-                               cfg->x0[2], 1.0, cfg->x0[0], cfg->x0[1], cfg->x0[2], 0.0,
-                               cfg->x0[0], cfg->x0[1], cfg->x0[2], 0.0};
+        const double rp[8] = {cfg->x0[0], cfg->x0[1], cfg->x0[2], 0.0,
+                               cfg->x0[0], cfg->x0[1], cfg->x0[2], 1.0};
         SLAM_HIP_TRY(hipMemcpy(h->refp, rp, sizeof(rp), hipMemcpyHostToDevice));
     }
     SLAM_HIP_TRY(hipMemset(h->flags, 0, kFlagWords * sizeof(int32_t)));

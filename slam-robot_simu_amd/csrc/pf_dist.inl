@@ -1396,34 +1396,15 @@ __global__ __launch_bounds__(kFinThreads) void dist_reduce_kernel(
     const double* __restrict__ ys, const double* __restrict__ ts, double* __restrict__ s_cur,
     double* __restrict__ refp, int32_t* __restrict__ flags, const double ess_th, StepIO io,
     const double np_recip, double* __restrict__ boff, DistScratch* __restrict__ scr,
-    const DistPeers P, const double* __restrict__ lm, const LikConst lc, const double dt) {
+    const DistPeers P) {
     __shared__ double sh[2048];                             // buffer partials (nch <= 2048)
-    __shared__ double s_prep[16];                           // the next step's closed-form sums
     const uint64_t epoch = dist_epoch(io);
     PROBE_AT(27);
-    // the next step's closed-form words (as finalize_deferred_kernel): its sums
-    // here, its expansion about this step's refp (read before the finalize
-    // replaces it) by the last wave before the global fold
-    const int32_t st_now = io.ctr[0];
-    const bool prep = FINALIZE && lc.closed && st_now + 1 < io.cap;
-    double prep_rp[3];
-    if (prep) {
-        closed_prep_sums(lm, io.z + (size_t)(st_now + 1) * 2 * lc.nl, lc.nl,
-                         (int)(threadIdx.x >> 6), kFinWaves, s_prep);
-        for (int k = 0; k < 3; ++k) prep_rp[k] = refp[8 + k];     // the mean pose (write_result)
-    }
     if (RECORD)
         dist_record(n, dp, w_un, tail_leaves, tail_ops, n_tail_leaves, n_tail_ops, xs, ys, ts, P,
                     epoch, sh);
     if (FINALIZE) {
-        __syncthreads();
-        if (prep && threadIdx.x == kFinThreads - 64) {
-            const int32_t sn = st_now + 1;
-            double px, py, pth;
-            closed_prep_reference(prep_rp, 2, io.ctl[2 * sn], io.ctl[2 * sn + 1], dt, io.motion, px,
-                                  py, pth);
-            closed_prep_constants(s_prep, lc.nl, px, py, pth, io.zc + (size_t)sn * kZcWords);
-        }
+        if (RECORD) __syncthreads();
         dist_finalize(n, dp, s_cur, refp, flags, ess_th, io, np_recip, boff, scr, P, epoch, sh);
         PROBE_AT(31);
     }

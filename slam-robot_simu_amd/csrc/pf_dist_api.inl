@@ -115,7 +115,7 @@ int dist_enqueue_step(slam_dist* d) {
         kern<<<1, kFinThreads, 0, h->stream>>>(
             h->n, h->dp, h->w_un, h->tail_leaves, h->tail_ops, h->n_tail_leaves, h->n_tail_ops,
             h->x[c], h->y[c], h->th[c], h->s_cur, h->refp, h->flags, h->cfg.ess_threshold,
-            step_io(h), h->pc.np_recip, h->boff, d->scr[i], d->peers[i], h->lm, h->lc, h->pc.dt);
+            step_io(h), h->pc.np_recip, h->boff, d->scr[i], d->peers[i]);
     };
     if (m == 1) {                                         // record + push, wait, global finalize
         reduce(0, dist_reduce_kernel<true, true>);

@@ -62,10 +62,8 @@ __global__ __launch_bounds__(kFinThreads) void finalize_deferred_kernel(
     const int32_t* __restrict__ tail_ops, const int32_t n_tail_leaves, const int32_t n_tail_ops,
     const double* __restrict__ xs, const double* __restrict__ ys, const double* __restrict__ ts,
     double* __restrict__ refp, int32_t* __restrict__ flags, const double ess_th, StepIO io,
-    const int32_t resampled_known, const double np_recip, double* __restrict__ boff,
-    const double* __restrict__ lm, const LikConst lc, const double dt) {
+    const int32_t resampled_known, const double np_recip, double* __restrict__ boff) {
     __shared__ double sh[2048];                      // buffer sums / tail leaves / block totals
-    __shared__ double s_prep[16];                    // the next step's closed-form sums
     __shared__ double s_q[11][kFinThreads];
     __shared__ BlockPartial shp[kFinWaves];
     __shared__ double s_wmax[kFinWaves];
@@ -108,17 +106,6 @@ __global__ __launch_bounds__(kFinThreads) void finalize_deferred_kernel(
 #pragma unroll
         for (int j = 0; j < 4; ++j) L[j] = Lp[j];
     }
-    // ---- the next step's closed-form words (StepIO.zc), while the
-    // loads are in flight: its eight sums here (one per wave), its expansion
-    // about the estimate two steps back from it (this step's refp, read before
-    // write_result_xe replaces it) by the last wave after the np.sum barrier
-    const int32_t st_now = io.ctr[0];
-    const bool prep = lc.closed && st_now + 1 < io.cap;
-    if (prep)
-        closed_prep_sums(lm, io.z + (size_t)(st_now + 1) * 2 * lc.nl, lc.nl, wave, kFinWaves, s_prep);
-    double prep_rp[3];
-#pragma unroll
-    for (int k = 0; k < 3; ++k) prep_rp[k] = refp[8 + k];     // the mean pose (write_result)
     // ---- lane partial sums scaled to the lane's max (rescaled to the global
     // max once that is known); q dies here except the totals q[k][0]
     double mlane = -1.0;
@@ -194,11 +181,6 @@ __global__ __launch_bounds__(kFinThreads) void finalize_deferred_kernel(
         if (nfull > 0)
             for (int k = 0; k < last_cnt; ++k) s = s + sh[k];
         __builtin_amdgcn_s_setprio(0);
-    } else if (prep && tid == kFinThreads - 64) {
-        const int32_t sn = st_now + 1;
-        double px, py, pth;
-        closed_prep_reference(prep_rp, 2, io.ctl[2 * sn], io.ctl[2 * sn + 1], dt, io.motion, px, py, pth);
-        closed_prep_constants(s_prep, lc.nl, px, py, pth, io.zc + (size_t)sn * kZcWords);
     }
     {
         const double rl = (mlane > 0.0 && M > 0.0) ? mlane / M : 0.0;

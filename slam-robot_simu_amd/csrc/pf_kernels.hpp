@@ -15,14 +15,12 @@ constexpr int kMotionNone = 2;     // internal: likelihood-only pass
 //  * the expansion about the step's reference pose (p^, c^, s^): F^ = the
 //    exact sum of squared residuals at it, A, B (gradient in the rotation)
 //    and L2 (landmark second moment about p^) as double-doubles (hi, lo),
-//    S_r (residual sum) and L1 (landmark sum about p^) rounded, and the
-//    coefficients K3..K5 of the per-particle rounding bound.
+//    S_r (residual sum) and L1 (landmark sum about p^) rounded.
 enum : int {
     kZcSum = 0,
     kZcPx = 16, kZcPy, kZcC, kZcS,
     kZcFh, kZcFl, kZcA, kZcAl, kZcB, kZcBl, kZcL2, kZcL2l,
     kZcSrx, kZcSry, kZcL1x, kZcL1y,
-    kZcK1, kZcK2, kZcK3, kZcK4, kZcK5,
     kZcWords = 40,
 };
 constexpr int kClosedWords = kZcWords;

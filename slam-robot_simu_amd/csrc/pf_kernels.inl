@@ -454,13 +454,13 @@ __device__ void closed_prep_sums(const double* __restrict__ lm, const double* __
     }
 }
 
-// The expansion's reference pose for a step: the weighted mean pose two steps
-// back (rp: x, y, th; refp[12..14] at the step's start, refp[8..10] at the
-// previous step's end) moved `moves` times by the step's control, noise free
-// (motion_model.py:64-86 / particle_filter.py:129-140): twice, or once for the
-// first step after the handle's creation (refp[7] = 1: the initial pose is the
-// particles' state before that step's predict).  Any finite pose gives exact
-// constants; a close one keeps every particle on the fp64 expansion.
+// The expansion's reference pose for a step: the estimate two steps back (rp:
+// x, y, th; refp[4..6] at the step's start, refp[0..2] at the previous step's
+// end) moved `moves` times by the step's control, noise free (motion_model.py
+// :64-86 / particle_filter.py:129-140): twice, or once for the first step after
+// the handle's creation (refp[7] = 1: the initial pose is the particles' state
+// before that step's predict).  Any finite pose gives exact constants; a close
+// one keeps every particle on the fp64 expansion.
 __device__ void closed_prep_reference(const double* rp, const int moves, const double v,
                                       const double om, const double dt, const int motion,
                                       double& px, double& py, double& pth) {
@@ -493,7 +493,7 @@ __device__ void closed_prep_reference(const double* rp, const int moves, const d
 //   A = c^ L2 - D^,  B = s^ L2 - E^,  S_r = R^ L1 - S_z,
 //   F^ = (c^^2 + s^^2) L2 - 2 (c^ D^ + s^ E^) + S_zz
 // (F^ = sum_j |R^(l_j - p^) - z_j|^2, A = sum r^.l^, B = sum r^ x l^), then
-// rounded (F^ kept as a double-double).
+// rounded (F^, A, B, L2 kept as double-doubles).
 __device__ void closed_prep_constants(const double* sdd, const int32_t nl, const double px,
                                       const double py, const double pth, double* __restrict__ zc) {
     double sh, ch;
@@ -532,17 +532,10 @@ __device__ void closed_prep_constants(const double* sdd, const int32_t nl, const
     zc[kZcL2l] = L2.l;
     zc[kZcL1x] = L1x.h;
     zc[kZcL1y] = L1y.h;
-    // bound coefficients (likelihood_lanes): K3..K5 weigh the fp64 terms,
-    // K1, K2 the rounding of dc, ds when they are not exact (weight 1/11)
-    zc[kZcK1] = 2.0 * (fabs(A.h) + fabs(B.h)) / 11.0;
-    zc[kZcK2] = 2.0 * L2.h / 11.0;
-    zc[kZcK3] = 2.0 * (fabs(L1x.h) + fabs(L1y.h));
-    zc[kZcK4] = 2.0 * (fabs(Srx.h) + fabs(Sry.h));
-    zc[kZcK5] = fnl;
 }
 
-// Both parts by one block (prestep / observation kernels): refp[12..14] = the
-// mean pose two steps back, refp[7] the moves from it (2; 1 after creation),
+// Both parts by one block (prestep / observation kernels): refp[4..6] = the
+// estimate two steps back, refp[7] the moves from it (2; 1 after creation),
 // (v, om) the step's control.
 __device__ void closed_prep_block(const double* __restrict__ lm, const double* __restrict__ z,
                                   const int32_t nl, const double* refp, const double v,
@@ -553,7 +546,7 @@ __device__ void closed_prep_block(const double* __restrict__ lm, const double* _
     __syncthreads();
     if (threadIdx.x == 0) {
         double px, py, pth;
-        closed_prep_reference(refp + 12, refp[7] == 1.0 ? 1 : 2, v, om, dt, motion, px, py, pth);
+        closed_prep_reference(refp + 4, refp[7] == 1.0 ? 1 : 2, v, om, dt, motion, px, py, pth);
         closed_prep_constants(sdd, nl, px, py, pth, zc);
     }
 }
@@ -718,12 +711,12 @@ __device__ __forceinline__ int likelihood_lanes(const double* xn, const double* 
         //          - 2 S_r.(u, v) - 2 (dR L1).(u, v) + NL (u^2 + v^2),  dR = [[dc, -ds], [ds, dc]]
         // (DESIGN 4.3).  The rotation terms, which carry the cloud's heading
         // spread (|dc A| and dc^2 L2 reach ~10 while F ~ NL sx2), are formed to
-        // ~u^2 from double-double A, B, L2 (exact products, TwoSum) and summed
-        // with F^ in double-double; dc, ds are exact when c, c^ (s, s^) are
-        // within a factor 2 (Sterbenz), else off by u|dc|; the remaining
-        // terms round in fp64.  All of it stays within 11 u V,
-        //   V = b (a K3 + K4 + b K5) + a (K1 + a K2),  a = |dc| + |ds|, b = |u| + |v|,
-        // so V <= expand_vmax keeps |dL| <= 1e-13.  Beyond it (a particle far from the reference pose) the
+        // ~u^2 from double-double dc, ds (TwoSum) and A, B, L2 (exact products,
+        // TwoSum) and summed with F^ in double-double; the translation terms
+        // round in fp64 within 11 u V, V = 2 (|gx u| + |gy v| + |Srx u| +
+        // |Sry v|) + t5 their magnitudes, so V <= expand_vmax keeps |dL| <=
+        // 3e-13 (the worst case; the measured difference to the double-double
+        // form is ~1e-14).  Beyond it (a particle far from the reference pose) the
         // double-double form of the same sum from the eight sums.  Either way
         // the exact value of the sum for the particle's rounded c, s up to that
         // bound and one final rounding: the difference to the reference is its
@@ -735,8 +728,6 @@ __device__ __forceinline__ int likelihood_lanes(const double* xn, const double* 
         const double L2h = zc[kZcL2], L2l = zc[kZcL2l];
         const double Srx = zc[kZcSrx], Sry = zc[kZcSry];
         const double L1x = zc[kZcL1x], L1y = zc[kZcL1y];
-        const double K1 = zc[kZcK1], K2 = zc[kZcK2], K3 = zc[kZcK3], K4 = zc[kZcK4];
-        const double K5 = zc[kZcK5];
         bool dd[P];
         int any_dd = 0;
 #pragma unroll
@@ -744,6 +735,9 @@ __device__ __forceinline__ int likelihood_lanes(const double* xn, const double* 
             const double c = cp[k], sn = sp[k];
             const double dx = xn[k] - phx, dy = yn[k] - phy;
             const double dc = c - chh, ds = sn - shh;
+            const double dcb = dc - c, dsb = ds - sn;                       // TwoSum errors of dc, ds
+            const double dce = (c - (dc - dcb)) + (-chh - dcb);
+            const double dse = (sn - (ds - dsb)) + (-shh - dsb);
             // rotation terms to ~u^2: 2 t1 = 2 (dc A + ds B), t3 = (dc^2 + ds^2) L2
             const double p1 = dc * Ah, e1 = fma(dc, Ah, -p1);
             const double p2 = ds * Bh, e2 = fma(ds, Bh, -p2);
@@ -753,7 +747,9 @@ __device__ __forceinline__ int likelihood_lanes(const double* xn, const double* 
             const double a2b = a2 - q1;
             const double a2e = ((q1 - (a2 - a2b)) + (q2 - a2b)) + (f1 + f2);
             const double p3 = a2 * L2h;
-            const double e3 = fma(a2, L2h, -p3) + fma(a2e, L2h, a2 * L2l);
+            // + the low parts of dc, ds: 2 (dce dc + dse ds) in t3, (dce A + dse B) in t1
+            const double a2x = a2e + 2.0 * fma(dce, dc, dse * ds);
+            const double e3 = fma(a2, L2h, -p3) + fma(a2x, L2h, a2 * L2l);
             // translation terms in fp64: t2 = S_r . R d, t4 = dR L1 . R d, t5 = NL |R d|^2
             const double u = fma(c, dx, -(sn * dy));
             const double v = fma(sn, dx, c * dy);
@@ -778,11 +774,11 @@ __device__ __forceinline__ int likelihood_lanes(const double* xn, const double* 
                 lo += (h - (t - bb)) + (p3 - bb);
                 h = t;
             }
-            const double rot_lo = fma(2.0, (e1 + e2) + fma(dc, Al, ds * Bl), e3);
+            const double rot_lo =
+                fma(2.0, (e1 + e2) + (fma(dc, Al, ds * Bl) + fma(dce, Ah, dse * Bh)), e3);
             lo = lo + ((Fl + rot_lo) + (fma(-2.0, t2 + t4, t5)));
             const double F = h + lo;
-            const double a = fabs(dc) + fabs(ds), b = fabs(u) + fabs(v);
-            const double V = fma(b, fma(a, K3, fma(b, K5, K4)), a * fma(a, K2, K1));
+            const double V = fma(2.0, fma(fabs(u), fabs(gx) + fabs(Srx), fabs(v) * (fabs(gy) + fabs(Sry))), t5);
             dd[k] = !(V <= lc.expand_vmax);                                  // also NaN
             any_dd |= dd[k] ? 1 : 0;
             L[k] = nl ? fma(-0.5, F * lc.rsx2, lc.neg_nl_ln_den) : lc.neg_nl_ln_den;
@@ -1147,6 +1143,23 @@ __global__ __launch_bounds__(256) SLAM_FUSED_ATTR void pf_fused_kernel(
 #ifndef SLAM_NO_EPILOGUE
         defer_epilogue(base, n, wv, xv, yv, tv, refp, dp, wave_s);
 #endif
+        // block 0, after its own particles: the NEXT step's closed-form words
+        // (StepIO.zc) -- its eight sums (two per wave) and its
+        // expansion about this step's refp (the estimate two steps before it)
+        // moved twice.  Off the step's critical path: the next launch reads
+        // them; a step staged by the host is prepared again by its prestep.
+        if (MOTION != kMotionNone && lc.closed && blockIdx.x == 0 && st + 1 < io.cap) {
+            __shared__ double s_prep[16];
+            const int32_t sn = st + 1;
+            closed_prep_sums(lm, io.z + (size_t)sn * 2 * lc.nl, lc.nl, wave_s, 4, s_prep);
+            __syncthreads();
+            if (threadIdx.x == 0) {
+                double px, py, pth;
+                closed_prep_reference(refp, 2, io.ctl[2 * sn], io.ctl[2 * sn + 1], pc.dt, io.motion,
+                                      px, py, pth);
+                closed_prep_constants(s_prep, lc.nl, px, py, pth, io.zc + (size_t)sn * kZcWords);
+            }
+        }
     } else if (valid[0]) {
         w_un[i0] = wv[0];
     }
@@ -1451,13 +1464,10 @@ __device__ void write_result(const BlockPartial& r, const double* xs, const doub
     flags[kFlagResample] = o.resample_next;
     flags[kFlagMarkGen] = flags[kFlagMarkGen] + 1;
     flags[kFlagStatus] = 0;
-    // the weighted mean pose (the moments' origin is the old refp), kept two
-    // steps deep as the expansion's reference (closed_prep_reference): the
-    // centre of the cloud the next steps' particles are resampled from
+    // the estimate, kept two steps deep as the expansion's reference
+    // (closed_prep_reference: the argmax particle is the same bits however
+    // the filter is sharded, which a summed mean would not be)
     for (int k = 0; k < 3; ++k) {
-        const double m = refp[k] + mu[k];
-        refp[12 + k] = refp[8 + k];
-        refp[8 + k] = isfinite(m) ? m : o.x_est[k];
         refp[4 + k] = refp[k];
         refp[k] = o.x_est[k];
     }
@@ -1493,13 +1503,10 @@ __device__ void write_result_xe(const BlockPartial& r, const double* xe, double*
     flags[kFlagResample] = o.resample_next;
     flags[kFlagMarkGen] = flags[kFlagMarkGen] + 1;
     flags[kFlagStatus] = 0;
-    // the weighted mean pose (the moments' origin is the old refp), kept two
-    // steps deep as the expansion's reference (closed_prep_reference): the
-    // centre of the cloud the next steps' particles are resampled from
+    // the estimate, kept two steps deep as the expansion's reference
+    // (closed_prep_reference: the argmax particle is the same bits however
+    // the filter is sharded, which a summed mean would not be)
     for (int k = 0; k < 3; ++k) {
-        const double m = refp[k] + mu[k];
-        refp[12 + k] = refp[8 + k];
-        refp[8 + k] = isfinite(m) ? m : o.x_est[k];
         refp[4 + k] = refp[k];
         refp[k] = o.x_est[k];
     }

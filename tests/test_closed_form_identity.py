@@ -8,12 +8,12 @@ rational arithmetic,
     from those sums reproduce the same sum through the per-particle polynomial
     F^ + 2 (dc A + ds B) - 2 S_r.R d + (dc^2 + ds^2) L2 - 2 (dR L1).R d + NL |R d|^2
     -- the fp64 fast form;
-  * V = b (a K3 + K4 + b K5) + a (K1 + a K2) bounds the magnitudes the kernel's
-    fp64 part rounds (its rounding bound is 11 u V; the rotation terms are
-    formed in double-double, their inputs dc, ds round by at most u);
+  * V = 2 (|gx u| + |gy v| + |Srx u| + |Sry v|) + t5 bounds the magnitudes the
+    kernel's fp64 part rounds (its rounding bound is 11 u V; the rotation terms
+    are formed in double-double, dc and ds with their TwoSum errors);
   * the kernel's own fp64 operation order stays within u |F| + 11 u V of the
     exact sum for a bench-like cloud, and such a cloud passes the fast-form
-    test V / sx2 <= 160.
+    test V / sx2 <= 480.
 
 No GPU: this pins the identities the kernel evaluates, independent of rounding.
 """
@@ -67,9 +67,7 @@ def _constants(S, nl, px, py, ch, sh):
     Srx = ch * L1x - sh * L1y - S["zx"]
     Sry = sh * L1x + ch * L1y - S["zy"]
     F = (ch * ch + sh * sh) * L2 - 2 * (Dh * ch + Eh * sh) + S["zz"]
-    return dict(F=F, A=A, B=B, Srx=Srx, Sry=Sry, L2=L2, L1x=L1x, L1y=L1y,
-                K1=2 * (abs(A) + abs(B)) / 11, K2=2 * L2 / 11, K3=2 * (abs(L1x) + abs(L1y)),
-                K4=2 * (abs(Srx) + abs(Sry)), K5=Fr(nl))
+    return dict(F=F, A=A, B=B, Srx=Srx, Sry=Sry, L2=L2, L1x=L1x, L1y=L1y, NL=Fr(nl))
 
 
 def _expansion(K, px, py, ch, sh, x, y, c, s):
@@ -81,14 +79,13 @@ def _expansion(K, px, py, ch, sh, x, y, c, s):
     gx, gy = dc * K["L1x"] - ds * K["L1y"], ds * K["L1x"] + dc * K["L1y"]
     t4 = gx * u + gy * v
     t3 = (dc * dc + ds * ds) * K["L2"]
-    t5 = (u * u + v * v) * K["K5"]
+    t5 = (u * u + v * v) * K["NL"]
     F = K["F"] + 2 * t1 - 2 * t2 + t3 - 2 * t4 + t5
-    # magnitudes the fp64 part rounds: the translation terms, and (weight
-    # 1/11: only their inputs dc, ds may round) the rotation terms
+    # magnitudes the fp64 part rounds: the translation terms (the rotation
+    # terms are formed in double-double)
     mags = (2 * abs(K["Srx"] * u) + 2 * abs(K["Sry"] * v) + 2 * abs(gx * u) + 2 * abs(gy * v)
-            + abs(t5) + (2 * abs(dc * K["A"]) + 2 * abs(ds * K["B"]) + 2 * abs(t3)) / 11)
-    a, b = abs(dc) + abs(ds), abs(u) + abs(v)
-    V = b * (a * K["K3"] + K["K4"] + b * K["K5"]) + a * (K["K1"] + a * K["K2"])
+            + abs(t5))
+    V = 2 * (abs(u) * (abs(gx) + abs(K["Srx"])) + abs(v) * (abs(gy) + abs(K["Sry"]))) + t5
     return F, mags, V
 
 
@@ -136,6 +133,9 @@ def _kernel_fast_form(Kd, K, x, y, c, s, nl):
     product + one rounding): returns (F, V)."""
     dx, dy = x - Kd["px"], y - Kd["py"]
     dc, ds = c - Kd["ch"], s - Kd["sh"]
+    dcb, dsb = dc - c, ds - s
+    dce = (c - (dc - dcb)) + (-Kd["ch"] - dcb)
+    dse = (s - (ds - dsb)) + (-Kd["sh"] - dsb)
     Ah, Al = K["Ah"], K["Al"]
     Bh, Bl = K["Bh"], K["Bl"]
     L2h, L2l = K["L2h"], K["L2l"]
@@ -151,7 +151,8 @@ def _kernel_fast_form(Kd, K, x, y, c, s, nl):
     a2b = a2 - q1
     a2e = ((q1 - (a2 - a2b)) + (q2 - a2b)) + (f1 + f2)
     p3 = a2 * L2h
-    e3 = _fma(a2, L2h, -p3) + _fma(a2e, L2h, a2 * L2l)
+    a2x = a2e + 2.0 * _fma(dce, dc, dse * ds)
+    e3 = _fma(a2, L2h, -p3) + _fma(a2x, L2h, a2 * L2l)
     u = _fma(c, dx, -(s * dy))
     v = _fma(s, dx, c * dy)
     t2 = _fma(Kd["Srx"], u, Kd["Sry"] * v)
@@ -163,11 +164,10 @@ def _kernel_fast_form(Kd, K, x, y, c, s, nl):
     lo += l2
     h, l3 = _two_sum(h, p3)
     lo += l3
-    rot_lo = _fma(2.0, (e1 + e2) + _fma(dc, Al, ds * Bl), e3)
+    rot_lo = _fma(2.0, (e1 + e2) + (_fma(dc, Al, ds * Bl) + _fma(dce, Ah, dse * Bh)), e3)
     lo = lo + ((K["Fl"] + rot_lo) + _fma(-2.0, t2 + t4, t5))
     F = h + lo
-    a, b = abs(dc) + abs(ds), abs(u) + abs(v)
-    V = _fma(b, _fma(a, Kd["K3"], _fma(b, Kd["K5"], Kd["K4"])), a * _fma(a, Kd["K2"], Kd["K1"]))
+    V = _fma(2.0, _fma(abs(u), abs(gx) + abs(Kd["Srx"]), abs(v) * (abs(gy) + abs(Kd["Sry"]))), t5)
     return F, V
 
 
@@ -180,7 +180,7 @@ def test_expansion_rounding_within_bound_for_a_cloud():
     """The kernel's fp64 evaluation of the expansion, for a cloud with the
     bench's per-step spread around the reference pose (velocity model,
     a1..a6 = 0.1 at v = 1.75 m/s: ~1 cm, ~0.013 rad), stays within
-    u |F| + 11 u V of the exact sum, and V sx2^-1 <= 160 (the kernel's
+    u |F| + 11 u V of the exact sum, and V sx2^-1 <= 480 (the kernel's
     fast-form test) for the cloud."""
     rs = np.random.RandomState(5)
     nl = 100
@@ -202,11 +202,11 @@ def test_expansion_rounding_within_bound_for_a_cloud():
     u53 = 2.0 ** -53
     vs = []
     for _ in range(40):
-        x, y = pose[0] + 0.01 * rs.randn(), pose[1] + 0.01 * rs.randn()
-        th = pose[2] + 0.013 * rs.randn()
+        x, y = pose[0] + 0.017 * rs.randn(), pose[1] + 0.017 * rs.randn()
+        th = pose[2] + 0.022 * rs.randn()
         c, s = np.cos(np.pi / 2 - th), np.sin(np.pi / 2 - th)
         F, V = _kernel_fast_form(Kd, Kx, x, y, c, s, nl)
         exact = _direct(lm, z, _fr(x), _fr(y), _fr(c), _fr(s))
         assert abs(Fr(F) - exact) <= Fr(u53) * abs(exact) + Fr(11 * u53) * Fr(V)
         vs.append(V / 0.09)
-    assert max(vs) <= 160.0, max(vs)
+    assert max(vs) <= 480.0, max(vs)

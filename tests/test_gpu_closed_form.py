@@ -91,7 +91,7 @@ def test_expansion_matches_double_double_near_reference(nl, n, spread):
 
 def test_far_particles_fall_back_bit_identical():
     rs = np.random.RandomState(3)
-    p, lm, z, px, pw = _world(rs, 30, 3000, 0.05, np.array([[0.6], [-0.4], [0.05]]))
+    p, lm, z, px, pw = _world(rs, 30, 3000, 0.2, np.array([[3.0], [-2.0], [0.3]]))
     _, wf = _update(px, pw, lm, z, "1")
     _, wd = _update(px, pw, lm, z, "0")
     assert np.array_equal(wf, wd)

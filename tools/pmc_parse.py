@@ -59,20 +59,32 @@ def main(src, tag):
     os.makedirs("profiles", exist_ok=True)
     with open(f"profiles/{tag}_pmc.json", "w") as f:
         json.dump(out, f, indent=1, sort_keys=True)
+    def summary(key):
+        v = out[key]
+        rec = {k: v[k] for k in ("fp64_flops", "SQ_INSTS_VALU", "SQ_WAVES", "avg_dur_us_profiled",
+                                 "valu_insts_per_wave", "SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES",
+                                 "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY",
+                                 "GRBM_GUI_ACTIVE") if k in v}
+        if "hbm_read_bytes" in v and "hbm_write_bytes" in v:
+            rec["hbm_bytes"] = v["hbm_read_bytes"] + v["hbm_write_bytes"]
+        return rec
+
     key = "pf_fused_kernel<1, 1, false, true>"       # the bench's kernel (velocity, log-sum)
     if key in out and "hbm_read_bytes" in out[key] and "hbm_write_bytes" in out[key]:
-        v = out[key]
-        traffic = v["hbm_read_bytes"] + v["hbm_write_bytes"]
-        extra = {k: v[k] for k in ("fp64_flops", "SQ_INSTS_VALU", "SQ_WAVES", "avg_dur_us_profiled")
-                 if k in v}
+        main_rec = summary(key)
+        kernels = {}
+        pkey = "pf_fused_kernel<1, 0, false, true>"  # the reference-literal product mode
+        if pkey in out:
+            kernels["product"] = summary(pkey)
         sys.path.insert(0, os.getcwd())
         from bench import pf_sources_sha
         with open("profiles/pmc_traffic.json", "w") as f:
             json.dump({"source": f"profiles/{tag}_pmc.json", "kernel": key,
-                       "fused_kernel_hbm_bytes_per_launch": traffic,
+                       "fused_kernel_hbm_bytes_per_launch": main_rec.get("hbm_bytes"),
                        "sources_sha": pf_sources_sha(),
-                       "fused_kernel": extra,
-                       "note": "FETCH_SIZE x2 (gfx950 half-count) + WRITE_SIZE, KB -> B, mean over launches"},
+                       "fused_kernel": main_rec, "kernels": kernels,
+                       "note": "FETCH_SIZE x2 (gfx950 half-count) + WRITE_SIZE, KB -> B, mean over "
+                               "launches; fp64_flops = 64 x (ADD + MUL + TRANS + 2 FMA)_F64"},
                       f, indent=1)
     for k, v in sorted(out.items()):
         print(f"{k:45s} rd {v.get('hbm_read_bytes', 0)/1e6:8.2f} MB  wr {v.get('hbm_write_bytes', 0)/1e6:7.2f} MB"
