@@ -338,7 +338,17 @@ typedef struct {
     double pcg_tol;       /* PCG: relative residual */
     int32_t pcg_max_iter;
     int32_t solver;       /* SLAM_GRAPH_* */
+    double cond_tol;      /* PCG path, cond estimate: a side stops when its Ritz value moved
+                             less than cond_tol (relative) over 16 iterations (<= 0: 1e-5) */
+    int32_t cond_max_iter;  /* estimate iterations cap (<= 0: 3000) */
+    int32_t cond_mode;    /* SLAM_GRAPH_COND_* */
 } slam_graph_config;
+
+/* The PCG path's cond (:495): SLAM_GRAPH_COND_ESTIMATE (default) estimates the
+ * extreme eigenvalues of H by LOBPCG on a second stream beside the solve and
+ * applies the reference's `cond < cond_max`; SLAM_GRAPH_COND_OFF skips it (cond
+ * NaN, the gate is the solve's convergence alone). */
+enum { SLAM_GRAPH_COND_ESTIMATE = 0, SLAM_GRAPH_COND_OFF = 1 };
 
 int slam_graph_create(const slam_graph_config* cfg, int device, slam_graph** out);
 int slam_graph_destroy(slam_graph* h);
@@ -349,10 +359,11 @@ int slam_graph_get_poses(slam_graph* h, double* poses);
 int slam_graph_set_edges(slam_graph* h, int64_t n_edges, const slam_graph_edge* edges);
 /* updateEstPose: linearise every edge at the current poses, assemble H and
  * b, gate, solve, update the poses.  stats[4] = {is_calc, sum delta^2, det,
- * cond} (:514).  On the PCG path det/cond are NaN and the reference's gate
- * (0.1 < det, cond < 1e15, :496) is not formed: is_calc = 1 means PCG
- * converged with positive curvature, 0 that it hit pcg_max_iter (poses
- * unchanged). */
+ * cond} (:514).  On the PCG path det is NaN (not formed at this size) and cond
+ * is the LOBPCG estimate lambda_max / lambda_min of H (inf when H is not
+ * positive definite; NaN with SLAM_GRAPH_COND_OFF): is_calc = 1 means PCG
+ * converged with positive curvature and cond < cond_max (:496), 0 that the
+ * gate rejected H or PCG hit pcg_max_iter (poses unchanged either way). */
 int slam_graph_update(slam_graph* h, double* stats);
 /* estimateOpticalTrajectory's loop: update until sum delta^2 < delta_sum_th
  * (:692-706) or max_iter; stats: max_iter x 4 (or NULL).  Returns
@@ -372,6 +383,11 @@ int slam_graph_get_delta(slam_graph* h, double* delta);
 /* Device time of the last update (ms): out[5] = {linearise, assemble, solve,
  * pose update, PCG iterations}. */
 int slam_graph_timing(slam_graph* h, double* out);
+/* The last PCG-path update's cond estimate: out[7] = {iterations, status (1
+ * converged, 2 stopped early: cond >= cond_max for certain, 3 cond_max_iter
+ * reached, 4 not positive definite), lambda_min, lambda_max, iterations of the
+ * min side, of the max side, device time (ms)}.  Zeros after a dense update. */
+int slam_graph_cond_info(slam_graph* h, double* out);
 /* HalfEdge (graph_based_slam.py:259-300) with its Observation (:20-75). */
 typedef struct {
     int64_t time, pose, landmark;

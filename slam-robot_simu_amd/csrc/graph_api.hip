@@ -48,6 +48,15 @@ struct slam_graph {
     double* q = nullptr;
     double* part = nullptr;
     PcgState* st = nullptr;
+    // condition-number estimate of the PCG path (second stream)
+    hipStream_t cstream = nullptr;
+    hipEvent_t cev[3] = {};        // [0] operands ready (main stream), [1]/[2] estimate start/end
+    double *cx = nullptr, *chx = nullptr, *cp = nullptr, *chp = nullptr;
+    double *cw = nullptr, *cw2 = nullptr, *chw = nullptr, *cpart = nullptr;
+    CondState* cst = nullptr;
+    bool cond_warm = false;        // cx holds the previous update's vectors of this edge set
+    int32_t cond_last_iters = 0;
+    double cond_info[7] = {0, 0, 0, 0, 0, 0, 0};
     hipEvent_t ev[5] = {};
     double last[5] = {0, 0, 0, 0, 0};
     int32_t pcg_last_iters = 0;    // iteration count of the previous PCG solve
@@ -135,6 +144,15 @@ int carve_edge_set(slam_graph* h, int64_t E, int64_t nt_ub, size_t tmp_bytes, Bu
         h->q = c.take<double>(n);
         h->part = c.take<double>(3 * (int64_t)nblk(n, kPcgThreads) + 3);
         h->st = c.take<PcgState>(1);
+        h->cx = c.take<double>(2 * n);
+        h->chx = c.take<double>(2 * n);
+        h->cp = c.take<double>(2 * n);
+        h->chp = c.take<double>(2 * n);
+        h->cw = c.take<double>(2 * n);
+        h->cw2 = c.take<double>(2 * n);
+        h->chw = c.take<double>(2 * n);
+        h->cpart = c.take<double>((2 * kCondGram + 2) * (int64_t)nblk(n, kPcgThreads) + 8);
+        h->cst = c.take<CondState>(1);
         h->luout = c.take<double>(8);
         if (bs) {
             bs->tl = c.take<int64_t>(2 * E);
@@ -183,6 +201,8 @@ int dense_buffers(slam_graph* h, int64_t n) {
 int finish_structure(slam_graph* h, int64_t E, int64_t nt, int64_t ns) {
     h->E = E;
     h->pcg_last_iters = 0;
+    h->cond_warm = false;
+    h->cond_last_iters = 0;
     h->nt = nt;
     h->n_slots = ns;
     const int64_t n = 3 * nt;
@@ -420,40 +440,140 @@ int solve_dense(slam_graph* h, double* stats, bool* solved) {
     return SLAM_OK;
 }
 
+// condition-number estimate (graph_kernels.inl: LOBPCG for the extreme
+// eigenvalues) on h->cstream, enqueued in batches of `count` iterations
+// starting at iteration k0 (k0 = 0: the start sequence first).
+int cond_enqueue(slam_graph* h, int32_t k0, int32_t count) {
+    const int64_t n = 3 * h->nt;
+    const unsigned nb = nblk(n, kPcgThreads);
+    hipStream_t s = h->cstream;
+    const double tol = h->cfg.cond_tol > 0.0 ? h->cfg.cond_tol : 1e-5;
+    const int32_t mx = h->cfg.cond_max_iter > 0 ? h->cfg.cond_max_iter : 3000;
+    int32_t k = k0;
+    if (k0 == 0) {
+        hipLaunchKernelGGL(graph_cond_init_kernel, dim3(nblk(2 * n)), dim3(256), 0, s, n,
+                           h->cond_warm ? 0 : 1, h->cx, h->cp, h->chp, h->cst);
+        hipLaunchKernelGGL(graph_cond_spmv_kernel<true>, dim3(nb), dim3(kSpmvThreads), 0, s, h->nt,
+                           h->rptr, h->scol, h->val, h->cx, h->chx, h->cw, h->cw2, h->chw, h->cp,
+                           h->chp, h->cpart, h->cst);
+        hipLaunchKernelGGL(graph_cond_fold_kernel, dim3(1), dim3(kCondFoldThreads), 0, s,
+                           (int64_t)nb, h->cpart, h->cst, 1);
+        hipLaunchKernelGGL(graph_cond_update_kernel, dim3(nb), dim3(kPcgThreads), 0, s, n, 0,
+                           h->minv, h->cx, h->chx, h->cw2, h->chw, h->cp, h->chp, h->cw, h->cpart,
+                           h->cst, tol, mx, h->cfg.cond_max);
+        k = 1;
+    }
+    for (; k < k0 + count; ++k) {
+        hipLaunchKernelGGL(graph_cond_spmv_kernel<false>, dim3(nb), dim3(kSpmvThreads), 0, s, h->nt,
+                           h->rptr, h->scol, h->val, h->cx, h->chx, h->cw, h->cw2, h->chw, h->cp,
+                           h->chp, h->cpart, h->cst);
+        hipLaunchKernelGGL(graph_cond_fold_kernel, dim3(1), dim3(kCondFoldThreads), 0, s,
+                           (int64_t)nb, h->cpart, h->cst, 0);
+        hipLaunchKernelGGL(graph_cond_update_kernel, dim3(nb), dim3(kPcgThreads), 0, s, n, k,
+                           h->minv, h->cx, h->chx, h->cw2, h->chw, h->cp, h->chp, h->cw, h->cpart,
+                           h->cst, tol, mx, h->cfg.cond_max);
+    }
+    SLAM_HIP_TRY(hipGetLastError());
+    return SLAM_OK;
+}
+
 // PCG on H delta = -b with block-Jacobi (large trajectories): two launches per
-// iteration, enqueued in chunks between host polls of the device state.
+// iteration, enqueued in chunks between host polls of the device state.  The
+// gate's condition number (:495) is estimated on a second stream at the same
+// time (cond_mode SLAM_GRAPH_COND_ESTIMATE); the solve is applied only if the
+// gate passes, as the reference inverts H only then (:496-497).
 int solve_pcg(slam_graph* h, double* stats, bool* solved, int32_t* iters) {
     const int64_t n = 3 * h->nt;
     const unsigned nb = nblk(n, kPcgThreads);
+    const bool est = (h->cfg.cond_mode == SLAM_GRAPH_COND_ESTIMATE);
     hipLaunchKernelGGL(graph_block_inv_kernel, dim3(nblk(h->nt)), dim3(256), 0, h->stream, h->nt,
                        h->dslot, h->val, h->minv);
+    if (est) {
+        SLAM_HIP_TRY(hipEventRecord(h->cev[0], h->stream));
+        SLAM_HIP_TRY(hipStreamWaitEvent(h->cstream, h->cev[0], 0));
+        SLAM_HIP_TRY(hipEventRecord(h->cev[1], h->cstream));
+    }
     hipLaunchKernelGGL(graph_pcg_start_kernel, dim3(nb), dim3(kPcgThreads), 0, h->stream, n,
                        h->minv, h->b, h->delta, h->r, h->z, h->part);
     SLAM_HIP_TRY(hipGetLastError());
     PcgState s{};
+    CondState cs{};
     // The first batch runs through the previous solve's iteration count (the
     // Gauss-Newton steps of one edge set converge in similar counts), so a
     // repeated solve usually needs a single host poll; then batches of 8.
     int32_t k_end = std::max<int32_t>(16, std::min<int32_t>(h->pcg_last_iters + 1, 1024));
-    for (int32_t k0 = 0;; k0 = k_end, k_end += 8) {
-        for (int32_t k = k0; k < k_end; ++k) {
-            hipLaunchKernelGGL(graph_pcg_dir_spmv_kernel, dim3(nb), dim3(kSpmvThreads), 0,
-                               h->stream, h->nt, k, h->rptr, h->scol, h->val, h->z, h->p, h->q,
-                               h->part, h->st, h->cfg.pcg_tol, h->cfg.pcg_max_iter);
-            hipLaunchKernelGGL(graph_pcg_step_kernel, dim3(nb), dim3(kPcgThreads), 0, h->stream,
-                               n, k, h->minv, h->p, h->q, h->delta, h->r, h->z, h->part, h->st);
+    int32_t c_end = std::max<int32_t>(kCondWin + 1, std::min<int32_t>(h->cond_last_iters + 1, 1024));
+    bool pcg_done = false, cond_done = !est, abandoned = false;
+    int32_t k0 = 0, c0 = 0;
+    while (!pcg_done || !cond_done) {
+        if (!pcg_done) {
+            for (int32_t k = k0; k < k_end; ++k) {
+                hipLaunchKernelGGL(graph_pcg_dir_spmv_kernel, dim3(nb), dim3(kSpmvThreads), 0,
+                                   h->stream, h->nt, k, h->rptr, h->scol, h->val, h->z, h->p, h->q,
+                                   h->part, h->st, h->cfg.pcg_tol, h->cfg.pcg_max_iter);
+                hipLaunchKernelGGL(graph_pcg_step_kernel, dim3(nb), dim3(kPcgThreads), 0, h->stream,
+                                   n, k, h->minv, h->p, h->q, h->delta, h->r, h->z, h->part, h->st);
+            }
+            SLAM_HIP_TRY(hipGetLastError());
+            SLAM_HIP_TRY(hipMemcpyAsync(&s, h->st, sizeof(PcgState), hipMemcpyDeviceToHost, h->stream));
         }
-        SLAM_HIP_TRY(hipGetLastError());
-        SLAM_HIP_TRY(hipMemcpyAsync(&s, h->st, sizeof(PcgState), hipMemcpyDeviceToHost, h->stream));
-        SLAM_HIP_TRY(hipStreamSynchronize(h->stream));
-        if (s.done) break;
+        if (!cond_done) {
+            GTRY(cond_enqueue(h, c0, c_end - c0));
+            SLAM_HIP_TRY(hipMemcpyAsync(&cs, h->cst, sizeof(CondState), hipMemcpyDeviceToHost,
+                                        h->cstream));
+        }
+        if (!pcg_done) {
+            SLAM_HIP_TRY(hipStreamSynchronize(h->stream));
+            pcg_done = s.done;
+            k0 = k_end;
+            k_end += 8;
+        }
+        if (!cond_done) {
+            SLAM_HIP_TRY(hipStreamSynchronize(h->cstream));
+            cond_done = cs.done;
+            c0 = c_end;
+            c_end += 16;
+            // the gate rejects H for certain (cond >= cond_max, or not positive
+            // definite): the reference does not solve (:496), neither do we
+            if (cs.done && (cs.status == 2 || cs.status == 4) && !pcg_done) {
+                pcg_done = true;
+                abandoned = true;
+            }
+        }
     }
     *iters = s.iter;
     h->pcg_last_iters = (s.status == 1) ? s.iter : 0;
-    stats[2] = std::numeric_limits<double>::quiet_NaN();
+    const bool pcg_ok = (s.status == 1);
+    stats[2] = std::numeric_limits<double>::quiet_NaN();     // det: not formed at this size
     stats[3] = std::numeric_limits<double>::quiet_NaN();
-    *solved = (s.status == 1);
-    h->pcg_failed = !*solved;
+    bool gate = true;
+    for (double& v : h->cond_info) v = 0.0;
+    if (est) {
+        SLAM_HIP_TRY(hipEventRecord(h->cev[2], h->cstream));
+        SLAM_HIP_TRY(hipEventSynchronize(h->cev[2]));
+        float ms = 0.f;
+        SLAM_HIP_TRY(hipEventElapsedTime(&ms, h->cev[1], h->cev[2]));
+        const double cond = (cs.status == 4 || !(cs.lam[0] > 0.0))
+                                ? std::numeric_limits<double>::infinity()
+                                : cs.lam[1] / cs.lam[0];
+        stats[3] = cond;
+        gate = cond < h->cfg.cond_max;                        // :496
+        h->cond_warm = (cs.status == 1 || cs.status == 3);
+        h->cond_last_iters = (cs.status == 1) ? cs.iter : 0;
+        h->cond_info[0] = cs.iter;
+        h->cond_info[1] = cs.status;
+        h->cond_info[2] = cs.lam[0];
+        h->cond_info[3] = cs.lam[1];
+        h->cond_info[4] = cs.iters_side[0];
+        h->cond_info[5] = cs.iters_side[1];
+        h->cond_info[6] = ms;
+    }
+    *solved = pcg_ok && gate && !abandoned;
+    h->pcg_failed = !pcg_ok && !abandoned;
+    if (abandoned) {
+        *iters = -1;
+        h->pcg_last_iters = 0;
+    }
     return SLAM_OK;
 }
 
@@ -508,13 +628,21 @@ int slam_graph_create(const slam_graph_config* cfg, int device, slam_graph** out
     slam_graph* h = new slam_graph();
     h->cfg = *cfg;
     if (h->cfg.pcg_max_iter <= 0) h->cfg.pcg_max_iter = 10000;
+    if (!(h->cfg.cond_tol > 0.0)) h->cfg.cond_tol = 1e-5;
+    if (h->cfg.cond_max_iter <= 0) h->cfg.cond_max_iter = 3000;
     if (!(h->cfg.pcg_tol > 0.0)) h->cfg.pcg_tol = 1e-10;
     h->device = device;
-    if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
-        delete h;
+    if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&h->cstream, hipStreamNonBlocking) != hipSuccess) {
+        slam_graph_destroy(h);
         return fail(SLAM_ERR_HIP, "slam_graph_create: stream creation failed");
     }
     for (auto& e : h->ev)
+        if (hipEventCreate(&e) != hipSuccess) {
+            slam_graph_destroy(h);
+            return fail(SLAM_ERR_HIP, "slam_graph_create: event creation failed");
+        }
+    for (auto& e : h->cev)
         if (hipEventCreate(&e) != hipSuccess) {
             slam_graph_destroy(h);
             return fail(SLAM_ERR_HIP, "slam_graph_create: event creation failed");
@@ -531,6 +659,9 @@ int slam_graph_destroy(slam_graph* h) {
     if (h->poses) (void)hipFree(h->poses);
     for (auto& e : h->ev)
         if (e) (void)hipEventDestroy(e);
+    for (auto& e : h->cev)
+        if (e) (void)hipEventDestroy(e);
+    if (h->cstream) (void)hipStreamDestroy(h->cstream);
     if (h->stream) (void)hipStreamDestroy(h->stream);
     delete h;
     return SLAM_OK;
@@ -668,6 +799,12 @@ int slam_graph_get_delta(slam_graph* h, double* delta) {
 int slam_graph_timing(slam_graph* h, double* out) {
     SLAM_ARG_CHECK(h && out, "slam_graph_timing: NULL argument");
     for (int k = 0; k < 5; ++k) out[k] = h->last[k];
+    return SLAM_OK;
+}
+
+int slam_graph_cond_info(slam_graph* h, double* out) {
+    SLAM_ARG_CHECK(h && out, "slam_graph_cond_info: NULL argument");
+    for (int k = 0; k < 7; ++k) out[k] = h->cond_info[k];
     return SLAM_OK;
 }
 

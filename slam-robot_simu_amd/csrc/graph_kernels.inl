@@ -838,6 +838,427 @@ __global__ __launch_bounds__(kPcgThreads) void graph_pcg_step_kernel(
     }
 }
 
+// ------------------------------------------- condition number (PCG path)
+// updateEstPose's gate (:494-498) needs cond(H) = lambda_max / lambda_min (H
+// is symmetric positive definite up to rounding, so the 2-norm condition
+// number numpy forms by SVD is the ratio of its extreme eigenvalues).  At
+// config-5 size the dense route is out of reach (a 180 GB H); the extreme
+// eigenvalues come from LOBPCG (block size 1) on the block-sparse H, run on
+// a second stream beside the PCG solve:
+//   side 0: lambda_min, preconditioned by the PCG's block-Jacobi inverses
+//           (the preconditioner is what makes the smallest eigenvalue
+//           converge in ~100-200 iterations; plain Lanczos needs thousands);
+//   side 1: lambda_max, unpreconditioned.
+// Per iteration, for each side still running: w = T (Hx - theta x) (T = the
+// preconditioner or I); w' = w - (x.w) x, Hw' = H w - (x.w) Hx; Rayleigh-Ritz
+// on span{x, w', p} from its 3x3 Gram and projected matrices (scaled to a
+// unit diagonal, Cholesky, p dropped when it is nearly dependent, cyclic
+// Jacobi); x <- the Ritz vector, p <- its (w', p) part.  Three launches:
+// update (+ residual, preconditioner, x.w partials), SpMV of both sides'
+// w (one read of every 3x3 block) + orthogonalisation + the 24 Gram
+// partials, one-workgroup fold of the partials in a fixed order.  Every
+// workgroup solves the small problems redundantly from the same folded
+// totals, so the decisions are identical everywhere.  A side stops when
+// theta moved less than tol * theta over kCondWin iterations; the estimate
+// stops early when theta_max / theta_min >= cond_max already (Ritz values lie
+// inside [lambda_min, lambda_max], so the true cond is at least that: the gate
+// rejects for certain) or theta_min <= 0 (not positive definite).
+constexpr int kCondHist = 64;
+constexpr int kCondWin = 16;
+constexpr int kCondGram = 12;   // per side: G00 G01 G02 G11 G12 G22, A00 A01 A02 A11 A12 A22
+
+struct CondState {
+    double theta[2][kCondHist];   // Ritz value of each side per iteration (ring)
+    double tot[2 * kCondGram];    // the fold launch's totals
+    double lam[2];                // the latest Ritz values (min side, max side)
+    int32_t iter, done, status, iters_side[2], conv[2], pad;
+};
+
+__device__ __forceinline__ uint64_t cond_mix64(uint64_t z) {
+    z += 0x9E3779B97F4A7C15ULL;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    return z ^ (z >> 31);
+}
+
+template <int NT, int K>
+__device__ __forceinline__ void block_sumK_fixed(double* v, double* sh) {
+    // K sums through one LDS round; sh holds K * NT / 64 doubles
+#pragma unroll
+    for (int j = 0; j < K; ++j)
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) v[j] += __shfl_xor(v[j], d, 64);
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0)
+#pragma unroll
+        for (int j = 0; j < K; ++j) sh[j * (NT / 64) + (threadIdx.x >> 6)] = v[j];
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+        double r = 0.0;
+        for (int w = 0; w < NT / 64; ++w) r += sh[j * (NT / 64) + w];
+        v[j] = r;
+    }
+    __syncthreads();
+}
+
+// Rayleigh-Ritz on span{x, w, p} (p absent when g22 == 0): g / a the six
+// distinct entries of the Gram and projected matrices.  Returns false when w
+// adds no direction (the side has converged to rounding).  c: coefficients of
+// the Ritz vector in (x, w, p), normalised so that |c0 x + c1 w + c2 p| = 1;
+// pn: |c1 w + c2 p|.
+__device__ bool cond_small(const double* g, const double* a, const bool want_max, double* c,
+                           double* theta, double* pn) {
+    double G[3][3] = {{g[0], g[1], g[2]}, {g[1], g[3], g[4]}, {g[2], g[4], g[5]}};
+    double A[3][3] = {{a[0], a[1], a[2]}, {a[1], a[3], a[4]}, {a[2], a[4], a[5]}};
+    int dim = (G[2][2] > 0.0) ? 3 : 2;
+    if (!(G[0][0] > 0.0) || !(G[1][1] > 0.0)) return false;
+    double s[3] = {1.0 / sqrt(G[0][0]), 1.0 / sqrt(G[1][1]), dim == 3 ? 1.0 / sqrt(G[2][2]) : 0.0};
+    double L[3][3] = {};
+    for (;;) {
+        // Cholesky of the unit-diagonal Gram
+        const double g10 = G[1][0] * s[1] * s[0];
+        L[0][0] = 1.0;
+        L[1][0] = g10;
+        const double l11 = 1.0 - g10 * g10;
+        if (!(l11 > 1e-10)) return false;
+        L[1][1] = sqrt(l11);
+        if (dim == 3) {
+            const double g20 = G[2][0] * s[2] * s[0], g21 = G[2][1] * s[2] * s[1];
+            L[2][0] = g20;
+            L[2][1] = (g21 - g20 * g10) / L[1][1];
+            const double l22 = 1.0 - L[2][0] * L[2][0] - L[2][1] * L[2][1];
+            if (l22 > 1e-10) {
+                L[2][2] = sqrt(l22);
+                break;
+            }
+            dim = 2;                       // p nearly dependent on x, w: drop it
+            s[2] = 0.0;
+            continue;
+        }
+        break;
+    }
+    // Li = L^-1 (lower triangular)
+    double Li[3][3] = {};
+    Li[0][0] = 1.0;
+    Li[1][1] = 1.0 / L[1][1];
+    Li[1][0] = -L[1][0] * Li[1][1];
+    if (dim == 3) {
+        Li[2][2] = 1.0 / L[2][2];
+        Li[2][1] = -L[2][1] * Li[1][1] * Li[2][2];
+        Li[2][0] = -(L[2][0] * Li[0][0] + L[2][1] * Li[1][0]) * Li[2][2];
+    }
+    // C = Li (s A s) Li^T
+    double As[3][3], T[3][3], C[3][3];
+    for (int i = 0; i < dim; ++i)
+        for (int j = 0; j < dim; ++j) As[i][j] = A[i][j] * s[i] * s[j];
+    for (int i = 0; i < dim; ++i)
+        for (int j = 0; j < dim; ++j) {
+            double acc = 0.0;
+            for (int k = 0; k <= i; ++k) acc = fma(Li[i][k], As[k][j], acc);
+            T[i][j] = acc;
+        }
+    for (int i = 0; i < dim; ++i)
+        for (int j = 0; j < dim; ++j) {
+            double acc = 0.0;
+            for (int k = 0; k <= j; ++k) acc = fma(T[i][k], Li[j][k], acc);
+            C[i][j] = acc;
+        }
+    for (int i = 0; i < dim; ++i)
+        for (int j = 0; j < i; ++j) C[i][j] = C[j][i] = 0.5 * (C[i][j] + C[j][i]);
+    // cyclic Jacobi (dim <= 3), eigenvectors in V
+    double V[3][3] = {{1, 0, 0}, {0, 1, 0}, {0, 0, 1}};
+    for (int sweep = 0; sweep < 12; ++sweep) {
+        double off = 0.0;
+        for (int i = 0; i < dim; ++i)
+            for (int j = i + 1; j < dim; ++j) off += C[i][j] * C[i][j];
+        if (off == 0.0) break;
+        for (int p = 0; p < dim; ++p)
+            for (int q = p + 1; q < dim; ++q) {
+                if (C[p][q] == 0.0) continue;
+                const double tau = (C[q][q] - C[p][p]) / (2.0 * C[p][q]);
+                const double t = (tau >= 0.0 ? 1.0 : -1.0) / (fabs(tau) + sqrt(1.0 + tau * tau));
+                const double cs = 1.0 / sqrt(1.0 + t * t), sn = t * cs;
+                for (int k = 0; k < dim; ++k) {           // C <- J^T C J
+                    const double ckp = C[k][p], ckq = C[k][q];
+                    C[k][p] = cs * ckp - sn * ckq;
+                    C[k][q] = sn * ckp + cs * ckq;
+                }
+                for (int k = 0; k < dim; ++k) {
+                    const double cpk = C[p][k], cqk = C[q][k];
+                    C[p][k] = cs * cpk - sn * cqk;
+                    C[q][k] = sn * cpk + cs * cqk;
+                }
+                for (int k = 0; k < dim; ++k) {
+                    const double vkp = V[k][p], vkq = V[k][q];
+                    V[k][p] = cs * vkp - sn * vkq;
+                    V[k][q] = sn * vkp + cs * vkq;
+                }
+            }
+    }
+    int e = 0;
+    for (int i = 1; i < dim; ++i)
+        if (want_max ? (C[i][i] > C[e][e]) : (C[i][i] < C[e][e])) e = i;
+    *theta = C[e][e];
+    // c = s (Li^T y)
+    double y[3] = {V[0][e], V[1][e], dim == 3 ? V[2][e] : 0.0};
+    for (int i = 0; i < 3; ++i) {
+        double acc = 0.0;
+        for (int k = i; k < dim; ++k) acc = fma(Li[k][i], y[k], acc);
+        c[i] = (i < dim) ? acc * s[i] : 0.0;
+    }
+    const double pp = c[1] * c[1] * G[1][1] + 2.0 * c[1] * c[2] * G[1][2] + c[2] * c[2] * G[2][2];
+    *pn = sqrt(fmax(pp, 0.0));
+    return true;
+}
+
+// random start (cold) or the previous update's vectors (warm); p = Hp = 0
+__global__ __launch_bounds__(256) void graph_cond_init_kernel(const int64_t n, const int cold,
+                                                              double* __restrict__ x,
+                                                              double* __restrict__ p,
+                                                              double* __restrict__ hp,
+                                                              CondState* __restrict__ st) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i == 0) {
+        st->iter = 0;
+        st->done = 0;
+        st->status = 0;
+        st->conv[0] = st->conv[1] = 0;
+        st->iters_side[0] = st->iters_side[1] = 0;
+    }
+    if (i >= 2 * n) return;
+    if (cold) x[i] = (double)(int64_t)(cond_mix64((uint64_t)i) >> 11) * 0x1.0p-52 - 1.0;
+    p[i] = 0.0;
+    hp[i] = 0.0;
+}
+
+__device__ __forceinline__ void cond_block_dot2(const int64_t s, const int64_t* __restrict__ col,
+                                                const double* __restrict__ val,
+                                                const double* __restrict__ v0,
+                                                const double* __restrict__ v1, double* a) {
+    const double* m = val + s * 9;
+    double b[9];
+#pragma unroll
+    for (int j = 0; j < 9; ++j) b[j] = m[j];
+    const int64_t c = 3 * col[s];
+    const double x0 = v0[c], x1 = v0[c + 1], x2 = v0[c + 2];
+    const double y0 = v1[c], y1 = v1[c + 1], y2 = v1[c + 2];
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+        a[r] = fma(b[3 * r], x0, a[r]);
+        a[r] = fma(b[3 * r + 1], x1, a[r]);
+        a[r] = fma(b[3 * r + 2], x2, a[r]);
+        a[3 + r] = fma(b[3 * r], y0, a[3 + r]);
+        a[3 + r] = fma(b[3 * r + 1], y1, a[3 + r]);
+        a[3 + r] = fma(b[3 * r + 2], y2, a[3 + r]);
+    }
+}
+
+// START = true: Hx of both sides' x, partials x.x and x.Hx (part rows 0, 6
+// of each side's 12).  START = false: alpha = x.w (folded from the update
+// launch's partials), Hw, w' = w - alpha x, Hw' = Hw - alpha Hx and the 24 Gram
+// partials.  part: [24][nb] Gram, then [2][nb] x.w.
+template <bool START>
+__global__ __launch_bounds__(kSpmvThreads) void graph_cond_spmv_kernel(
+    const int64_t nt, const int64_t* __restrict__ rptr, const int64_t* __restrict__ col,
+    const double* __restrict__ val, const double* __restrict__ x, double* __restrict__ hx,
+    const double* __restrict__ w, double* __restrict__ w2, double* __restrict__ hw,
+    const double* __restrict__ p, const double* __restrict__ hp, double* __restrict__ part,
+    const CondState* __restrict__ st) {
+    __shared__ double sh[2 * kCondGram * kSpmvThreads / 64];
+    if (!START && st->done) return;
+    const int64_t n = 3 * nt;
+    const int64_t nb = gridDim.x;
+    double alpha[2] = {0.0, 0.0};
+    bool run[2] = {true, true};
+    if (!START) {
+        double al[2] = {pcg_fold_lane<kSpmvThreads>(part + 2 * kCondGram * nb, nb),
+                        pcg_fold_lane<kSpmvThreads>(part + (2 * kCondGram + 1) * nb, nb)};
+        block_sumK_fixed<kSpmvThreads, 2>(al, sh);
+        alpha[0] = al[0];
+        alpha[1] = al[1];
+        run[0] = !st->conv[0];
+        run[1] = !st->conv[1];
+    }
+    const double* src = START ? x : w;
+    const int g = threadIdx.x & (kSpmvGroup - 1);
+    const int64_t rw = (int64_t)blockIdx.x * (kSpmvThreads / kSpmvGroup) + threadIdx.x / kSpmvGroup;
+    double a[6] = {0, 0, 0, 0, 0, 0};
+    if (rw < nt) {
+        const int64_t s1 = rptr[rw + 1];
+        for (int64_t s = rptr[rw] + g; s < s1; s += kSpmvGroup) cond_block_dot2(s, col, val, src, src + n, a);
+    }
+#pragma unroll
+    for (int d = 1; d < kSpmvGroup; d <<= 1)
+#pragma unroll
+        for (int j = 0; j < 6; ++j) a[j] += __shfl_xor(a[j], d, 64);
+    double v[2 * kCondGram];
+#pragma unroll
+    for (int j = 0; j < 2 * kCondGram; ++j) v[j] = 0.0;
+    if (rw < nt && g < 3) {
+        const int64_t i = 3 * rw + g;
+#pragma unroll
+        for (int sd = 0; sd < 2; ++sd) {
+            const double hv = (g == 0) ? a[3 * sd] : (g == 1) ? a[3 * sd + 1] : a[3 * sd + 2];
+            const int64_t k = sd * n + i;
+            double* o = v + sd * kCondGram;
+            if (START) {
+                hx[k] = hv;
+                const double xi = x[k];
+                o[0] = xi * xi;
+                o[6] = xi * hv;
+            } else if (run[sd]) {
+                const double xi = x[k], hxi = hx[k], pi = p[k], hpi = hp[k];
+                const double wi = fma(-alpha[sd], xi, w[k]);
+                const double hwi = fma(-alpha[sd], hxi, hv);
+                w2[k] = wi;
+                hw[k] = hwi;
+                o[0] = xi * xi;
+                o[1] = xi * wi;
+                o[2] = xi * pi;
+                o[3] = wi * wi;
+                o[4] = wi * pi;
+                o[5] = pi * pi;
+                o[6] = xi * hxi;
+                o[7] = 0.5 * (xi * hwi + wi * hxi);
+                o[8] = 0.5 * (xi * hpi + pi * hxi);
+                o[9] = wi * hwi;
+                o[10] = 0.5 * (wi * hpi + pi * hwi);
+                o[11] = pi * hpi;
+            }
+        }
+    }
+    block_sumK_fixed<kSpmvThreads, 2 * kCondGram>(v, sh);
+    if (threadIdx.x == 0)
+#pragma unroll
+        for (int j = 0; j < 2 * kCondGram; ++j) part[j * nb + blockIdx.x] = v[j];
+}
+
+// one workgroup: the 24 Gram partial rows folded in a fixed order (one wave
+// per row, lanes strided, then the xor butterfly) into st->tot
+constexpr int kCondFoldThreads = 1024;
+__global__ __launch_bounds__(kCondFoldThreads) void graph_cond_fold_kernel(
+    const int64_t nb, const double* __restrict__ part, CondState* __restrict__ st, const int first) {
+    if (!first && st->done) return;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    for (int j = wave; j < 2 * kCondGram; j += kCondFoldThreads / 64) {
+        double s = 0.0;
+        for (int64_t k = lane; k < nb; k += 64) s += part[j * nb + k];
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) s += __shfl_xor(s, d, 64);
+        if (lane == 0) st->tot[j] = s;
+    }
+}
+
+// k = 0: normalise x (and Hx) from x.x, theta = x.Hx.  k > 0: Rayleigh-Ritz,
+// x, Hx, p, Hp updated on the own rows, the stopping tests.  Then r = Hx -
+// theta x, w = T r (side 0: the block-Jacobi inverse of the pose, the three
+// rows of a pose in one workgroup) and the x.w partials.
+__global__ __launch_bounds__(kPcgThreads) void graph_cond_update_kernel(
+    const int64_t n, const int32_t k, const double* __restrict__ minv, double* __restrict__ x,
+    double* __restrict__ hx, const double* __restrict__ w2, const double* __restrict__ hw,
+    double* __restrict__ p, double* __restrict__ hp, double* __restrict__ w,
+    double* __restrict__ part, CondState* __restrict__ st, const double tol,
+    const int32_t max_iter, const double cond_max) {
+    __shared__ double sh[2 * kPcgThreads / 64];
+    __shared__ double rs[kPcgThreads];
+    if (st->done) return;
+    const int64_t nb = gridDim.x;
+    const int64_t i = (int64_t)blockIdx.x * kPcgThreads + threadIdx.x;
+    double th[2];
+    bool run[2] = {!st->conv[0], !st->conv[1]};
+    bool conv_now[2] = {false, false};
+    int status = 0;
+    double xo[2] = {0.0, 0.0}, hxo[2] = {0.0, 0.0};
+    for (int sd = 0; sd < 2; ++sd) {
+        const double* t = st->tot + sd * kCondGram;
+        const int64_t kk = sd * n + i;
+        if (k == 0) {
+            const double sc = 1.0 / sqrt(t[0]);
+            th[sd] = t[6] / t[0];
+            if (i < n) {
+                xo[sd] = x[kk] * sc;
+                hxo[sd] = hx[kk] * sc;
+                x[kk] = xo[sd];
+                hx[kk] = hxo[sd];
+            }
+            continue;
+        }
+        th[sd] = st->lam[sd];
+        if (!run[sd]) continue;
+        const double g[6] = {t[0], t[1], t[2], t[3], t[4], t[5]};
+        const double a[6] = {t[6], t[7], t[8], t[9], t[10], t[11]};
+        double c[3], theta, pn;
+        if (!cond_small(g, a, sd == 1, c, &theta, &pn)) {
+            conv_now[sd] = true;               // w' adds nothing: converged to rounding
+            if (i < n) {
+                xo[sd] = x[kk];
+                hxo[sd] = hx[kk];
+            }
+            continue;
+        }
+        th[sd] = theta;
+        if (i < n) {
+            const double xi = x[kk], hxi = hx[kk], wi = w2[kk], hwi = hw[kk], pi = p[kk], hpi = hp[kk];
+            xo[sd] = fma(c[2], pi, fma(c[1], wi, c[0] * xi));
+            hxo[sd] = fma(c[2], hpi, fma(c[1], hwi, c[0] * hxi));
+            x[kk] = xo[sd];
+            hx[kk] = hxo[sd];
+            const double ip = (pn > 0.0) ? 1.0 / pn : 0.0;
+            p[kk] = fma(c[2], pi, c[1] * wi) * ip;
+            hp[kk] = fma(c[2], hpi, c[1] * hwi) * ip;
+        }
+        const double old = st->theta[sd][(k - kCondWin) & (kCondHist - 1)];
+        if (k >= kCondWin && fabs(old - theta) <= tol * fabs(theta)) conv_now[sd] = true;
+    }
+    // stopping tests (identical in every workgroup)
+    const bool c0 = !run[0] || conv_now[0], c1 = !run[1] || conv_now[1];
+    if (!(th[0] > 0.0)) status = 4;                                   // not positive definite
+    else if (th[1] >= cond_max * th[0]) status = 2;                   // cond >= cond_max for certain
+    else if (c0 && c1) status = 1;
+    else if (k >= max_iter) status = 3;
+    if (pcg_lead()) {
+        for (int sd = 0; sd < 2; ++sd) {
+            st->theta[sd][k & (kCondHist - 1)] = th[sd];
+            st->lam[sd] = th[sd];
+            if (run[sd]) st->iters_side[sd] = k;
+            if (conv_now[sd]) st->conv[sd] = 1;
+        }
+        st->iter = k;
+        st->status = status;
+        st->done = status != 0;
+    }
+    if (status) return;
+    // r = Hx - theta x, w = T r, partials x.w
+    double xw[2] = {0.0, 0.0};
+    for (int sd = 0; sd < 2; ++sd) {
+        const bool act = (k == 0) || (run[sd] && !conv_now[sd]);
+        const double ri = (i < n && act) ? fma(-th[sd], xo[sd], hxo[sd]) : 0.0;
+        double wi = ri;
+        if (sd == 0) {
+            rs[threadIdx.x] = ri;
+            __syncthreads();
+            if (i < n) {
+                const int a3 = (int)(i % 3);
+                const double* m = minv + (i - a3) * 3 + 3 * a3;
+                const double* rb = rs + threadIdx.x - a3;
+                wi = m[0] * rb[0];
+                wi = fma(m[1], rb[1], wi);
+                wi = fma(m[2], rb[2], wi);
+            }
+        }
+        if (i < n && act) {
+            w[sd * n + i] = wi;
+            xw[sd] = xo[sd] * wi;
+        }
+    }
+    block_sum2_fixed<kPcgThreads>(xw[0], xw[1], sh);
+    if (threadIdx.x == 0) {
+        part[2 * kCondGram * nb + blockIdx.x] = xw[0];
+        part[(2 * kCondGram + 1) * nb + blockIdx.x] = xw[1];
+    }
+}
+
 // block-Jacobi preconditioner: inverses of the diagonal 3x3 blocks
 __global__ __launch_bounds__(256) void graph_block_inv_kernel(const int64_t nb,
                                                               const int64_t* __restrict__ dslot,

@@ -60,10 +60,12 @@ class GraphEdge(C.Structure):
 class GraphConfig(C.Structure):
     _fields_ = [("r_dist", C.c_double), ("r_dir", C.c_double), ("r_orient", C.c_double),
                 ("anchor", C.c_double), ("det_min", C.c_double), ("cond_max", C.c_double),
-                ("pcg_tol", C.c_double), ("pcg_max_iter", C.c_int32), ("solver", C.c_int32)]
+                ("pcg_tol", C.c_double), ("pcg_max_iter", C.c_int32), ("solver", C.c_int32),
+                ("cond_tol", C.c_double), ("cond_max_iter", C.c_int32), ("cond_mode", C.c_int32)]
 
 
 GRAPH_SOLVER = {"auto": 0, "dense": 1, "pcg": 2}
+GRAPH_COND = {"estimate": 0, "off": 1}
 
 _P = C.c_void_p
 _D = C.POINTER(C.c_double)
@@ -165,6 +167,7 @@ SIGNATURES = {
     "slam_graph_get_bsr": (C.c_int, [_P, _I64, _I64, _I64, _D]),
     "slam_graph_get_delta": (C.c_int, [_P, _D]),
     "slam_graph_timing": (C.c_int, [_P, _D]),
+    "slam_graph_cond_info": (C.c_int, [_P, _D]),
     "slam_graph_linearize_solve": (C.c_int, [C.POINTER(GraphConfig), _P, C.c_int64, _D, C.c_int64,
                                              _D, C.c_int]),
     "slam_graph_pair_halves": (C.c_int, [C.c_int64, _P, C.c_int64, C.c_int, _I64, _P]),

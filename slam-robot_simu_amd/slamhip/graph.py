@@ -8,7 +8,7 @@ import ctypes as C
 import numpy as np
 
 from . import _lib
-from ._lib import GRAPH_SOLVER, GraphConfig, check, dptr
+from ._lib import GRAPH_COND, GRAPH_SOLVER, GraphConfig, check, dptr
 
 # slam_graph_edge, 80 bytes
 EDGE_DTYPE = np.dtype([("time_bfr", "<i8"), ("pose_bfr", "<i8"), ("time_aft", "<i8"),
@@ -65,12 +65,14 @@ class DeviceGraph:
 
     def __init__(self, *, r_dist=0.05, r_dir=np.deg2rad(2.0), r_orient=np.deg2rad(2.0),
                  anchor=1e4, det_min=0.1, cond_max=1e15, solver="auto", pcg_tol=1e-10,
-                 pcg_max_iter=20000, device=0):
+                 pcg_max_iter=20000, cond="estimate", cond_tol=1e-5, cond_max_iter=3000, device=0):
         cfg = GraphConfig()
         cfg.r_dist, cfg.r_dir, cfg.r_orient = float(r_dist), float(r_dir), float(r_orient)
         cfg.anchor, cfg.det_min, cfg.cond_max = float(anchor), float(det_min), float(cond_max)
         cfg.pcg_tol, cfg.pcg_max_iter = float(pcg_tol), int(pcg_max_iter)
         cfg.solver = GRAPH_SOLVER[solver]
+        cfg.cond_mode = GRAPH_COND[cond]
+        cfg.cond_tol, cfg.cond_max_iter = float(cond_tol), int(cond_max_iter)
         self.cfg = cfg
         self._lib = _lib.load()
         h = C.c_void_p()
@@ -155,6 +157,14 @@ class DeviceGraph:
         check(self._lib.slam_graph_timing(self._h, dptr(out)), "slam_graph_timing")
         return dict(linearize_ms=out[0], assemble_ms=out[1], solve_ms=out[2], update_ms=out[3],
                     pcg_iterations=int(out[4]))
+
+    def cond_info(self):
+        """The last PCG-path update's condition estimate (slam_graph_cond_info)."""
+        out = np.zeros(7)
+        check(self._lib.slam_graph_cond_info(self._h, dptr(out)), "slam_graph_cond_info")
+        return dict(iterations=int(out[0]), status=int(out[1]), lambda_min=out[2],
+                    lambda_max=out[3], iterations_min=int(out[4]), iterations_max=int(out[5]),
+                    ms=out[6])
 
 
 def circle_graph(n_poses, n_landmarks=64, loops_per_pose=3, seed=0, odom_noise=0.02):

@@ -146,7 +146,7 @@ def test_c5_graph_full_size_pcg_solves():
         dev.set_edges(edges)
         for _ in range(2):
             is_calc, dsum, det, cond = dev.update()
-            assert is_calc and np.isnan(det) and np.isnan(cond)
+            assert is_calc and np.isnan(det) and np.isfinite(cond) and cond < 1e15
             rows, cols, vals = dev.get_bsr()
             nt = int(rows.max()) + 1
             assert nt == 50000

@@ -15,18 +15,32 @@ import sys
 
 
 def load(dirpath):
+    """Counters per (kernel, grid size): one kernel launched at several sizes
+    (the bench's 2^20 line and its 2^23 strong-scaling reference) is kept
+    apart, the 2^20 grid under the plain name, others as 'name @grid G'."""
     per = collections.defaultdict(lambda: collections.defaultdict(list))
+    grids = collections.defaultdict(collections.Counter)
+    rows = []
     for f in glob.glob(os.path.join(dirpath, "p*", "pmc_counter_collection.csv")):
         for r in csv.DictReader(open(f)):
-            name = r["Kernel_Name"]
-            per[name][r["Counter_Name"]].append(float(r["Counter_Value"]))
-            per[name]["_dur_ns"].append(float(r["End_Timestamp"]) - float(r["Start_Timestamp"]))
+            rows.append(r)
+            grids[r["Kernel_Name"]][int(r["Grid_Size"])] += 1
+    for r in rows:
+        name, g = r["Kernel_Name"], int(r["Grid_Size"])
+        if len(grids[name]) > 1 and g != FUSED_GRID:
+            name = f"{name} @grid {g}"
+        per[name][r["Counter_Name"]].append(float(r["Counter_Value"]))
+        per[name]["_dur_ns"].append(float(r["End_Timestamp"]) - float(r["Start_Timestamp"]))
     return per
+
+
+FUSED_GRID = (1 << 20) // 2          # the bench's fused grid: 2^20 particles, two per lane
 
 
 def short(name):
     n = name.replace("slam::", "").replace("void ", "")
-    return n.split("(")[0]
+    g = n.split(" @grid ")
+    return n.split("(")[0] + (f" @grid {g[1]}" if len(g) > 1 else "")
 
 
 def main(src, tag):
