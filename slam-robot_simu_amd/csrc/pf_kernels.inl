@@ -850,57 +850,34 @@ __device__ __forceinline__ int likelihood_lanes(const double* xn, const double* 
         }
     }
     bool slow[P];
-    int any_slow = 0;
 #pragma unroll
     for (int k = 0; k < P; ++k) {
         bn[k] = exp_lean(L[k]);
         slow[k] = !(L[k] >= lc.fast_min_l);                 // also NaN
-        any_slow |= slow[k] ? 1 : 0;
-    }
 #ifdef SLAM_PROBE_NO_SLOW                                  // timing probe only: not exact
-    any_slow = 0;
+        slow[k] = false;
 #endif
-    // The few slow particles of the block (bench workload: ~1,500 of 2^20 on
-    // every third step, in half of the blocks; ~100 on the step after) are
-    // compacted through LDS and taken one per wave.  Block-uniform: every lane
-    // reaches the barriers.
-    if (__syncthreads_or(any_slow)) {
-        constexpr int kMax = 256 * P;
-        __shared__ int s_nslow;
-        __shared__ double s_pt[4][kMax];
-        __shared__ double s_bn[kMax];
-        const int tl = (wave_s << 6) | (int)__lane_id();
-        if (tl == 0) s_nslow = 0;
-        __syncthreads();
-        int slot[P];
+    }
+    // The few slow particles (bench workload: ~1,500 of 2^20 on every third
+    // step, ~100 on the step after) are taken by their own wave, one at a
+    // time with all 64 lanes on it: no block barrier and no LDS staging, so a
+    // wave without one pays two ballots.  Wave-uniform loops.
 #pragma unroll
-        for (int k = 0; k < P; ++k) {
-            slot[k] = -1;
-            if (slow[k]) {
-                slot[k] = atomicAdd(&s_nslow, 1);
-                s_pt[0][slot[k]] = xn[k];
-                s_pt[1][slot[k]] = yn[k];
-                s_pt[2][slot[k]] = sp[k];
-                s_pt[3][slot[k]] = cp[k];
-            }
-        }
-        __syncthreads();
-        const int ns = s_nslow;
+    for (int k = 0; k < P; ++k) {
+        unsigned long long m = __ballot(slow[k]);
 #ifdef SLAM_PROBE_COUNT_SLOW                               // probe builds only
-        if (tl == 0) {
-            atomicAdd(&g_probe_slow[0], (unsigned long long)ns);
+        if (__lane_id() == 0 && m) {
+            atomicAdd(&g_probe_slow[0], (unsigned long long)__popcll(m));
             atomicAdd(&g_probe_slow[1], 1ull);
         }
 #endif
-        // one slow particle per wave, all 64 lanes on it (wave-uniform loop)
-        for (int t = wave_s; t < ns; t += (int)(blockDim.x >> 6)) {
-            const double r = logsum_slow(s_pt[0][t], s_pt[1][t], s_pt[2][t], s_pt[3][t], lm, z, lc);
-            if ((tl & 63) == 0) s_bn[t] = r;
+        while (m) {
+            const int l = __ffsll((long long)m) - 1;
+            m &= m - 1;
+            const double r = logsum_slow(__shfl(xn[k], l, 64), __shfl(yn[k], l, 64),
+                                         __shfl(sp[k], l, 64), __shfl(cp[k], l, 64), lm, z, lc);
+            if ((int)__lane_id() == l) bn[k] = r;
         }
-        __syncthreads();
-#pragma unroll
-        for (int k = 0; k < P; ++k)
-            if (slot[k] >= 0) bn[k] = s_bn[slot[k]];
     }
     return lane_dd;
 }
@@ -975,6 +952,29 @@ __global__ __launch_bounds__(256) SLAM_FUSED_ATTR void pf_fused_kernel(
         }
     } else {
         wprev[0] = w_in[idx[0]];
+    }
+    // host / pre-drawn noise of the lane's particles (particle-major [n][3]):
+    // three 16-byte loads per pair, issued with the others
+    double gn[P][3];
+    if (HOSTNOISE && MOTION != kMotionNone) {
+        if (DEFER && i0 + P <= n) {
+#pragma unroll
+            for (int h = 0; h < P; h += 2) {
+                const double2* q2 = reinterpret_cast<const double2*>(noise + 3 * (i0 + h));
+                const double2 a = q2[0], b = q2[1], c3 = q2[2];
+                gn[h][0] = a.x;
+                gn[h][1] = a.y;
+                gn[h][2] = b.x;
+                gn[h + 1][0] = b.y;
+                gn[h + 1][1] = c3.x;
+                gn[h + 1][2] = c3.y;
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < P; ++k)
+#pragma unroll
+                for (int j = 0; j < 3; ++j) gn[k][j] = noise[3 * idx[k] + j];
+        }
     }
 
     // ---- source particles: the resample gather (rflag 1: search the exact
@@ -1065,11 +1065,9 @@ __global__ __launch_bounds__(256) SLAM_FUSED_ATTR void pf_fused_kernel(
         for (int k = 0; k < P; ++k) g[k][0] = g[k][1] = g[k][2] = 0.0;
     } else if (HOSTNOISE) {
 #pragma unroll
-        for (int k = 0; k < P; ++k) {
-            g[k][0] = noise[3 * idx[k] + 0];
-            g[k][1] = noise[3 * idx[k] + 1];
-            g[k][2] = noise[3 * idx[k] + 2];
-        }
+        for (int k = 0; k < P; ++k)
+#pragma unroll
+            for (int j = 0; j < 3; ++j) g[k][j] = gn[k][j];
     } else {
         const uint64_t gi = (uint64_t)(pc.gbase + i0);
         double h[6];
@@ -1123,8 +1121,14 @@ __global__ __launch_bounds__(256) SLAM_FUSED_ATTR void pf_fused_kernel(
 
     // ---- likelihood and weight (particle_filter.py:170-198)
     double bn[P];
+#ifdef SLAM_PROBE_NO_LIK                                   // timing probe only: not exact
+#pragma unroll
+    for (int k = 0; k < P; ++k) bn[k] = exp_lean(-1e-3 * (xv[k] + yv[k] + sp[k] + cp[k]));
+    const int lane_dd = 0;
+#else
     const int lane_dd = likelihood_lanes<LIK, P>(xv, yv, sp, cp, lm, zs,
                                                  io.zc + (size_t)st * kZcWords, lc, bn, wave_s);
+#endif
     if (__ballot(lane_dd) != 0 && __lane_id() == 0) atomicAdd(&flags[kFlagDDWaves], 1);
     // previous weights: particle_filter.py:222 (a resampled step starts from
     // 1/NP) / :235-236 (deferred: w_un / s, NaN -> 1/NP)

@@ -56,6 +56,11 @@ K32(cvt_f32_u32, "v_cvt_f32_u32 %0, %0")
 K32(mul_u32_u24, "v_mul_u32_u24 %0, %0, %1")
 K32(mul_hi_u32_u24, "v_mul_hi_u32_u24 %0, %0, %1")
 K32(cndmask, "v_cndmask_b32 %0, %0, %1, vcc")
+K32(sin_f32, "v_sin_f32 %0, %0")
+K32(exp_f32, "v_exp_f32 %0, %0")
+K32(sqrt_f32, "v_sqrt_f32 %0, %0")
+K32(mul_f32, "v_mul_f32 %0, %0, %1")
+K64(fract_f64, "v_fract_f64 %0, %0")
 
 // v_mad_u64_u32 needs a 64-bit destination: 4 chains of 64-bit state
 __global__ __launch_bounds__(256) void k_mad_u64_u32(double* out, double a, double b) {
@@ -118,6 +123,7 @@ int main() {
     R(fma_f64); R(add_f64); R(mul_f64); R(rcp_f64); R(rsq_f64); R(sqrt_f64); R(ldexp_f64);
     R(frexp_mant_f64); R(rndne_f64); R(max_f64); R(mul_lo_u32); R(mul_hi_u32); R(mad_u64_u32);
     R(xor_b32); R(add_u32); R(alignbit_b32); R(fma_f32); R(log_f32); R(cvt_f32_u32);
-    R(mul_u32_u24); R(mul_hi_u32_u24); R(cndmask);
+    R(mul_u32_u24); R(mul_hi_u32_u24); R(cndmask); R(sin_f32); R(exp_f32); R(sqrt_f32);
+    R(mul_f32); R(fract_f64);
     return 0;
 }
