@@ -378,13 +378,26 @@ def bench_graph(n_poses=50000, iters=3, device=0):
         dev.set_edges(edges)
         t_sets.append(time.perf_counter() - t0)
     t_struct = float(np.median(t_sets))
-    dev.update()                                   # warm-up iteration
-    per, brk = [], []
+    dev.update()                                   # warm-up iteration (cold cond estimate)
+    cond_first = dev.cond_info()
+    per, brk, conds = [], [], []
     for _ in range(iters):
         t0 = time.perf_counter()
         st = dev.update()
         per.append(time.perf_counter() - t0)
         brk.append(dev.timing())
+        conds.append(dict(dev.cond_info(), cond=st[3]))
+    dev.close()
+    # the same iterations without the gate's cond estimate (cond_mode off)
+    dev = DeviceGraph(solver="pcg", pcg_tol=1e-10, cond="off", device=device)
+    dev.set_poses(init)
+    dev.set_edges(edges)
+    dev.update()
+    per_off = []
+    for _ in range(iters):
+        t0 = time.perf_counter()
+        dev.update()
+        per_off.append(time.perf_counter() - t0)
     dev.close()
     lin = float(np.mean([b["linearize_ms"] for b in brk])) / 1e3
     return {"workload": f"graph SLAM C5: {n_poses} poses, {len(edges)} edges, block-Jacobi PCG",
@@ -393,6 +406,9 @@ def bench_graph(n_poses=50000, iters=3, device=0):
             "structure_build_first_ms": t_first * 1e3,
             "structure_build_max_ms": max(t_sets) * 1e3,
             "breakdown_ms": brk[-1], "is_calc": bool(st[0]),
+            "cond": conds[-1]["cond"], "cond_estimate": conds[-1],
+            "cond_estimate_first_update": cond_first,
+            "ms_per_iteration_without_cond": float(np.mean(per_off)) * 1e3,
             "linearize_edges_per_s": len(edges) / lin,
             "roofline": {"bound": "hbm", "kernel": "graph_linearize_kernel",
                          "achieved": (80 + 48 + 336) * len(edges) / lin / 1e9, "peak": HBM_PEAK_GBS,

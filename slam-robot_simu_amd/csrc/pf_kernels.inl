@@ -557,11 +557,23 @@ __device__ __forceinline__ double ref_q(const double xn, const double yn, const 
                                         const double cp, const double lx, const double ly,
                                         const double zx, const double zy, const LikConst& lc);
 
+// TAB: exp from the LDS table etab (product mode; exp_tab) instead of
+// exp_lean.  Without rho, q >= 0 (a sum of two rounded non-negative
+// quotients), so the argument is never positive.
+template <bool TAB = false>
 __device__ __forceinline__ double ref_factor(const double xn, const double yn, const double sp,
                                              const double cp, const double lx, const double ly,
-                                             const double zx, const double zy, const LikConst& lc) {
+                                             const double zx, const double zy, const LikConst& lc,
+                                             const double2* etab = nullptr) {
     const double q = ref_q(xn, yn, sp, cp, lx, ly, zx, zy, lc);
-    const double e = lc.has_rho ? exp_lean((-q) / lc.d2) : exp_lean((-q) * 0.5);  // d2 == 2 exactly
+    double e;
+    if (lc.has_rho) {
+        const double a = (-q) / lc.d2;
+        e = TAB ? exp_tab<false>(a, etab) : exp_lean(a);
+    } else {
+        const double a = (-q) * 0.5;                            // d2 == 2 exactly
+        e = TAB ? exp_tab<true>(a, etab) : exp_lean(a);
+    }
     return div_refined(e, lc.den, lc.rden);
 }
 
@@ -687,6 +699,10 @@ __device__ __forceinline__ int likelihood_lanes(const double* xn, const double* 
                                                  double* bn, const int wave_s) {
     const int nl = lc.nl;
     if (LIK == SLAM_LIK_PRODUCT) {
+        // the exp table in LDS (every lane of the block reaches this barrier)
+        __shared__ double2 s_etab[64];
+        if (threadIdx.x < 64) s_etab[threadIdx.x] = kExpTab64[threadIdx.x];
+        __syncthreads();
         double acc[P];
 #pragma unroll
         for (int k = 0; k < P; ++k) acc[k] = 1.0;
@@ -694,7 +710,7 @@ __device__ __forceinline__ int likelihood_lanes(const double* xn, const double* 
             const double lx = lm[2 * j], ly = lm[2 * j + 1], zx = z[2 * j], zy = z[2 * j + 1];
 #pragma unroll
             for (int k = 0; k < P; ++k)
-                acc[k] = acc[k] * ref_factor(xn[k], yn[k], sp[k], cp[k], lx, ly, zx, zy, lc);
+                acc[k] = acc[k] * ref_factor<true>(xn[k], yn[k], sp[k], cp[k], lx, ly, zx, zy, lc, s_etab);
         }
 #pragma unroll
         for (int k = 0; k < P; ++k) bn[k] = acc[k];

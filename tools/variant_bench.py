@@ -15,7 +15,8 @@ from slamhip.pf import DeviceParticleFilter  # noqa: E402
 steps = 24
 lm, zs, (vel, omega, dt) = bench.simulate_world(3 * steps)
 ctl = np.tile([vel, omega], (3 * steps, 1))
-pf = DeviceParticleFilter(bench.NP_PER_GPU, lm, dt=dt, motion="velocity", likelihood="logsum", seed=3)
+pf = DeviceParticleFilter(bench.NP_PER_GPU, lm, dt=dt, motion="velocity",
+                          likelihood=os.environ.get("VB_LIK", "logsum"), seed=3)
 pf.load_observations(zs)
 pf.run(0, ctl[:steps], want_results=False)
 t0 = time.perf_counter()
