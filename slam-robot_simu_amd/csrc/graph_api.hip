@@ -54,6 +54,8 @@ struct slam_graph {
     double *cx = nullptr, *chx = nullptr, *cp = nullptr, *chp = nullptr;
     double *cw = nullptr, *cw2 = nullptr, *chw = nullptr, *cpart = nullptr;
     CondState* cst = nullptr;
+    PcgState* pcg_host = nullptr;  // pinned copies of the device states: the polls of the
+    CondState* cond_host = nullptr;  // two streams must not block the host (pageable copies do)
     bool cond_warm = false;        // cx holds the previous update's vectors of this edge set
     int32_t cond_last_iters = 0;
     double cond_info[7] = {0, 0, 0, 0, 0, 0, 0};
@@ -457,10 +459,10 @@ int cond_enqueue(slam_graph* h, int32_t k0, int32_t count) {
                            h->rptr, h->scol, h->val, h->cx, h->chx, h->cw, h->cw2, h->chw, h->cp,
                            h->chp, h->cpart, h->cst);
         hipLaunchKernelGGL(graph_cond_fold_kernel, dim3(1), dim3(kCondFoldThreads), 0, s,
-                           (int64_t)nb, h->cpart, h->cst, 1);
+                           (int64_t)nb, h->cpart, h->cst, 0, tol, mx, h->cfg.cond_max);
         hipLaunchKernelGGL(graph_cond_update_kernel, dim3(nb), dim3(kPcgThreads), 0, s, n, 0,
                            h->minv, h->cx, h->chx, h->cw2, h->chw, h->cp, h->chp, h->cw, h->cpart,
-                           h->cst, tol, mx, h->cfg.cond_max);
+                           h->cst);
         k = 1;
     }
     for (; k < k0 + count; ++k) {
@@ -468,10 +470,10 @@ int cond_enqueue(slam_graph* h, int32_t k0, int32_t count) {
                            h->rptr, h->scol, h->val, h->cx, h->chx, h->cw, h->cw2, h->chw, h->cp,
                            h->chp, h->cpart, h->cst);
         hipLaunchKernelGGL(graph_cond_fold_kernel, dim3(1), dim3(kCondFoldThreads), 0, s,
-                           (int64_t)nb, h->cpart, h->cst, 0);
+                           (int64_t)nb, h->cpart, h->cst, k, tol, mx, h->cfg.cond_max);
         hipLaunchKernelGGL(graph_cond_update_kernel, dim3(nb), dim3(kPcgThreads), 0, s, n, k,
                            h->minv, h->cx, h->chx, h->cw2, h->chw, h->cp, h->chp, h->cw, h->cpart,
-                           h->cst, tol, mx, h->cfg.cond_max);
+                           h->cst);
     }
     SLAM_HIP_TRY(hipGetLastError());
     return SLAM_OK;
@@ -496,8 +498,10 @@ int solve_pcg(slam_graph* h, double* stats, bool* solved, int32_t* iters) {
     hipLaunchKernelGGL(graph_pcg_start_kernel, dim3(nb), dim3(kPcgThreads), 0, h->stream, n,
                        h->minv, h->b, h->delta, h->r, h->z, h->part);
     SLAM_HIP_TRY(hipGetLastError());
-    PcgState s{};
-    CondState cs{};
+    PcgState& s = *h->pcg_host;
+    CondState& cs = *h->cond_host;
+    s = PcgState{};
+    cs = CondState{};
     // The first batch runs through the previous solve's iteration count (the
     // Gauss-Newton steps of one edge set converge in similar counts), so a
     // repeated solve usually needs a single host poll; then batches of 8.
@@ -515,11 +519,12 @@ int solve_pcg(slam_graph* h, double* stats, bool* solved, int32_t* iters) {
                                    n, k, h->minv, h->p, h->q, h->delta, h->r, h->z, h->part, h->st);
             }
             SLAM_HIP_TRY(hipGetLastError());
-            SLAM_HIP_TRY(hipMemcpyAsync(&s, h->st, sizeof(PcgState), hipMemcpyDeviceToHost, h->stream));
+            SLAM_HIP_TRY(hipMemcpyAsync(h->pcg_host, h->st, sizeof(PcgState), hipMemcpyDeviceToHost,
+                                        h->stream));
         }
         if (!cond_done) {
             GTRY(cond_enqueue(h, c0, c_end - c0));
-            SLAM_HIP_TRY(hipMemcpyAsync(&cs, h->cst, sizeof(CondState), hipMemcpyDeviceToHost,
+            SLAM_HIP_TRY(hipMemcpyAsync(h->cond_host, h->cst, sizeof(CondState), hipMemcpyDeviceToHost,
                                         h->cstream));
         }
         if (!pcg_done) {
@@ -647,6 +652,11 @@ int slam_graph_create(const slam_graph_config* cfg, int device, slam_graph** out
             slam_graph_destroy(h);
             return fail(SLAM_ERR_HIP, "slam_graph_create: event creation failed");
         }
+    if (hipHostMalloc(&h->pcg_host, sizeof(PcgState)) != hipSuccess ||
+        hipHostMalloc(&h->cond_host, sizeof(CondState)) != hipSuccess) {
+        slam_graph_destroy(h);
+        return fail(SLAM_ERR_HIP, "slam_graph_create: pinned state buffers");
+    }
     *out = h;
     return SLAM_OK;
 }
@@ -661,6 +671,8 @@ int slam_graph_destroy(slam_graph* h) {
         if (e) (void)hipEventDestroy(e);
     for (auto& e : h->cev)
         if (e) (void)hipEventDestroy(e);
+    if (h->pcg_host) (void)hipHostFree(h->pcg_host);
+    if (h->cond_host) (void)hipHostFree(h->cond_host);
     if (h->cstream) (void)hipStreamDestroy(h->cstream);
     if (h->stream) (void)hipStreamDestroy(h->stream);
     delete h;

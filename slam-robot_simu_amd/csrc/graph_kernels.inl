@@ -871,7 +871,8 @@ struct CondState {
     double theta[2][kCondHist];   // Ritz value of each side per iteration (ring)
     double tot[2 * kCondGram];    // the fold launch's totals
     double lam[2];                // the latest Ritz values (min side, max side)
-    int32_t iter, done, status, iters_side[2], conv[2], pad;
+    double coef[2][4];            // this iteration's update of each side: c0, c1, c2, 1 / |p'|
+    int32_t iter, done, status, iters_side[2], conv[2], upd[2], pad;
 };
 
 __device__ __forceinline__ uint64_t cond_mix64(uint64_t z) {
@@ -902,112 +903,136 @@ __device__ __forceinline__ void block_sumK_fixed(double* v, double* sh) {
     __syncthreads();
 }
 
+// One Jacobi rotation of the symmetric 3x3 C in the (P, Q) plane, eigenvectors
+// accumulated in V; compile-time indices only (the arrays stay in registers).
+template <int P, int Q>
+__device__ __forceinline__ void jacobi_rot3(double (&C)[3][3], double (&V)[3][3]) {
+    if (!(fabs(C[P][Q]) > 1e-19 * (fabs(C[P][P]) + fabs(C[Q][Q])))) return;   // settled (or NaN)
+    const double tau = (C[Q][Q] - C[P][P]) / (2.0 * C[P][Q]);
+    const double t = (tau >= 0.0 ? 1.0 : -1.0) / (fabs(tau) + sqrt(1.0 + tau * tau));
+    const double cs = 1.0 / sqrt(1.0 + t * t), sn = t * cs;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const double ckp = C[k][P], ckq = C[k][Q];
+        C[k][P] = cs * ckp - sn * ckq;
+        C[k][Q] = sn * ckp + cs * ckq;
+    }
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const double cpk = C[P][k], cqk = C[Q][k];
+        C[P][k] = cs * cpk - sn * cqk;
+        C[Q][k] = sn * cpk + cs * cqk;
+    }
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const double vkp = V[k][P], vkq = V[k][Q];
+        V[k][P] = cs * vkp - sn * vkq;
+        V[k][Q] = sn * vkp + cs * vkq;
+    }
+}
+
 // Rayleigh-Ritz on span{x, w, p} (p absent when g22 == 0): g / a the six
 // distinct entries of the Gram and projected matrices.  Returns false when w
 // adds no direction (the side has converged to rounding).  c: coefficients of
 // the Ritz vector in (x, w, p), normalised so that |c0 x + c1 w + c2 p| = 1;
-// pn: |c1 w + c2 p|.
-__device__ bool cond_small(const double* g, const double* a, const bool want_max, double* c,
-                           double* theta, double* pn) {
-    double G[3][3] = {{g[0], g[1], g[2]}, {g[1], g[3], g[4]}, {g[2], g[4], g[5]}};
-    double A[3][3] = {{a[0], a[1], a[2]}, {a[1], a[3], a[4]}, {a[2], a[4], a[5]}};
-    int dim = (G[2][2] > 0.0) ? 3 : 2;
-    if (!(G[0][0] > 0.0) || !(G[1][1] > 0.0)) return false;
-    double s[3] = {1.0 / sqrt(G[0][0]), 1.0 / sqrt(G[1][1]), dim == 3 ? 1.0 / sqrt(G[2][2]) : 0.0};
-    double L[3][3] = {};
-    for (;;) {
-        // Cholesky of the unit-diagonal Gram
-        const double g10 = G[1][0] * s[1] * s[0];
-        L[0][0] = 1.0;
-        L[1][0] = g10;
-        const double l11 = 1.0 - g10 * g10;
-        if (!(l11 > 1e-10)) return false;
-        L[1][1] = sqrt(l11);
-        if (dim == 3) {
-            const double g20 = G[2][0] * s[2] * s[0], g21 = G[2][1] * s[2] * s[1];
-            L[2][0] = g20;
-            L[2][1] = (g21 - g20 * g10) / L[1][1];
-            const double l22 = 1.0 - L[2][0] * L[2][0] - L[2][1] * L[2][1];
-            if (l22 > 1e-10) {
-                L[2][2] = sqrt(l22);
-                break;
-            }
-            dim = 2;                       // p nearly dependent on x, w: drop it
-            s[2] = 0.0;
-            continue;
-        }
-        break;
+// pn: |c1 w + c2 p|.  The basis is scaled to a unit diagonal and its Gram
+// factored by Cholesky; p is dropped when it is nearly dependent on x, w.
+// Written with compile-time indices only (no scratch).
+__device__ __forceinline__ bool cond_small(const double* g, const double* a, const bool want_max,
+                                           double* c, double* theta, double* pn) {
+    if (!(g[0] > 0.0) || !(g[3] > 0.0)) return false;
+    const double s0 = 1.0 / sqrt(g[0]), s1 = 1.0 / sqrt(g[3]);
+    const double g10 = g[1] * s1 * s0;
+    const double l11q = 1.0 - g10 * g10;
+    if (!(l11q > 1e-10)) return false;
+    const double l11 = sqrt(l11q);
+    // the p direction, when present and independent enough
+    bool three = g[5] > 0.0;
+    double s2 = 0.0, l20 = 0.0, l21 = 0.0, l22 = 1.0;
+    if (three) {
+        s2 = 1.0 / sqrt(g[5]);
+        l20 = g[2] * s2 * s0;
+        l21 = (g[4] * s2 * s1 - l20 * g10) / l11;
+        const double l22q = 1.0 - l20 * l20 - l21 * l21;
+        three = l22q > 1e-10;
+        if (three) l22 = sqrt(l22q);
     }
-    // Li = L^-1 (lower triangular)
-    double Li[3][3] = {};
-    Li[0][0] = 1.0;
-    Li[1][1] = 1.0 / L[1][1];
-    Li[1][0] = -L[1][0] * Li[1][1];
-    if (dim == 3) {
-        Li[2][2] = 1.0 / L[2][2];
-        Li[2][1] = -L[2][1] * Li[1][1] * Li[2][2];
-        Li[2][0] = -(L[2][0] * Li[0][0] + L[2][1] * Li[1][0]) * Li[2][2];
+    // Li = L^-1 (lower triangular; the third row / column is the identity's
+    // when p is dropped, which decouples it)
+    const double i11 = 1.0 / l11, i10 = -g10 * i11;
+    double i22 = 1.0, i21 = 0.0, i20 = 0.0;
+    if (three) {
+        i22 = 1.0 / l22;
+        i21 = -l21 * i11 * i22;
+        i20 = -(l20 + l21 * i10) * i22;
     }
-    // C = Li (s A s) Li^T
-    double As[3][3], T[3][3], C[3][3];
-    for (int i = 0; i < dim; ++i)
-        for (int j = 0; j < dim; ++j) As[i][j] = A[i][j] * s[i] * s[j];
-    for (int i = 0; i < dim; ++i)
-        for (int j = 0; j < dim; ++j) {
+    const double Li[3][3] = {{1.0, 0.0, 0.0}, {i10, i11, 0.0}, {i20, i21, i22}};
+    // As = s A s; a dropped p gets a diagonal entry no Ritz value of (x, w)
+    // can lose to (so it is never selected)
+    const double sc[3] = {s0, s1, three ? s2 : 0.0};
+    double As[3][3] = {{a[0], a[1], a[2]}, {a[1], a[3], a[4]}, {a[2], a[4], a[5]}};
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) As[i][j] *= sc[i] * sc[j];
+    if (!three) {
+        As[0][2] = As[2][0] = As[1][2] = As[2][1] = 0.0;
+        As[2][2] = want_max ? -__builtin_huge_val() : __builtin_huge_val();
+    }
+    // C = Li As Li^T
+    double T[3][3], C[3][3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
             double acc = 0.0;
+#pragma unroll
             for (int k = 0; k <= i; ++k) acc = fma(Li[i][k], As[k][j], acc);
             T[i][j] = acc;
         }
-    for (int i = 0; i < dim; ++i)
-        for (int j = 0; j < dim; ++j) {
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
             double acc = 0.0;
+#pragma unroll
             for (int k = 0; k <= j; ++k) acc = fma(T[i][k], Li[j][k], acc);
             C[i][j] = acc;
         }
-    for (int i = 0; i < dim; ++i)
+    if (!three) {                      // keep the dummy entry exactly decoupled
+        C[0][2] = C[2][0] = C[1][2] = C[2][1] = 0.0;
+        C[2][2] = As[2][2];
+    }
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
         for (int j = 0; j < i; ++j) C[i][j] = C[j][i] = 0.5 * (C[i][j] + C[j][i]);
-    // cyclic Jacobi (dim <= 3), eigenvectors in V
-    double V[3][3] = {{1, 0, 0}, {0, 1, 0}, {0, 0, 1}};
+    double V[3][3] = {{1.0, 0.0, 0.0}, {0.0, 1.0, 0.0}, {0.0, 0.0, 1.0}};
+    auto settled = [&](int p, int q) {
+        return !(fabs(C[p][q]) > 1e-19 * (fabs(C[p][p]) + fabs(C[q][q])));
+    };
     for (int sweep = 0; sweep < 12; ++sweep) {
-        double off = 0.0;
-        for (int i = 0; i < dim; ++i)
-            for (int j = i + 1; j < dim; ++j) off += C[i][j] * C[i][j];
-        if (off == 0.0) break;
-        for (int p = 0; p < dim; ++p)
-            for (int q = p + 1; q < dim; ++q) {
-                if (C[p][q] == 0.0) continue;
-                const double tau = (C[q][q] - C[p][p]) / (2.0 * C[p][q]);
-                const double t = (tau >= 0.0 ? 1.0 : -1.0) / (fabs(tau) + sqrt(1.0 + tau * tau));
-                const double cs = 1.0 / sqrt(1.0 + t * t), sn = t * cs;
-                for (int k = 0; k < dim; ++k) {           // C <- J^T C J
-                    const double ckp = C[k][p], ckq = C[k][q];
-                    C[k][p] = cs * ckp - sn * ckq;
-                    C[k][q] = sn * ckp + cs * ckq;
-                }
-                for (int k = 0; k < dim; ++k) {
-                    const double cpk = C[p][k], cqk = C[q][k];
-                    C[p][k] = cs * cpk - sn * cqk;
-                    C[q][k] = sn * cpk + cs * cqk;
-                }
-                for (int k = 0; k < dim; ++k) {
-                    const double vkp = V[k][p], vkq = V[k][q];
-                    V[k][p] = cs * vkp - sn * vkq;
-                    V[k][q] = sn * vkp + cs * vkq;
-                }
-            }
+        if (settled(0, 1) && settled(0, 2) && settled(1, 2)) break;
+        jacobi_rot3<0, 1>(C, V);
+        if (three) {
+            jacobi_rot3<0, 2>(C, V);
+            jacobi_rot3<1, 2>(C, V);
+        }
     }
+    // the wanted end (the dummy never wins)
     int e = 0;
-    for (int i = 1; i < dim; ++i)
-        if (want_max ? (C[i][i] > C[e][e]) : (C[i][i] < C[e][e])) e = i;
-    *theta = C[e][e];
+    double best = C[0][0];
+    if (want_max ? (C[1][1] > best) : (C[1][1] < best)) { e = 1; best = C[1][1]; }
+    if (three && (want_max ? (C[2][2] > best) : (C[2][2] < best))) { e = 2; best = C[2][2]; }
+    *theta = best;
+    const double y0 = e == 0 ? V[0][0] : (e == 1 ? V[0][1] : V[0][2]);
+    const double y1 = e == 0 ? V[1][0] : (e == 1 ? V[1][1] : V[1][2]);
+    const double y2 = three ? (e == 0 ? V[2][0] : (e == 1 ? V[2][1] : V[2][2])) : 0.0;
     // c = s (Li^T y)
-    double y[3] = {V[0][e], V[1][e], dim == 3 ? V[2][e] : 0.0};
-    for (int i = 0; i < 3; ++i) {
-        double acc = 0.0;
-        for (int k = i; k < dim; ++k) acc = fma(Li[k][i], y[k], acc);
-        c[i] = (i < dim) ? acc * s[i] : 0.0;
-    }
-    const double pp = c[1] * c[1] * G[1][1] + 2.0 * c[1] * c[2] * G[1][2] + c[2] * c[2] * G[2][2];
+    c[0] = (Li[0][0] * y0 + Li[1][0] * y1 + Li[2][0] * y2) * s0;
+    c[1] = (Li[1][1] * y1 + Li[2][1] * y2) * s1;
+    c[2] = three ? (Li[2][2] * y2) * s2 : 0.0;
+    const double pp = c[1] * c[1] * g[3] + 2.0 * c[1] * c[2] * g[4] + c[2] * c[2] * g[5];
     *pn = sqrt(fmax(pp, 0.0));
     return true;
 }
@@ -1057,7 +1082,10 @@ __device__ __forceinline__ void cond_block_dot2(const int64_t s, const int64_t* 
 // START = true: Hx of both sides' x, partials x.x and x.Hx (part rows 0, 6
 // of each side's 12).  START = false: alpha = x.w (folded from the update
 // launch's partials), Hw, w' = w - alpha x, Hw' = Hw - alpha Hx and the 24 Gram
-// partials.  part: [24][nb] Gram, then [2][nb] x.w.
+// partials.  part: [24][nb] Gram, then [2][nb] x.w.  The 24 products of each
+// of the workgroup's 192 rows go through LDS and are summed in a fixed order
+// (three per wave: lanes take three rows each, then the xor butterfly).
+constexpr int kCondRows = kSpmvThreads / kSpmvGroup * 3;   // 192 rows per workgroup
 template <bool START>
 __global__ __launch_bounds__(kSpmvThreads) void graph_cond_spmv_kernel(
     const int64_t nt, const int64_t* __restrict__ rptr, const int64_t* __restrict__ col,
@@ -1065,20 +1093,21 @@ __global__ __launch_bounds__(kSpmvThreads) void graph_cond_spmv_kernel(
     const double* __restrict__ w, double* __restrict__ w2, double* __restrict__ hw,
     const double* __restrict__ p, const double* __restrict__ hp, double* __restrict__ part,
     const CondState* __restrict__ st) {
-    __shared__ double sh[2 * kCondGram * kSpmvThreads / 64];
+    __shared__ double s_prod[2 * kCondGram][kCondRows];
+    __shared__ double sh[2 * kSpmvThreads / 64];
     if (!START && st->done) return;
     const int64_t n = 3 * nt;
     const int64_t nb = gridDim.x;
-    double alpha[2] = {0.0, 0.0};
-    bool run[2] = {true, true};
+    double alpha0 = 0.0, alpha1 = 0.0;
+    bool run0 = true, run1 = true;
     if (!START) {
-        double al[2] = {pcg_fold_lane<kSpmvThreads>(part + 2 * kCondGram * nb, nb),
-                        pcg_fold_lane<kSpmvThreads>(part + (2 * kCondGram + 1) * nb, nb)};
-        block_sumK_fixed<kSpmvThreads, 2>(al, sh);
-        alpha[0] = al[0];
-        alpha[1] = al[1];
-        run[0] = !st->conv[0];
-        run[1] = !st->conv[1];
+        double al0 = pcg_fold_lane<kSpmvThreads>(part + 2 * kCondGram * nb, nb);
+        double al1 = pcg_fold_lane<kSpmvThreads>(part + (2 * kCondGram + 1) * nb, nb);
+        block_sum2_fixed<kSpmvThreads>(al0, al1, sh);
+        alpha0 = al0;
+        alpha1 = al1;
+        run0 = !st->conv[0];
+        run1 = !st->conv[1];
     }
     const double* src = START ? x : w;
     const int g = threadIdx.x & (kSpmvGroup - 1);
@@ -1092,25 +1121,30 @@ __global__ __launch_bounds__(kSpmvThreads) void graph_cond_spmv_kernel(
     for (int d = 1; d < kSpmvGroup; d <<= 1)
 #pragma unroll
         for (int j = 0; j < 6; ++j) a[j] += __shfl_xor(a[j], d, 64);
-    double v[2 * kCondGram];
-#pragma unroll
-    for (int j = 0; j < 2 * kCondGram; ++j) v[j] = 0.0;
-    if (rw < nt && g < 3) {
+    if (g < 3) {
+        const int lr = (int)(threadIdx.x / kSpmvGroup) * 3 + g;      // row within the workgroup
         const int64_t i = 3 * rw + g;
+        const bool ok = rw < nt;
 #pragma unroll
         for (int sd = 0; sd < 2; ++sd) {
             const double hv = (g == 0) ? a[3 * sd] : (g == 1) ? a[3 * sd + 1] : a[3 * sd + 2];
             const int64_t k = sd * n + i;
-            double* o = v + sd * kCondGram;
+            const bool run = sd == 0 ? run0 : run1;
+            const double al = sd == 0 ? alpha0 : alpha1;
+            double o[kCondGram];
+#pragma unroll
+            for (int j = 0; j < kCondGram; ++j) o[j] = 0.0;
             if (START) {
-                hx[k] = hv;
-                const double xi = x[k];
-                o[0] = xi * xi;
-                o[6] = xi * hv;
-            } else if (run[sd]) {
+                if (ok) {
+                    hx[k] = hv;
+                    const double xi = x[k];
+                    o[0] = xi * xi;
+                    o[6] = xi * hv;
+                }
+            } else if (ok && run) {
                 const double xi = x[k], hxi = hx[k], pi = p[k], hpi = hp[k];
-                const double wi = fma(-alpha[sd], xi, w[k]);
-                const double hwi = fma(-alpha[sd], hxi, hv);
+                const double wi = fma(-al, xi, w[k]);
+                const double hwi = fma(-al, hxi, hv);
                 w2[k] = wi;
                 hw[k] = hwi;
                 o[0] = xi * xi;
@@ -1126,114 +1160,154 @@ __global__ __launch_bounds__(kSpmvThreads) void graph_cond_spmv_kernel(
                 o[10] = 0.5 * (wi * hpi + pi * hwi);
                 o[11] = pi * hpi;
             }
+#pragma unroll
+            for (int j = 0; j < kCondGram; ++j) s_prod[sd * kCondGram + j][lr] = o[j];
         }
     }
-    block_sumK_fixed<kSpmvThreads, 2 * kCondGram>(v, sh);
-    if (threadIdx.x == 0)
+    __syncthreads();
+    // wave v sums quantities 3v .. 3v + 2 over the 192 rows: lane l takes rows
+    // l, l + 64, l + 128 in order, then the butterfly
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
 #pragma unroll
-        for (int j = 0; j < 2 * kCondGram; ++j) part[j * nb + blockIdx.x] = v[j];
+    for (int q = 0; q < 3; ++q) {
+        const int j = 3 * wv + q;
+        double v = s_prod[j][lane];
+        v += s_prod[j][lane + 64];
+        v += s_prod[j][lane + 128];
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
+        if (lane == 0) part[j * nb + blockIdx.x] = v;
+    }
 }
+static_assert(kSpmvThreads / 64 * 3 == 2 * kCondGram, "three Gram quantities per wave");
 
-// one workgroup: the 24 Gram partial rows folded in a fixed order (one wave
-// per row, lanes strided, then the xor butterfly) into st->tot
+// One workgroup per iteration: the 24 Gram partial rows folded in a fixed
+// order (one wave per row, lanes strided, then the xor butterfly), then the
+// two small problems (one lane each, on different waves), the stopping tests
+// and this iteration's update coefficients into the state; the update launch
+// only applies them.  k = 0: x normalised, theta its Rayleigh quotient.
 constexpr int kCondFoldThreads = 1024;
 __global__ __launch_bounds__(kCondFoldThreads) void graph_cond_fold_kernel(
-    const int64_t nb, const double* __restrict__ part, CondState* __restrict__ st, const int first) {
-    if (!first && st->done) return;
+    const int64_t nb, const double* __restrict__ part, CondState* __restrict__ st, const int32_t k,
+    const double tol, const int32_t max_iter, const double cond_max) {
+    __shared__ double s_tot[2 * kCondGram];
+    __shared__ int s_conv[2];
+    if (st->done) return;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     for (int j = wave; j < 2 * kCondGram; j += kCondFoldThreads / 64) {
-        double s = 0.0;
-        for (int64_t k = lane; k < nb; k += 64) s += part[j * nb + k];
+        // lane-strided sequential sums, four loads in flight (missing terms
+        // add +0.0: the order of the plain loop)
+        double v = 0.0;
+        const double* pj = part + j * nb;
+        for (int64_t q = lane; q < nb; q += 4 * 64) {
+            const double v0 = pj[q];
+            const double v1 = (q + 64 < nb) ? pj[q + 64] : 0.0;
+            const double v2 = (q + 128 < nb) ? pj[q + 128] : 0.0;
+            const double v3 = (q + 192 < nb) ? pj[q + 192] : 0.0;
+            v += v0;
+            v += v1;
+            v += v2;
+            v += v3;
+        }
 #pragma unroll
-        for (int d = 32; d >= 1; d >>= 1) s += __shfl_xor(s, d, 64);
-        if (lane == 0) st->tot[j] = s;
+        for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
+        if (lane == 0) s_tot[j] = v;
     }
-}
-
-// k = 0: normalise x (and Hx) from x.x, theta = x.Hx.  k > 0: Rayleigh-Ritz,
-// x, Hx, p, Hp updated on the own rows, the stopping tests.  Then r = Hx -
-// theta x, w = T r (side 0: the block-Jacobi inverse of the pose, the three
-// rows of a pose in one workgroup) and the x.w partials.
-__global__ __launch_bounds__(kPcgThreads) void graph_cond_update_kernel(
-    const int64_t n, const int32_t k, const double* __restrict__ minv, double* __restrict__ x,
-    double* __restrict__ hx, const double* __restrict__ w2, const double* __restrict__ hw,
-    double* __restrict__ p, double* __restrict__ hp, double* __restrict__ w,
-    double* __restrict__ part, CondState* __restrict__ st, const double tol,
-    const int32_t max_iter, const double cond_max) {
-    __shared__ double sh[2 * kPcgThreads / 64];
-    __shared__ double rs[kPcgThreads];
-    if (st->done) return;
-    const int64_t nb = gridDim.x;
-    const int64_t i = (int64_t)blockIdx.x * kPcgThreads + threadIdx.x;
-    double th[2];
-    bool run[2] = {!st->conv[0], !st->conv[1]};
-    bool conv_now[2] = {false, false};
-    int status = 0;
-    double xo[2] = {0.0, 0.0}, hxo[2] = {0.0, 0.0};
-    for (int sd = 0; sd < 2; ++sd) {
-        const double* t = st->tot + sd * kCondGram;
-        const int64_t kk = sd * n + i;
+    __syncthreads();
+    if (lane == 0 && wave < 2) {
+        const int sd = wave;
+        const double* t = s_tot + sd * kCondGram;
+        double th = st->lam[sd], c0 = 1.0, c1 = 0.0, c2 = 0.0, pinv = 0.0;
+        int upd = 0, conv = st->conv[sd];
         if (k == 0) {
-            const double sc = 1.0 / sqrt(t[0]);
-            th[sd] = t[6] / t[0];
-            if (i < n) {
-                xo[sd] = x[kk] * sc;
-                hxo[sd] = hx[kk] * sc;
-                x[kk] = xo[sd];
-                hx[kk] = hxo[sd];
+            c0 = 1.0 / sqrt(t[0]);
+            th = t[6] / t[0];
+            upd = 1;
+            conv = 0;
+        } else if (!conv) {
+            const double g[6] = {t[0], t[1], t[2], t[3], t[4], t[5]};
+            const double a[6] = {t[6], t[7], t[8], t[9], t[10], t[11]};
+            double c[3], theta, pn;
+            if (!cond_small(g, a, sd == 1, c, &theta, &pn)) {
+                conv = 1;                        // w' adds nothing: converged to rounding
+            } else {
+                th = theta;
+                c0 = c[0];
+                c1 = c[1];
+                c2 = c[2];
+                pinv = (pn > 0.0) ? 1.0 / pn : 0.0;
+                upd = 1;
+                const double old = st->theta[sd][(k - kCondWin) & (kCondHist - 1)];
+                if (k >= kCondWin && fabs(old - theta) <= tol * fabs(theta)) conv = 1;
+                st->iters_side[sd] = k;
             }
-            continue;
         }
-        th[sd] = st->lam[sd];
-        if (!run[sd]) continue;
-        const double g[6] = {t[0], t[1], t[2], t[3], t[4], t[5]};
-        const double a[6] = {t[6], t[7], t[8], t[9], t[10], t[11]};
-        double c[3], theta, pn;
-        if (!cond_small(g, a, sd == 1, c, &theta, &pn)) {
-            conv_now[sd] = true;               // w' adds nothing: converged to rounding
-            if (i < n) {
-                xo[sd] = x[kk];
-                hxo[sd] = hx[kk];
-            }
-            continue;
-        }
-        th[sd] = theta;
-        if (i < n) {
-            const double xi = x[kk], hxi = hx[kk], wi = w2[kk], hwi = hw[kk], pi = p[kk], hpi = hp[kk];
-            xo[sd] = fma(c[2], pi, fma(c[1], wi, c[0] * xi));
-            hxo[sd] = fma(c[2], hpi, fma(c[1], hwi, c[0] * hxi));
-            x[kk] = xo[sd];
-            hx[kk] = hxo[sd];
-            const double ip = (pn > 0.0) ? 1.0 / pn : 0.0;
-            p[kk] = fma(c[2], pi, c[1] * wi) * ip;
-            hp[kk] = fma(c[2], hpi, c[1] * hwi) * ip;
-        }
-        const double old = st->theta[sd][(k - kCondWin) & (kCondHist - 1)];
-        if (k >= kCondWin && fabs(old - theta) <= tol * fabs(theta)) conv_now[sd] = true;
+        st->theta[sd][k & (kCondHist - 1)] = th;
+        st->lam[sd] = th;
+        st->coef[sd][0] = c0;
+        st->coef[sd][1] = c1;
+        st->coef[sd][2] = c2;
+        st->coef[sd][3] = pinv;
+        st->upd[sd] = upd;
+        st->conv[sd] = conv;
+        s_conv[sd] = conv;
     }
-    // stopping tests (identical in every workgroup)
-    const bool c0 = !run[0] || conv_now[0], c1 = !run[1] || conv_now[1];
-    if (!(th[0] > 0.0)) status = 4;                                   // not positive definite
-    else if (th[1] >= cond_max * th[0]) status = 2;                   // cond >= cond_max for certain
-    else if (c0 && c1) status = 1;
-    else if (k >= max_iter) status = 3;
-    if (pcg_lead()) {
-        for (int sd = 0; sd < 2; ++sd) {
-            st->theta[sd][k & (kCondHist - 1)] = th[sd];
-            st->lam[sd] = th[sd];
-            if (run[sd]) st->iters_side[sd] = k;
-            if (conv_now[sd]) st->conv[sd] = 1;
-        }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const double t0 = st->lam[0], t1 = st->lam[1];
+        int status = 0;
+        if (!(t0 > 0.0)) status = 4;                                   // not positive definite
+        else if (t1 >= cond_max * t0) status = 2;                      // cond >= cond_max for certain
+        else if (s_conv[0] && s_conv[1]) status = 1;
+        else if (k >= max_iter) status = 3;
         st->iter = k;
         st->status = status;
         st->done = status != 0;
     }
-    if (status) return;
-    // r = Hx - theta x, w = T r, partials x.w
-    double xw[2] = {0.0, 0.0};
+}
+
+// Applies the fold launch's coefficients to the own rows (x, Hx, p, Hp of each
+// side it updated); unless the estimate is done, r = Hx - theta x, w = T r
+// (side 0: the block-Jacobi inverse of the pose, the three rows of a pose in
+// one workgroup; side 1: w = r) and the x.w partials.
+__global__ __launch_bounds__(kPcgThreads) void graph_cond_update_kernel(
+    const int64_t n, const int32_t k, const double* __restrict__ minv, double* __restrict__ x,
+    double* __restrict__ hx, const double* __restrict__ w2, const double* __restrict__ hw,
+    double* __restrict__ p, double* __restrict__ hp, double* __restrict__ w,
+    double* __restrict__ part, const CondState* __restrict__ st) {
+    __shared__ double sh[2 * kPcgThreads / 64];
+    __shared__ double rs[kPcgThreads];
+    const int32_t iter = st->iter;
+    if (iter != k) return;                   // the fold launch stopped before this iteration
+    const int64_t nb = gridDim.x;
+    const int64_t i = (int64_t)blockIdx.x * kPcgThreads + threadIdx.x;
+    const bool done = st->done;
+    double xw0 = 0.0, xw1 = 0.0;
+#pragma unroll
     for (int sd = 0; sd < 2; ++sd) {
-        const bool act = (k == 0) || (run[sd] && !conv_now[sd]);
-        const double ri = (i < n && act) ? fma(-th[sd], xo[sd], hxo[sd]) : 0.0;
+        const bool upd = st->upd[sd];
+        const double c0 = st->coef[sd][0], c1 = st->coef[sd][1], c2 = st->coef[sd][2];
+        const double pinv = st->coef[sd][3], th = st->lam[sd];
+        const int64_t kk = sd * n + i;
+        double xo = 0.0, hxo = 0.0;
+        if (i < n && upd) {
+            const double xi = x[kk], hxi = hx[kk];
+            if (k == 0) {
+                xo = xi * c0;
+                hxo = hxi * c0;
+            } else {
+                const double wi = w2[kk], hwi = hw[kk], pi = p[kk], hpi = hp[kk];
+                xo = fma(c2, pi, fma(c1, wi, c0 * xi));
+                hxo = fma(c2, hpi, fma(c1, hwi, c0 * hxi));
+                p[kk] = fma(c2, pi, c1 * wi) * pinv;
+                hp[kk] = fma(c2, hpi, c1 * hwi) * pinv;
+            }
+            x[kk] = xo;
+            hx[kk] = hxo;
+        }
+        if (done) continue;
+        const bool act = upd && !st->conv[sd];
+        const double ri = (i < n && act) ? fma(-th, xo, hxo) : 0.0;
         double wi = ri;
         if (sd == 0) {
             rs[threadIdx.x] = ri;
@@ -1248,14 +1322,16 @@ __global__ __launch_bounds__(kPcgThreads) void graph_cond_update_kernel(
             }
         }
         if (i < n && act) {
-            w[sd * n + i] = wi;
-            xw[sd] = xo[sd] * wi;
+            w[kk] = wi;
+            if (sd == 0) xw0 = xo * wi;
+            else xw1 = xo * wi;
         }
     }
-    block_sum2_fixed<kPcgThreads>(xw[0], xw[1], sh);
+    if (done) return;
+    block_sum2_fixed<kPcgThreads>(xw0, xw1, sh);
     if (threadIdx.x == 0) {
-        part[2 * kCondGram * nb + blockIdx.x] = xw[0];
-        part[(2 * kCondGram + 1) * nb + blockIdx.x] = xw[1];
+        part[2 * kCondGram * nb + blockIdx.x] = xw0;
+        part[(2 * kCondGram + 1) * nb + blockIdx.x] = xw1;
     }
 }
 
