@@ -405,6 +405,7 @@ def bench_graph(n_poses=50000, iters=3, device=0):
             "ms_per_iteration": float(np.mean(per)) * 1e3, "structure_build_ms": t_struct * 1e3,
             "structure_build_first_ms": t_first * 1e3,
             "structure_build_max_ms": max(t_sets) * 1e3,
+            "structure_build_each_ms": [t * 1e3 for t in t_sets],
             "breakdown_ms": brk[-1], "is_calc": bool(st[0]),
             "cond": conds[-1]["cond"], "cond_estimate": conds[-1],
             "cond_estimate_first_update": cond_first,

@@ -112,6 +112,11 @@ int slam_pf_update(slam_pf* h, const double* z, slam_pf_result* res);           
 int slam_pf_resample_indices(slam_pf* h, double u_resample, int64_t* idx_out, int32_t* n_special);
 /* numpy-order np.sum of the current weights (particle_filter.py:234). */
 int slam_pf_weight_sum(slam_pf* h, double* sum_out);
+/* Diagnostics: the device RNG's six standard normals of particle pairs
+ * [p0, p0 + count) at RNG step rstep (the perf-mode motion noise, Philox-4x32-10
+ * / Philox-2x32-10 + Box-Muller; not a reference interface), out: count x 6. */
+int slam_debug_pair_normals(int device, uint64_t p0, int64_t count, uint32_t rstep, uint64_t seed,
+                            double* out);
 
 /* Device-resident multi-step run (bench path): observations for n_steps steps
  * are uploaded once; steps are enqueued back to back with no host sync. */

@@ -505,6 +505,18 @@ int launch_mt(slam_pf* h) {
     return SLAM_OK;
 }
 
+// The device-RNG normals of particle pairs [p0, p0 + count) (slam_debug_pair_normals)
+__global__ __launch_bounds__(256) void debug_pair_normals_kernel(const uint64_t p0, const int64_t count,
+                                                                const uint32_t rstep, const uint64_t seed,
+                                                                double* __restrict__ out) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= count) return;
+    double g[6];
+    pair_normals(p0 + (uint64_t)i, rstep, seed, g);
+#pragma unroll
+    for (int j = 0; j < 6; ++j) out[6 * i + j] = g[j];
+}
+
 // One whole device-decided step (scans gate on the flag; no host decision).
 int launch_step(slam_pf* h, bool host_noise) {
     int rc;
@@ -966,6 +978,25 @@ int slam_pf_update(slam_pf* h, const double* z, slam_pf_result* res) {
     if ((rc = launch_fused(h, kMotionNone, false))) return rc;
     if ((rc = launch_reduce(h, 0))) return rc;
     return sync_results(h, 0, 1, res);
+}
+
+int slam_debug_pair_normals(int device, uint64_t p0, int64_t count, uint32_t rstep, uint64_t seed,
+                            double* out) {
+    SLAM_ARG_CHECK(out && count >= 0 && count <= (int64_t(1) << 26),
+                   "slam_debug_pair_normals: bad arguments");
+    if (count == 0) return SLAM_OK;
+    int ndev = 0;
+    SLAM_HIP_TRY(hipGetDeviceCount(&ndev));
+    SLAM_ARG_CHECK(device >= 0 && device < ndev, "slam_debug_pair_normals: no such HIP device");
+    SLAM_HIP_TRY(hipSetDevice(device));
+    double* d = nullptr;
+    SLAM_HIP_TRY(hipMalloc(&d, 6 * count * sizeof(double)));
+    debug_pair_normals_kernel<<<grid_for(count, 256), 256>>>(p0, count, rstep, seed, d);
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess) e = hipMemcpy(out, d, 6 * count * sizeof(double), hipMemcpyDeviceToHost);
+    (void)hipFree(d);
+    if (e != hipSuccess) return fail(SLAM_ERR_HIP, std::string("slam_debug_pair_normals: ") + hipGetErrorString(e));
+    return SLAM_OK;
 }
 
 int slam_pf_weight_sum(slam_pf* h, double* sum_out) {

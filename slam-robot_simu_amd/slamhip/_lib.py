@@ -90,6 +90,7 @@ SIGNATURES = {
     "slam_pf_update": (C.c_int, [_P, _D, C.POINTER(PFResult)]),
     "slam_pf_resample_indices": (C.c_int, [_P, C.c_double, _I64, _I32]),
     "slam_pf_weight_sum": (C.c_int, [_P, _D]),
+    "slam_debug_pair_normals": (C.c_int, [C.c_int, C.c_uint64, C.c_int64, C.c_uint32, C.c_uint64, _D]),
     "slam_pf_load_observations": (C.c_int, [_P, C.c_int32, _D]),
     "slam_pf_run": (C.c_int, [_P, C.c_int32, C.c_int32, _D, C.POINTER(PFResult)]),
     "slam_pf_enable_timing": (C.c_int, [_P, C.c_int32]),
