@@ -101,10 +101,20 @@ __device__ __forceinline__ void fast_sincos(const double x, double* sp, double* 
     *cp = ((q + 1) & 2) ? -ca : ca;
 }
 
-// sin/cos of a turn increment: |x| <= pi/4 goes straight to the kernels (no
-// reduction, no quadrant selects), anything larger to fast_sincos.
+// sin/cos of a turn increment: |x| <= 1/16 (every increment of the bench's
+// motion model) by the Taylor polynomials in z = x^2 (truncation below
+// 3e-19 relative; cos as 1 + z q(z), so the only rounding of note is the last
+// one: < 1 ulp, and sin to x^9); |x| <= pi/4 straight to the kernels (no
+// reduction, no quadrant selects); anything larger to fast_sincos.
 __device__ __forceinline__ void small_sincos(const double x, double* sp, double* cp) {
-    if (fabs(x) <= fm::kPio4) {
+    if (fabs(x) <= 0.0625) {
+        const double z = x * x;
+        const double ps = fma_k(z, fma_k(z, fma_kk(z, 1.0 / 362880.0, -1.0 / 5040.0), 1.0 / 120.0),
+                                -1.0 / 6.0);
+        *sp = fma(x * z, ps, x);
+        const double pc = fma_k(z, fma_k(z, fma_kk(z, 1.0 / 40320.0, -1.0 / 720.0), 1.0 / 24.0), -0.5);
+        *cp = fma(z, pc, 1.0);
+    } else if (fabs(x) <= fm::kPio4) {
         *sp = fm::ksin0(x);
         *cp = fm::kcos(x, 0.0);
     } else {
