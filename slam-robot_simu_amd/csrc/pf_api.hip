@@ -542,8 +542,6 @@ int sync_results(slam_pf* h, int32_t first, int32_t count, slam_pf_result* out) 
             rc = fail(SLAM_ERR_HIP, "exact-cumsum launch: release token timed out");
         if (h->res_host[i].status & 256)
             rc = fail(SLAM_ERR_HIP, "mt19937 draw: candidate bound exhausted");
-        if (h->res_host[i].status & 512)
-            rc = fail(SLAM_ERR_HIP, "mt19937 draw: look-back wait expired");
         if (h->res_host[i].status & 1)
             rc = fail(SLAM_ERR_INDEX, "resample position beyond the last cumulative weight "
                                       "(IndexError in particle_filter.py:219); clamped to NP-1");
