@@ -87,11 +87,20 @@ __device__ __forceinline__ void philox2x32(uint32_t& c0, uint32_t& c1, uint32_t 
 
 // One Box-Muller pair from two 32-bit words: uniforms (a + 1) 2^-32 and
 // (b + 1) 2^-32 in (0, 1] (radius resolution 2^-32: |g| <= 6.66, a tail mass of
-// 3e-11 per draw); log, sqrt and sin/cos from fastmath.hpp (< 2 ulp).
-__device__ __forceinline__ void bm_pair(uint32_t a, uint32_t b, double& gc, double& gs) {
+// 3e-11 per draw); log and sin/cos from the LDS tables of fastmath.hpp
+// (rng_log_tab, rng_sincos2pi_tab: < 1.5 ulp), sqrt_pos.
+__device__ __forceinline__ void bm_pair(uint32_t a, uint32_t b, const RngTabs& T, double& gc,
+                                        double& gs) {
+#ifdef SLAM_RNG_NO_TABLES                                   // A/B diagnostic: the round-2 forms
+    (void)T;
     const double rad = sqrt_pos(-2.0 * rng_log_scaled((double)a + 1.0, -32));
     double s, c;
     rng_sincos2pi(((double)b + 1.0) * 0x1p-32, &s, &c);
+#else
+    const double rad = sqrt_pos(-2.0 * rng_log_tab(a, T));
+    double s, c;
+    rng_sincos2pi_tab(b, T, &s, &c);
+#endif
     gc = rad * c;
     gs = rad * s;
 }
@@ -106,14 +115,14 @@ enum : uint32_t { kStreamPredict = 1, kStreamResample = 2, kStreamPredict2 = 3 }
 // particle 2p+1 (B.s, C.c, C.s): three pairs per two particles, no normal
 // formed and dropped.
 __device__ __forceinline__ void pair_normals(const uint64_t p, const uint32_t rstep,
-                                             const uint64_t seed, double g[6]) {
+                                             const uint64_t seed, const RngTabs& T, double g[6]) {
     const u32x4 r = philox4x32(u32x4{(uint32_t)p, (uint32_t)(p >> 32), kStreamPredict, rstep},
                                (uint32_t)seed, (uint32_t)(seed >> 32));
     uint32_t c0 = (uint32_t)p, c1 = rstep;
     philox2x32(c0, c1, ((uint32_t)seed ^ (uint32_t)(seed >> 32) * 0x85EBCA6Bu) ^ (kStreamPredict2 * 0x27D4EB2Fu));
-    bm_pair(r.x, r.y, g[0], g[1]);
-    bm_pair(r.z, r.w, g[2], g[3]);
-    bm_pair(c0, c1, g[4], g[5]);
+    bm_pair(r.x, r.y, T, g[0], g[1]);
+    bm_pair(r.z, r.w, T, g[2], g[3]);
+    bm_pair(c0, c1, T, g[4], g[5]);
 }
 
 

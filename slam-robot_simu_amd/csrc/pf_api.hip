@@ -509,10 +509,13 @@ int launch_mt(slam_pf* h) {
 __global__ __launch_bounds__(256) void debug_pair_normals_kernel(const uint64_t p0, const int64_t count,
                                                                 const uint32_t rstep, const uint64_t seed,
                                                                 double* __restrict__ out) {
+    __shared__ RngTabsLds s_rng;
+    const RngTabs T = rng_tabs_stage(&s_rng, (int)threadIdx.x, 256);
+    __syncthreads();
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (i >= count) return;
     double g[6];
-    pair_normals(p0 + (uint64_t)i, rstep, seed, g);
+    pair_normals(p0 + (uint64_t)i, rstep, seed, T, g);
 #pragma unroll
     for (int j = 0; j < 6; ++j) out[6 * i + j] = g[j];
 }

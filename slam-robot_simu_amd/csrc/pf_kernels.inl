@@ -932,6 +932,13 @@ __global__ __launch_bounds__(256) SLAM_FUSED_ATTR void pf_fused_kernel(
     const int64_t base = (int64_t)blockIdx.x * (256 * P);
     const int64_t i0 = base + P * (int64_t)threadIdx.x;
     const int wave_s = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+    // the device RNG's tables in LDS (every lane reaches the barrier)
+    __shared__ RngTabsLds s_rng;
+    RngTabs rtab{};
+    if constexpr (MOTION != kMotionNone && !HOSTNOISE) {
+        rtab = rng_tabs_stage(&s_rng, (int)threadIdx.x, 256);
+        __syncthreads();
+    }
     bool valid[P];
     int64_t idx[P];
 #pragma unroll
@@ -1093,13 +1100,13 @@ __global__ __launch_bounds__(256) SLAM_FUSED_ATTR void pf_fused_kernel(
 #ifdef SLAM_PROBE_NO_RNG                                      // instruction-count probe only
                 for (int j = 0; j < 6; ++j) h[j] = 0.0;
 #else
-                pair_normals((gi >> 1) + pr, rstep, seed, h);
+                pair_normals((gi >> 1) + pr, rstep, seed, rtab, h);
 #endif
 #pragma unroll
                 for (int j = 0; j < 6; ++j) g[2 * pr + j / 3][j % 3] = h[j];
             }
         } else {
-            pair_normals(gi >> 1, rstep, seed, h);
+            pair_normals(gi >> 1, rstep, seed, rtab, h);
             const bool odd = gi & 1;
 #pragma unroll
             for (int j = 0; j < 3; ++j) g[0][j] = odd ? h[3 + j] : h[j];
