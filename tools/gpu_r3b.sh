@@ -16,3 +16,7 @@ rc=$?; echo "bench rc=$rc"; [ $rc -eq 0 ] || { tail -5 $out/bench.err; exit $rc;
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $out/prof -o prof -- python bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-secondary > $out/prof_bench.json 2> $out/prof.err
 rc=$?; echo "rocprof rc=$rc"; [ $rc -eq 0 ] || { tail -5 $out/prof.err; exit $rc; }
 TAG=${tag}_pmc BENCH_ARGS="--no-secondary" PMC_TIMEOUT=200 tools/pmc.sh
+rc=$?; echo "pmc rc=$rc"; [ $rc -eq 0 ] || exit $rc
+# the driver's own command: default flags (cpu_baseline and secondary rows)
+timeout -k 10 600 python bench.py > $out/bench_default.json 2> $out/bench_default.err
+rc=$?; echo "default bench rc=$rc"; exit $rc
