@@ -994,7 +994,7 @@ __device__ __forceinline__ void dist_record(const int64_t n, const DeferParts& d
                                             const double* __restrict__ ys,
                                             const double* __restrict__ ts, const DistPeers& P,
                                             const uint64_t epoch, double* sh) {
-    __shared__ double s_red[12][kFinWaves];
+    __shared__ double s_q[12][kFinThreads];             // lane sums (transposed reduction)
     __shared__ double s_wm[kFinWaves];
     __shared__ unsigned long long s_cand[kDistWin], s_mblk;
     __shared__ DistRec rec;
@@ -1094,15 +1094,7 @@ __device__ __forceinline__ void dist_record(const int64_t n, const DeferParts& d
         for (int j = 2; j < 11; ++j) acc[j] *= rl;
     }
 #pragma unroll
-    for (int j = 0; j < 12; ++j) {
-        double r = acc[j];
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const double o = __shfl_xor(r, d, 64);
-            r = (lane & d) ? (o + r) : (r + o);
-        }
-        if (lane == 0) s_red[j][wave] = r;
-    }
+    for (int j = 0; j < 12; ++j) s_q[j][tid] = acc[j];
     // first block holding M, and the first kDistWin candidate blocks (index order)
     if (M > 0.0) {
         unsigned long long mb = ~0ull;
@@ -1134,12 +1126,23 @@ __device__ __forceinline__ void dist_record(const int64_t n, const DeferParts& d
     }
     __syncthreads();
     PROBE_AT(2);
-    if (tid < 12) {
-        double r = s_red[tid][0];
+    // the 12 sums (written to s_q before the candidate rounds' barriers): wave w
+    // reduces quantities w and w + 8 -- lane-strided reads, then one butterfly
+    // with the lower lane on the left (a fixed order; twelve butterflies per
+    // wave were a 3.7 us dependent chain of lane permutes)
+    for (int j = wave; j < 12; j += kFinWaves) {
+        double r = s_q[j][lane];
 #pragma unroll
-        for (int w = 1; w < kFinWaves; ++w) r = r + s_red[tid][w];
-        if (tid < 11) rec.q[tid] = r;
-        else rec.T = r;
+        for (int m = 1; m < kFinThreads / 64; ++m) r = r + s_q[j][lane + 64 * m];
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const double o = __shfl_xor(r, d, 64);
+            r = (lane & d) ? (o + r) : (r + o);
+        }
+        if (lane == 0) {
+            if (j < 11) rec.q[j] = r;
+            else rec.T = r;
+        }
     }
     if (nch > nfull) {
         __shared__ double tl[1024];
