@@ -50,7 +50,6 @@ struct MtBuffers {
     uint32_t* q = nullptr;          // x^(R S) mod phi: its set bits as 16-bit offsets (R > 1)
     int32_t n_idx = 0;              // offsets (a multiple of 16, padded)
     unsigned* bcnt = nullptr;       // accepted candidates per count block
-    int64_t* boff = nullptr;        // their exclusive prefix
     double* normals = nullptr;      // G normals of the last request
     double* pre = nullptr;          // n_pre doubles of the last request (standalone use)
     int64_t g_cap = 0;              // normals per request this allocation holds

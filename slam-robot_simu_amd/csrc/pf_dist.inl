@@ -1057,9 +1057,7 @@ __device__ __forceinline__ void dist_record(const int64_t n, const DeferParts& d
             add(dp.pmax[b], qq);
         }
     }
-    double mx = mlane;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) mx = fmax(mx, __shfl_xor(mx, d, 64));
+    const double mx = wave_max_f64(mlane);
     if (lane == 0) s_wm[wave] = mx;
     // ---- np.sum buffer partials: 4 lanes per 8192-element buffer, pairwise tree
     for (int64_t c0 = 0; c0 < nfull; c0 += kFinBufPerRound) {
@@ -1073,10 +1071,14 @@ __device__ __forceinline__ void dist_record(const int64_t n, const DeferParts& d
             }
             v = (L[0] + L[1]) + (L[2] + L[3]);
         }
-#pragma unroll
-        for (int d = 1; d < kFinLeafLanes; d <<= 1) {
-            const double o = __shfl_xor(v, d, 64);
-            v = (part & d) ? (o + v) : (v + o);              // left operand = lower lane
+        static_assert(kFinLeafLanes == 4, "two quad swaps");
+        {
+            const double o = dpp_f64<kDppXor1>(v);
+            v = (part & 1) ? (o + v) : (v + o);              // left operand = lower lane
+        }
+        {
+            const double o = dpp_f64<kDppXor2>(v);
+            v = (part & 2) ? (o + v) : (v + o);
         }
         if (part == 0 && c < nfull) sh[c] = v;
     }
@@ -1136,7 +1138,7 @@ __device__ __forceinline__ void dist_record(const int64_t n, const DeferParts& d
         for (int m = 1; m < kFinThreads / 64; ++m) r = r + s_q[j][lane + 64 * m];
 #pragma unroll
         for (int d = 1; d < 64; d <<= 1) {
-            const double o = __shfl_xor(r, d, 64);
+            const double o = xor_f64(r, d);
             r = (lane & d) ? (o + r) : (r + o);
         }
         if (lane == 0) {

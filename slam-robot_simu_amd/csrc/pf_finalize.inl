@@ -138,9 +138,7 @@ __global__ __launch_bounds__(kFinThreads) void finalize_deferred_kernel(
             for (int j = 2; j < 11; ++j) acc[j] += r * dp.ps[j][b];
         }
     }
-    double mx = mlane;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) mx = fmax(mx, __shfl_xor(mx, d, 64));
+    const double mx = wave_max_f64(mlane);
     if (lane == 0) s_wmax[wave] = mx;
     // ---- np.sum: 8192-element buffers, 128 per round, pairwise inside
     double s = 0.0;
@@ -156,10 +154,14 @@ __global__ __launch_bounds__(kFinThreads) void finalize_deferred_kernel(
             }
             v = (L[0] + L[1]) + (L[2] + L[3]);
         }
-#pragma unroll
-        for (int d = 1; d < kFinLeafLanes; d <<= 1) {
-            const double o = __shfl_xor(v, d, 64);
-            v = (part & d) ? (o + v) : (v + o);          // left operand = lower lane
+        static_assert(kFinLeafLanes == 4, "two quad swaps");
+        {
+            const double o = dpp_f64<kDppXor1>(v);
+            v = (part & 1) ? (o + v) : (v + o);          // left operand = lower lane
+        }
+        {
+            const double o = dpp_f64<kDppXor2>(v);
+            v = (part & 2) ? (o + v) : (v + o);
         }
         if (c0 > 0) __syncthreads();                     // lane 0 is done with the previous round
         if (part == 0 && tid / kFinLeafLanes < cnt) sh[tid / kFinLeafLanes] = v;
@@ -228,7 +230,7 @@ __global__ __launch_bounds__(kFinThreads) void finalize_deferred_kernel(
             for (int m = 1; m < kFinThreads / 64; ++m) r = r + s_q[j][lane + 64 * m];
 #pragma unroll
             for (int d = 1; d < 64; d <<= 1) {
-                const double o = __shfl_xor(r, d, 64);
+                const double o = xor_f64(r, d);
                 r = (lane & d) ? (o + r) : (r + o);
             }
             if (lane == 0) s_tot[j] = r;

@@ -187,6 +187,62 @@ __device__ __forceinline__ void max_first(double& v, int64_t& i, const double ov
     }
 }
 
+// ---- wave reductions through DPP lane moves (VALU, no LDS round trip):
+// quad_perm [1,0,3,2] is the lane-xor-1 partner (bit-identical to
+// __shfl_xor(v, 1)); max / min over the wave by quad swaps, the half-row and
+// row mirrors, then the four row results read into scalars.
+constexpr int kDppXor1 = 0xB1, kDppXor2 = 0x4E, kDppHalfMirror = 0x141, kDppMirror = 0x140;
+template <int CTRL>
+__device__ __forceinline__ uint64_t dpp_u64(const uint64_t v) {
+    const int lo = __builtin_amdgcn_mov_dpp((int)(uint32_t)v, CTRL, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_mov_dpp((int)(uint32_t)(v >> 32), CTRL, 0xF, 0xF, false);
+    return ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo;
+}
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(const double v) {
+    return __longlong_as_double((long long)dpp_u64<CTRL>((uint64_t)__double_as_longlong(v)));
+}
+__device__ __forceinline__ uint64_t readlane_u64(const uint64_t v, const int l) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l);
+    return ((uint64_t)hi << 32) | lo;
+}
+// the lane-xor-d partner of a butterfly step (d a constant after unrolling):
+// quad swaps by DPP for d = 1, 2, the LDS permute beyond
+__device__ __forceinline__ double xor_f64(const double v, const int d) {
+    if (d == 1) return dpp_f64<kDppXor1>(v);
+    if (d == 2) return dpp_f64<kDppXor2>(v);
+    return __shfl_xor(v, d, 64);
+}
+// max over the wave (every lane gets it); fmax semantics as the butterfly's
+__device__ __forceinline__ double wave_max_f64(double v) {
+    v = fmax(v, dpp_f64<kDppXor1>(v));
+    v = fmax(v, dpp_f64<kDppXor2>(v));
+    v = fmax(v, dpp_f64<kDppHalfMirror>(v));
+    v = fmax(v, dpp_f64<kDppMirror>(v));
+    const uint64_t b = (uint64_t)__double_as_longlong(v);
+    const double r0 = __longlong_as_double((long long)readlane_u64(b, 0));
+    const double r1 = __longlong_as_double((long long)readlane_u64(b, 16));
+    const double r2 = __longlong_as_double((long long)readlane_u64(b, 32));
+    const double r3 = __longlong_as_double((long long)readlane_u64(b, 48));
+    return fmax(fmax(r0, r1), fmax(r2, r3));
+}
+__device__ __forceinline__ int64_t wave_min_i64(int64_t v) {
+    int64_t o;
+    o = (int64_t)dpp_u64<kDppXor1>((uint64_t)v);
+    v = o < v ? o : v;
+    o = (int64_t)dpp_u64<kDppXor2>((uint64_t)v);
+    v = o < v ? o : v;
+    o = (int64_t)dpp_u64<kDppHalfMirror>((uint64_t)v);
+    v = o < v ? o : v;
+    o = (int64_t)dpp_u64<kDppMirror>((uint64_t)v);
+    v = o < v ? o : v;
+    const int64_t r0 = (int64_t)readlane_u64((uint64_t)v, 0), r1 = (int64_t)readlane_u64((uint64_t)v, 16);
+    const int64_t r2 = (int64_t)readlane_u64((uint64_t)v, 32), r3 = (int64_t)readlane_u64((uint64_t)v, 48);
+    const int64_t a = r0 < r1 ? r0 : r1, b = r2 < r3 ? r2 : r3;
+    return a < b ? a : b;
+}
+
 // Deferred-path epilogue of a 256-lane, kPartPer-particle fused block (see
 // DeferParts).  Lane t holds particles kDeferPPT t + k (k < kDeferPPT); invalid
 // ones carry w = 0.  Three barriers: (1) the wave maxima, (2) the lane-pair
@@ -223,19 +279,12 @@ __device__ void defer_epilogue(const int64_t base, const int64_t n, const double
             mi = i;
         }
     }
-    double mv = m;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) mv = fmax(mv, __shfl_xor(mv, d, 64));
+    const double mv = wave_max_f64(m);
     if (lane == 0) s_mv[wave] = mv;
     __syncthreads();                                                    // (1)
     const double M = fmax(fmax(s_mv[0], s_mv[1]), fmax(s_mv[2], s_mv[3]));
     // first index holding M in this wave
-    int64_t cand = (m == M) ? mi : INT64_MAX;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const int64_t o = __shfl_xor(cand, d, 64);
-        cand = o < cand ? o : cand;
-    }
+    const int64_t cand = wave_min_i64((m == M) ? mi : INT64_MAX);
     if (lane == 0) s_mi[wave] = cand;
     // moments scaled by the block max, lane-pair sums into LDS
     const double rs = (M > 0.0) ? 1.0 / M : 0.0;
@@ -263,7 +312,7 @@ __device__ void defer_epilogue(const int64_t base, const int64_t n, const double
     }
 #pragma unroll
     for (int j = 0; j < kQ; ++j) {
-        const double o = __shfl_xor(q[j], 1, 64);
+        const double o = dpp_f64<kDppXor1>(q[j]);
         q[j] = (lane & 1) ? o + q[j] : q[j] + o;                     // (2l) + (2l+1)
     }
     if (!(lane & 1)) {
@@ -286,8 +335,7 @@ __device__ void defer_epilogue(const int64_t base, const int64_t n, const double
             dp.pxe[2][blk] = tv[k];
         }
     }
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) pre = fmax(pre, __shfl_xor(pre, d, 64));
+    pre = wave_max_f64(pre);
     if (lane == 0) s_pre[wave] = pre;
     if (t < kQ * 16) {
         // quantity t / 16, segment t % 16: pairs seg, seg + 16, ..., seg + 112
@@ -319,7 +367,7 @@ __device__ void defer_epilogue(const int64_t base, const int64_t n, const double
         }
 #pragma unroll
         for (int d = 1; d < kLeaves; d <<= 1) {
-            const double o = __shfl_xor(v, d, 64);
+            const double o = xor_f64(v, d);
             v = (lane & d) ? (o + v) : (v + o);
         }
         if (t == 64) dp.leaf[blk] = v;

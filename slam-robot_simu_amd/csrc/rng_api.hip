@@ -1,6 +1,6 @@
 // rng_api.hip -- NumPy's legacy RandomState stream on the device (mt19937.hpp).
 //
-// A request (mt_enqueue) is five launches, none of which needs the host:
+// A request (mt_enqueue) is four launches, none of which needs the host:
 //   mt_round_kernel   when fewer words than a request can read lie ahead: R
 //                     workgroups each generate S words of the untempered
 //                     MT19937 sequence (one 624-word block per barrier) from
@@ -8,8 +8,9 @@
 //                     R S words ahead (mt_stream.hpp);
 //   mt_count_kernel   per candidate pair (4 words): the polar test
 //                     0 < x1^2 + x2^2 < 1, accepted candidates per block;
-//   mt_scan_kernel    exclusive prefix of the block counts;
-//   mt_emit_kernel    rank of every accepted candidate; the first P give the
+//   mt_emit_kernel    the block's offset (the counts of the blocks before it,
+//                     summed by the block itself: no scan launch), the rank of
+//                     every accepted candidate; the first P give the
 //                     normals f x2, f x1 (f = sqrt(-2 log(r2) / r2), glibc's
 //                     log), the P-th ends the draw;
 //   mt_finish_kernel  the pre-draw doubles, the cached normal in slot 0, the
@@ -35,12 +36,12 @@ constexpr int kMtGenThreads = 640;   // one lane per word of a block
 constexpr int kMtCandPerThread = 4;
 constexpr int kMtCountThreads = 256;
 constexpr int kMtCandPerBlock = kMtCountThreads * kMtCandPerThread;
-constexpr int kMtScanThreads = 1024;
 // requests one parallel round feeds: the jump (~160 us, LDS-bound) is paid
 // once per round, the sequential generation grows with it; 4 -> 16 took the
-// device stream from 0.229 to 0.201 ms per 2^20-particle step (the ring is
-// ~2 GB at that request size)
-constexpr int64_t kMtRoundsAhead = 16;
+// device stream from 0.229 to 0.201 ms per 2^20-particle step, 16 -> 32 from
+// 0.150 to 0.145 (the ring is ~4 GB at that request size, the one-time
+// priming ~150 ms)
+constexpr int64_t kMtRoundsAhead = 32;
 
 // ------------------------------------------------------------------ kernels
 
@@ -245,52 +246,21 @@ __global__ __launch_bounds__(kMtCountThreads) void mt_count_kernel(
     }
 }
 
-__global__ __launch_bounds__(kMtScanThreads) void mt_scan_kernel(
-    MtDeviceState* __restrict__ st, const unsigned* __restrict__ bcnt, const int64_t nb,
-    int64_t* __restrict__ boff, const int64_t g, int32_t* __restrict__ status) {
-    __shared__ int64_t s_w[kMtScanThreads / 64];
-    __shared__ int64_t s_carry;
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    if (threadIdx.x == 0) s_carry = 0;
-    __syncthreads();
-    for (int64_t base = 0; base < nb; base += kMtScanThreads) {
-        const int64_t i = base + threadIdx.x;
-        int64_t v = i < nb ? (int64_t)bcnt[i] : 0;
-        const int64_t own = v;
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const int64_t o = __shfl_up(v, d, 64);
-            if (lane >= d) v += o;
-        }
-        if (lane == 63) s_w[wave] = v;
-        __syncthreads();
-        int64_t add = s_carry, all = 0;
-        for (int w = 0; w < kMtScanThreads / 64; ++w) {
-            add += (w < wave) ? s_w[w] : 0;
-            all += s_w[w];
-        }
-        if (i < nb) boff[i] = add + v - own;
-        __syncthreads();
-        if (threadIdx.x == 0) s_carry += all;
-        __syncthreads();
-    }
-    if (threadIdx.x == 0) {
-        const bool shrt = s_carry < mt_pairs(st, g);
-        st->short_draw = shrt ? 1 : 0;
-        if (shrt && status) atomicOr(status, 256);
-    }
-}
-
 __global__ __launch_bounds__(kMtCountThreads) void mt_emit_kernel(
     MtDeviceState* __restrict__ st, const uint32_t* __restrict__ X, const int64_t cap,
     const int32_t* __restrict__ pre_flag, const int64_t n_pre, const int64_t ncand,
-    const int64_t* __restrict__ boff, const int64_t g, const GlibcLogTable* __restrict__ tab,
-    double* __restrict__ normals) {
+    const unsigned* __restrict__ bcnt, const int64_t nb, const int64_t g,
+    const GlibcLogTable* __restrict__ tab, double* __restrict__ normals, int32_t* __restrict__ status) {
     const int64_t pw = mt_pre_words(pre_flag, n_pre);
     const int64_t w0 = st->p + pw;
     const int h = st->has_gauss ? 1 : 0;
     const int64_t P = mt_pairs(st, g);
     const int64_t c0 = (int64_t)blockIdx.x * kMtCandPerBlock + threadIdx.x * kMtCandPerThread;
+    // the accepted pairs of the blocks before this one (integer sums: any order);
+    // block 0 sums every block's count for the short-draw check
+    const int64_t nsum = blockIdx.x == 0 ? nb : (int64_t)blockIdx.x;
+    int64_t part = 0;
+    for (int64_t i = threadIdx.x; i < nsum; i += kMtCountThreads) part += bcnt[i];
     double x1[kMtCandPerThread], x2[kMtCandPerThread], r2[kMtCandPerThread];
     bool acc[kMtCandPerThread];
     int cnt = 0;
@@ -300,9 +270,24 @@ __global__ __launch_bounds__(kMtCountThreads) void mt_emit_kernel(
         acc[k] = c < ncand && mt_candidate(X, w0 + 4 * c, cap, x1[k], x2[k], r2[k]);
         cnt += acc[k] ? 1 : 0;
     }
+    __shared__ long long s_part[kMtCountThreads / 64];
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) part += __shfl_xor(part, d, 64);
+    if ((threadIdx.x & 63) == 0) s_part[threadIdx.x >> 6] = part;
     int tot;
-    const int incl = mt_block_scan(cnt, &tot);
-    int64_t q = boff[blockIdx.x] + incl - cnt;
+    const int incl = mt_block_scan(cnt, &tot);          // (its barrier publishes s_part)
+    int64_t before = 0;
+#pragma unroll
+    for (int w = 0; w < kMtCountThreads / 64; ++w) before += s_part[w];
+    if (blockIdx.x == 0) {
+        if (threadIdx.x == 0) {
+            const bool shrt = before < P;
+            st->short_draw = shrt ? 1 : 0;
+            if (shrt && status) atomicOr(status, 256);
+        }
+        before = 0;
+    }
+    int64_t q = before + incl - cnt;
     if (q >= P) return;
 #pragma unroll
     for (int k = 0; k < kMtCandPerThread; ++k) {
@@ -599,7 +584,7 @@ int glibc_log_table(GlibcLogTable* out) {
 }
 
 void mt_free(MtBuffers& b) {
-    void* ps[] = {b.st, b.tab, b.X, b.seg, b.q, b.bcnt, b.boff, b.normals, b.pre};
+    void* ps[] = {b.st, b.tab, b.X, b.seg, b.q, b.bcnt, b.normals, b.pre};
     for (void* p : ps)
         if (p) (void)hipFree(p);
     b = MtBuffers{};
@@ -672,7 +657,6 @@ int mt_reserve(MtBuffers& b, int64_t g_cap, int64_t pre_cap, int device) {
     SLAM_HIP_TRY(hipMalloc(&b.seg, sizeof(uint32_t) * kMtN * (size_t)b.R));
     SLAM_HIP_TRY(hipMalloc(&b.q, sizeof(uint32_t) * (kMtDeg / 2 + 16)));
     SLAM_HIP_TRY(hipMalloc(&b.bcnt, sizeof(unsigned) * (size_t)std::max<int64_t>(b.nb_count, 1)));
-    SLAM_HIP_TRY(hipMalloc(&b.boff, sizeof(int64_t) * (size_t)std::max<int64_t>(b.nb_count, 1)));
     SLAM_HIP_TRY(hipMalloc(&b.normals, sizeof(double) * (size_t)std::max<int64_t>(g_cap, 1)));
     SLAM_HIP_TRY(hipMalloc(&b.pre, sizeof(double) * (size_t)std::max<int64_t>(pre_cap, 1)));
     SLAM_HIP_TRY(hipMemcpy(b.tab, &T, sizeof(T), hipMemcpyHostToDevice));
@@ -763,11 +747,10 @@ int mt_enqueue(const MtBuffers& b, int64_t n_pre, const int32_t* pre_flag, doubl
     const unsigned nbc = (unsigned)((ncand + kMtCandPerBlock - 1) / kMtCandPerBlock);
     mt_count_kernel<<<std::max(nbc, 1u), kMtCountThreads, 0, s>>>(b.st, b.X, b.cap, pre_flag, n_pre,
                                                                    ncand, b.bcnt, RS, b.need);
-    if (nbc > 0) {
-        mt_scan_kernel<<<1, kMtScanThreads, 0, s>>>(b.st, b.bcnt, nbc, b.boff, g, status);
+    if (nbc > 0)
         mt_emit_kernel<<<nbc, kMtCountThreads, 0, s>>>(b.st, b.X, b.cap, pre_flag, n_pre, ncand,
-                                                       b.boff, g, b.tab, b.normals);
-    }
+                                                       b.bcnt, (int64_t)nbc, g, b.tab, b.normals,
+                                                       status);
     SLAM_HIP_TRY(hipGetLastError());
     mt_finish_kernel<<<1, kMtGenThreads, 0, s>>>(b.st, b.X, b.cap, pre_flag, n_pre, pre_scale, pre_out,
                                                  pre_index, g, b.normals);
