@@ -636,11 +636,11 @@ int create_impl(const slam_pf_config* cfg, int64_t n_local, int64_t n_global, in
     A(h->bsum, std::max(h->nb_norm, h->nb_part));
     A(h->boff, std::max(h->nb_norm, h->nb_part) + 1);
     A(h->s_cur, 1);
-    A(h->dp.pmax, h->nb_part);
+    A(h->dp.pmax, h->nb_part + 1);                        // + 1: the finalize's pair loads
     A(h->dp.pidx, h->nb_part);
     A(h->dp.ppre, h->nb_part);
     for (int q = 0; q < 3; ++q) A(h->dp.pxe[q], h->nb_part);
-    for (int q = 0; q < 11; ++q) A(h->dp.ps[q], h->nb_part);
+    for (int q = 0; q < 11; ++q) A(h->dp.ps[q], h->nb_part + 1);
     A(h->dp.leaf, (size_t)(kPartPer / 128) * h->nb_part);
     A(h->dp.mark, npad);
     A(h->dp.carry, h->nb_part + 1);

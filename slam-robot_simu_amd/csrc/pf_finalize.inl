@@ -56,6 +56,12 @@ __device__ __forceinline__ void fin_load_record(const DeferParts& dp, const int6
 // 16-leaf subtree.
 static_assert(kSumChunk == 16 * kPartPer, "a buffer is 16 fused blocks, 4 per np.sum lane");
 
+// register block k of lane t (k < kFinRegBlocks): neighbour pairs, increasing in k
+__device__ __forceinline__ int64_t fin_blk(const int t, const int k) {
+    static_assert(kFinRegBlocks % 2 == 0, "pairs of blocks");
+    return 2 * (int64_t)t + (k & 1) + 2 * (int64_t)kFinThreads * (k >> 1);
+}
+
 __global__ __launch_bounds__(kFinThreads) void finalize_deferred_kernel(
     const int64_t n, const DeferParts dp, const double* __restrict__ w_un,
     double* __restrict__ s_cur, const int32_t* __restrict__ tail_leaves,
@@ -86,17 +92,26 @@ __global__ __launch_bounds__(kFinThreads) void finalize_deferred_kernel(
         s_min = ~0ull;
         s_flag = 0;
     }
-    // ---- loads, issued up front: this lane's blocks tid + 512 k and its leaves
+    // ---- loads, issued up front: this lane's blocks fin_blk(tid, k) (pairs of
+    // neighbours, one 16-byte load per array: the partial arrays hold nb + 1
+    // entries) and its leaves
     double pm[kFinRegBlocks], q[kFinRegBlocks][11];
     bool has[kFinRegBlocks];
 #pragma unroll
-    for (int k = 0; k < kFinRegBlocks; ++k) {
-        const int64_t b = tid + (int64_t)kFinThreads * k;
-        has[k] = b < nb;
-        const int64_t bb = has[k] ? b : 0;
-        pm[k] = dp.pmax[bb];
+    for (int kp = 0; kp < kFinRegBlocks / 2; ++kp) {
+        const int64_t b = fin_blk(tid, 2 * kp);
+        has[2 * kp] = b < nb;
+        has[2 * kp + 1] = b + 1 < nb;
+        const int64_t bb = has[2 * kp] ? b : 0;
+        const double2 t = *reinterpret_cast<const double2*>(dp.pmax + bb);
+        pm[2 * kp] = t.x;
+        pm[2 * kp + 1] = t.y;
 #pragma unroll
-        for (int j = 0; j < 11; ++j) q[k][j] = dp.ps[j][bb];
+        for (int j = 0; j < 11; ++j) {
+            const double2 u = *reinterpret_cast<const double2*>(dp.ps[j] + bb);
+            q[2 * kp][j] = u.x;
+            q[2 * kp + 1][j] = u.y;
+        }
     }
     const int part = tid & (kFinLeafLanes - 1);
     double L[4];                                   // fused-block subtree sums
@@ -200,7 +215,7 @@ __global__ __launch_bounds__(kFinThreads) void finalize_deferred_kernel(
         if (has[k] && pm[k] >= M * (1.0 - 0x1p-48)) {
             const int slot = atomicAdd(&s_ncand, 1);
             if (slot < kFinCand) {
-                const int64_t b = tid + (int64_t)kFinThreads * k;
+                const int64_t b = fin_blk(tid, k);
                 FinRecord f;
                 fin_load_record(dp, b, f);
                 s_cblk[slot] = b;
@@ -241,7 +256,7 @@ __global__ __launch_bounds__(kFinThreads) void finalize_deferred_kernel(
 #pragma unroll
         for (int k = kFinRegBlocks - 1; k >= 0; --k)
             if (has[k] && pm[k] >= M * (1.0 - 0x1p-48) && pm[k] / s == mval)
-                cb = (unsigned long long)(tid + (int64_t)kFinThreads * k);
+                cb = (unsigned long long)fin_blk(tid, k);
         for (int64_t b = tid + (int64_t)kFinThreads * kFinRegBlocks; b < nb; b += kFinThreads)
             if (cb == ~0ull && dp.pmax[b] / s == mval) cb = (unsigned long long)b;
         if (cb != ~0ull) atomicMin(&s_min, cb);
@@ -340,7 +355,7 @@ __global__ __launch_bounds__(kFinThreads) void finalize_deferred_kernel(
         if (in_lds) {
 #pragma unroll
             for (int k = 0; k < kFinRegBlocks; ++k)
-                if (has[k]) sh[tid + kFinThreads * k] = (pm[k] / s) * q[k][0];
+                if (has[k]) sh[fin_blk(tid, k)] = (pm[k] / s) * q[k][0];
         }
         __syncthreads();
         auto btot = [&](int64_t b) {

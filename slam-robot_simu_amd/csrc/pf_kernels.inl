@@ -214,6 +214,33 @@ __device__ __forceinline__ double xor_f64(const double v, const int d) {
     if (d == 2) return dpp_f64<kDppXor2>(v);
     return __shfl_xor(v, d, 64);
 }
+// inclusive max-scan of an int32 over the wave, and the exclusive value
+// (lane 0: -1): row shifts by DPP (lanes without a source read -1), then the
+// three lower rows' maxima read into scalars
+__device__ __forceinline__ int32_t wave_max_scan_i32(int32_t v, int32_t& excl) {
+    constexpr int kRowShr = 0x110;                                      // row_shr:d = 0x110 + d
+    int32_t o;
+    o = __builtin_amdgcn_update_dpp(-1, v, kRowShr + 1, 0xF, 0xF, false);
+    v = o > v ? o : v;
+    o = __builtin_amdgcn_update_dpp(-1, v, kRowShr + 2, 0xF, 0xF, false);
+    v = o > v ? o : v;
+    o = __builtin_amdgcn_update_dpp(-1, v, kRowShr + 4, 0xF, 0xF, false);
+    v = o > v ? o : v;
+    o = __builtin_amdgcn_update_dpp(-1, v, kRowShr + 8, 0xF, 0xF, false);
+    v = o > v ? o : v;
+    const int lane = (int)__lane_id(), row = lane >> 4;
+    const int32_t r0 = __builtin_amdgcn_readlane(v, 15), r1 = __builtin_amdgcn_readlane(v, 31);
+    const int32_t r2 = __builtin_amdgcn_readlane(v, 47);
+    const int32_t m01 = r0 > r1 ? r0 : r1, m012 = m01 > r2 ? m01 : r2;
+    const int32_t below = row == 0 ? -1 : row == 1 ? r0 : row == 2 ? m01 : m012;
+    v = below > v ? below : v;
+    // lane l - 1's inclusive value: within the row by row_shr:1, the row's
+    // first lane takes the rows below
+    const int32_t prev = __builtin_amdgcn_update_dpp(-1, v, kRowShr + 1, 0xF, 0xF, false);
+    excl = (lane & 15) ? prev : below;
+    return v;
+}
+
 // max over the wave (every lane gets it); fmax semantics as the butterfly's
 __device__ __forceinline__ double wave_max_f64(double v) {
     v = fmax(v, dpp_f64<kDppXor1>(v));
@@ -1064,15 +1091,9 @@ __global__ __launch_bounds__(256) SLAM_FUSED_ATTR void pf_fused_kernel(
             if (k > 0) r[k] = r[k] > r[k - 1] ? r[k] : r[k - 1];
         }
         const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-        int32_t v = r[P - 1];
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const int32_t o = __shfl_up(v, d, 64);
-            if (lane >= d) v = o > v ? o : v;
-        }
+        int32_t before;
+        const int32_t v = wave_max_scan_i32(r[P - 1], before);
         if (lane == 63) s_wmax[wave] = v;
-        int32_t before = __shfl_up(v, 1, 64);
-        if (lane == 0) before = -1;
         __syncthreads();
         int32_t run = dp.carry[blockIdx.x];
         for (int w = 0; w < wave; ++w) run = s_wmax[w] > run ? s_wmax[w] : run;
