@@ -529,8 +529,7 @@ __device__ void dist_unpack_items(const int64_t n, double* __restrict__ xs, doub
         for (int64_t b = (lo + kPartPer - 1) / kPartPer; b * kPartPer < hi; ++b) carry[b] = (int32_t)k;
         cov += (uint64_t)(hi - lo);
     }
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) cov += __shfl_xor(cov, d, 64);
+    cov = wave_sum_u64(cov);
     if ((threadIdx.x & 63) == 0 && cov) atomicAdd(&s_cov, (unsigned long long)cov);
     __syncthreads();
     if (threadIdx.x == 0 && s_cov) atomicAdd((unsigned long long*)&scr->covered, s_cov);
@@ -878,10 +877,10 @@ __global__ __launch_bounds__(kScanThreads) void dist_resample_merged_kernel(
                     else if (lv[k] < P.gb[d + 1]) ++cc;
                 }
             }
-#pragma unroll
-            for (int o = 1; o < 64; o <<= 1) {
-                cb += __shfl_xor(cb, o, 64);
-                cc += __shfl_xor(cc, o, 64);
+            {   // both counts (<= 512 per wave) in one word
+                const int32_t both = wave_sum_i32((cb << 16) | cc);
+                cb = both >> 16;
+                cc = both & 0xFFFF;
             }
             if (lane == 0) {
                 if (cb) atomicAdd(&s_cb[d], cb);
@@ -917,8 +916,7 @@ __global__ __launch_bounds__(kScanThreads) void dist_resample_merged_kernel(
 #pragma unroll
                 for (int u = 0; u < 8; ++u) a += v[u];
             }
-#pragma unroll
-            for (int o = 1; o < 64; o <<= 1) a += __shfl_xor(a, o, 64);
+            a = (int64_t)wave_sum_u64((uint64_t)a);
             if (lane == 0) st_wt((e & 1) ? (void*)&scr->dcnt[e >> 1] : (void*)&scr->dbase[e >> 1], (uint64_t)a);
         }
         dist_token_release(&scr->rel[1], tokB);
@@ -1009,13 +1007,20 @@ __device__ __forceinline__ void dist_record(const int64_t n, const DeferParts& d
     double pm[kFinRegBlocks], q[kFinRegBlocks][11];
     bool has[kFinRegBlocks];
 #pragma unroll
-    for (int k = 0; k < kFinRegBlocks; ++k) {
-        const int64_t b = tid + (int64_t)kFinThreads * k;
-        has[k] = b < nb;
-        const int64_t bb = has[k] ? b : 0;
-        pm[k] = dp.pmax[bb];
+    for (int kp = 0; kp < kFinRegBlocks / 2; ++kp) {     // neighbour pairs (finalize_deferred_kernel)
+        const int64_t b = fin_blk(tid, 2 * kp);
+        has[2 * kp] = b < nb;
+        has[2 * kp + 1] = b + 1 < nb;
+        const int64_t bb = has[2 * kp] ? b : 0;
+        const double2 t = *reinterpret_cast<const double2*>(dp.pmax + bb);
+        pm[2 * kp] = t.x;
+        pm[2 * kp + 1] = t.y;
 #pragma unroll
-        for (int j = 0; j < 11; ++j) q[k][j] = dp.ps[j][bb];
+        for (int j = 0; j < 11; ++j) {
+            const double2 u = *reinterpret_cast<const double2*>(dp.ps[j] + bb);
+            q[2 * kp][j] = u.x;
+            q[2 * kp + 1][j] = u.y;
+        }
     }
     const int part = tid & (kFinLeafLanes - 1);
     double L[4];                                   // fused-block subtree sums
@@ -1102,7 +1107,7 @@ __device__ __forceinline__ void dist_record(const int64_t n, const DeferParts& d
         unsigned long long mb = ~0ull;
 #pragma unroll
         for (int k = kFinRegBlocks - 1; k >= 0; --k)
-            if (has[k] && pm[k] == M) mb = (unsigned long long)(tid + (int64_t)kFinThreads * k);
+            if (has[k] && pm[k] == M) mb = (unsigned long long)fin_blk(tid, k);
         for (int64_t b = bx0; b < nb && mb == ~0ull; b += kFinThreads)
             if (dp.pmax[b] == M) mb = (unsigned long long)b;
         if (mb != ~0ull) atomicMin(&s_mblk, mb);
@@ -1114,7 +1119,7 @@ __device__ __forceinline__ void dist_record(const int64_t n, const DeferParts& d
         if (M > 0.0) {
 #pragma unroll
             for (int k = kFinRegBlocks - 1; k >= 0; --k) {
-                const unsigned long long b = (unsigned long long)(tid + (int64_t)kFinThreads * k);
+                const unsigned long long b = (unsigned long long)fin_blk(tid, k);
                 if (has[k] && pm[k] >= thr && b >= prev) cb = b;
             }
             for (int64_t b = bx0; b < nb && cb == ~0ull; b += kFinThreads)

@@ -241,6 +241,23 @@ __device__ __forceinline__ int32_t wave_max_scan_i32(int32_t v, int32_t& excl) {
     return v;
 }
 
+// integer sums over the wave (every lane gets them; any order is exact)
+__device__ __forceinline__ int32_t wave_sum_i32(int32_t v) {
+    v += __builtin_amdgcn_mov_dpp(v, kDppXor1, 0xF, 0xF, false);
+    v += __builtin_amdgcn_mov_dpp(v, kDppXor2, 0xF, 0xF, false);
+    v += __builtin_amdgcn_mov_dpp(v, kDppHalfMirror, 0xF, 0xF, false);
+    v += __builtin_amdgcn_mov_dpp(v, kDppMirror, 0xF, 0xF, false);
+    return __builtin_amdgcn_readlane(v, 0) + __builtin_amdgcn_readlane(v, 16) +
+           __builtin_amdgcn_readlane(v, 32) + __builtin_amdgcn_readlane(v, 48);
+}
+__device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
+    v += dpp_u64<kDppXor1>(v);
+    v += dpp_u64<kDppXor2>(v);
+    v += dpp_u64<kDppHalfMirror>(v);
+    v += dpp_u64<kDppMirror>(v);
+    return readlane_u64(v, 0) + readlane_u64(v, 16) + readlane_u64(v, 32) + readlane_u64(v, 48);
+}
+
 // max over the wave (every lane gets it); fmax semantics as the butterfly's
 __device__ __forceinline__ double wave_max_f64(double v) {
     v = fmax(v, dpp_f64<kDppXor1>(v));
