@@ -6,6 +6,8 @@
 // the scan_* passes (launched at the start of a step; they gate on the
 // device resample flag, so a device-resident run needs no host decisions).
 // Particles are SoA fp64 (x[], y[], th[]) in HBM, one particle per lane.
+#include <type_traits>
+
 #include "pf_kernels.hpp"
 
 // Phase stamps of the resample passes (probe builds only: -DSLAM_PROBE,
@@ -28,15 +30,55 @@ __device__ unsigned long long g_probe_slow[2];   // slow particles, blocks with 
 // ====================================================================
 // wave / block helpers (wave = 64 lanes)
 // ====================================================================
+// DPP row_shr:D of a 32- or 64-bit integer; lanes without a source read 0
+template <int D, typename T>
+__device__ __forceinline__ T dpp_row_shr0(const T v) {
+    constexpr int kCtrl = 0x110 + D;
+    if constexpr (sizeof(T) == 8) {
+        const uint64_t u = (uint64_t)v;
+        const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)u, kCtrl, 0xF, 0xF, false);
+        const uint32_t hi =
+            (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(u >> 32), kCtrl, 0xF, 0xF, false);
+        return (T)(((uint64_t)hi << 32) | lo);
+    } else {
+        return (T)__builtin_amdgcn_update_dpp(0, (int)v, kCtrl, 0xF, 0xF, false);
+    }
+}
+template <typename T>
+__device__ __forceinline__ T readlane_int(const T v, const int l) {
+    if constexpr (sizeof(T) == 8) {
+        const uint64_t u = (uint64_t)v;
+        const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)u, l);
+        const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), l);
+        return (T)(((uint64_t)hi << 32) | lo);
+    } else {
+        return (T)__builtin_amdgcn_readlane((int)v, l);
+    }
+}
+
+// inclusive wave scan.  Integers (exact in any order): Hillis-Steele inside
+// each 16-lane row by DPP row shifts, then the lower rows' totals read into
+// scalars; floating point keeps the lane-shuffle order.
 template <typename T>
 __device__ __forceinline__ T wave_incl_scan(T v) {
-    const int lane = threadIdx.x & 63;
+    if constexpr (std::is_integral<T>::value) {
+        v += dpp_row_shr0<1>(v);
+        v += dpp_row_shr0<2>(v);
+        v += dpp_row_shr0<4>(v);
+        v += dpp_row_shr0<8>(v);
+        const T r0 = readlane_int(v, 15), r1 = readlane_int(v, 31), r2 = readlane_int(v, 47);
+        const int row = (int)((threadIdx.x & 63) >> 4);
+        v += (row >= 1 ? r0 : T(0)) + (row >= 2 ? r1 : T(0)) + (row >= 3 ? r2 : T(0));
+        return v;
+    } else {
+        const int lane = threadIdx.x & 63;
 #pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        T o = __shfl_up(v, d, 64);
-        if (lane >= d) v = v + o;
+        for (int d = 1; d < 64; d <<= 1) {
+            T o = __shfl_up(v, d, 64);
+            if (lane >= d) v = v + o;
+        }
+        return v;
     }
-    return v;
 }
 
 // Exclusive block scan over NT threads; sh needs NT/64+1 entries.  Returns the
@@ -45,8 +87,13 @@ template <typename T, int NT>
 __device__ __forceinline__ T block_excl_scan(T v, T* sh, T& total) {
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const T inc = wave_incl_scan(v);
-    T ex = __shfl_up(inc, 1, 64);
-    if (lane == 0) ex = T(0);
+    T ex;
+    if constexpr (std::is_integral<T>::value) {
+        ex = inc - v;
+    } else {
+        ex = __shfl_up(inc, 1, 64);
+        if (lane == 0) ex = T(0);
+    }
     if (lane == 63) sh[wid] = inc;
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -2095,10 +2142,15 @@ struct TileScan {
 template <typename T>
 __device__ __forceinline__ T wave_excl_scan(const T v, T& total) {
     const T inc = wave_incl_scan(v);
-    T ex = __shfl_up(inc, 1, 64);
-    if ((threadIdx.x & 63) == 0) ex = T(0);
-    total = __shfl(inc, 63, 64);
-    return ex;
+    if constexpr (std::is_integral<T>::value) {
+        total = readlane_int(inc, 63);
+        return inc - v;
+    } else {
+        T ex = __shfl_up(inc, 1, 64);
+        if ((threadIdx.x & 63) == 0) ex = T(0);
+        total = __shfl(inc, 63, 64);
+        return ex;
+    }
 }
 
 // Tile `tile` of the weights w = w_un / s, lane l owns elements 8l .. 8l+7
