@@ -160,9 +160,10 @@ __device__ __forceinline__ double exp_lean(const double x) {
 
 // exp(x) from a 64-entry table of 2^(j/64) (each entry the rounded value and
 // its rounding error), held in LDS by the caller: x = (64 k + j) ln2/64 + r,
-// |r| <= ln2/128, exp(r) - 1 by its degree-6 Taylor polynomial (truncation
-// < 3e-20), exp(x) = 2^k (T_j + (T_j p + T_lo_j)) -- under 0.51 ulp, with six
-// polynomial fmas against exp_lean's thirteen.  ln2/64 is split so that
+// |r| <= ln2/128, exp(r) - 1 by its degree-5 Taylor polynomial (truncation
+// < 3.5e-17, round 3: degree 6 before), exp(x) = 2^k (T_j + (T_j p + T_lo_j))
+// -- under 0.9 ulp, with five polynomial fmas against exp_lean's thirteen (the
+// parity bar is the weights' 1e-12, not the last ulp).  ln2/64 is split so that
 // kd ln2hi/64 is exact for |kd| < 2^24.  Below -746 the result is +0, above
 // 710 +inf, NaN stays NaN (as exp_lean).
 __device__ __constant__ const double2 kExpTab64[64] = {
@@ -238,14 +239,18 @@ __device__ __forceinline__ double exp_tab(const double x, const double2* __restr
     constexpr double kInvLn2N = 0x1.71547652b82fep+6;       // 64 / ln2
     constexpr double kNegLn2HiN = -0x1.62e42ff000000p-7;    // -(ln2/64), 29 significant bits
     constexpr double kNegLn2LoN = 0x1.718432a1b0e26p-41;    // -(ln2/64 - ln2hi/64)
-    const double kd = rint(x * kInvLn2N);
+    // k = round(x 64/ln2) by the 1.5 2^52 shift: the integer sits in the low
+    // word of kdm (no rint / convert); |x 64/ln2| >= 2^51 only where the range
+    // select below decides
+    const double kdm = fma(x, kInvLn2N, 0x1.8p52);
+    const double kd = kdm - 0x1.8p52;
     const double r = fma(kd, kNegLn2LoN, fma(kd, kNegLn2HiN, x));
-    const int ki = (int)kd;
+    const int ki = (int)(uint32_t)__double_as_longlong(kdm);
     const double2 t = tab[ki & 63];
     const double r2 = r * r;
-    const double c46 = fma(r2, 1.0 / 720.0, fma_kk(r, 1.0 / 120.0, 1.0 / 24.0));   // 1/24 + r/120 + r^2/720
+    const double c45 = fma_kk(r, 1.0 / 120.0, 1.0 / 24.0);                      // 1/24 + r/120
     const double c23 = fma_kk(r, 1.0 / 6.0, 0.5);                                 // 1/2 + r/6
-    const double p = fma(r2, fma(r2, c46, c23), r);                               // exp(r) - 1
+    const double p = fma(r2, fma(r2, c45, c23), r);      // exp(r) - 1 to degree 5 (r^6/720 < 3.5e-17)
     const double v = t.x + fma(t.x, p, t.y);
     const double e = ldexp(v, ki >> 6);
     if (NONPOS) return (x < -746.0) ? 0.0 : e;
