@@ -661,16 +661,21 @@ __device__ void dist_fold_global(const DistPeers& P, const int64_t* s_off, const
                 if ((double)K >= 0x1p53) bad = true;
             }
             const double w = mine_l ? e.w : 0.0;
-            double cs = 0.0;
+            // the chain: two dependent adds per special, the operands read into
+            // scalars (fully unrolled: the reads do not wait on the chain); each
+            // lane keeps the sums at its own special and checks its binade after
+            double cs = 0.0, cr = 0.0;
             const int lim = (M - t0 < 63) ? (int)(M - t0) : 63;
-            for (int l = 0; l < lim; ++l) {
-                s = s + readlane_d(w, l);
-                if (lane == l) cs = s;
-                const double blo = readlane_d(lo, l), bhi = readlane_d(hi, l);
-                if (!(s >= blo) || !(s < bhi)) bad = true;
-                s = s + readlane_d(ku, l);
-                if (!(s < bhi)) bad = true;
+#pragma unroll
+            for (int l = 0; l < 63; ++l) {
+                if (l < lim) {                            // wave-uniform
+                    s = s + readlane_d(w, l);             // the special element's own add
+                    if (lane == l) cs = s;
+                    s = s + readlane_d(ku, l);            // the run: K ulps, exact
+                    if (lane == l) cr = s;
+                }
             }
+            if (lane < lim && (!(cs >= lo) || !(cs < hi) || !(cr < hi))) bad = true;   // its run keeps the binade
             if (mine_l) {
                 SpecialOut o;
                 o.cs = cs;
