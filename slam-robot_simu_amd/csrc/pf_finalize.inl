@@ -56,6 +56,32 @@ __device__ __forceinline__ void fin_load_record(const DeferParts& dp, const int6
 // 16-leaf subtree.
 static_assert(kSumChunk == 16 * kPartPer, "a buffer is 16 fused blocks, 4 per np.sum lane");
 
+// s + a[0] + a[1] + ... + a[cnt - 1], left to right (np.sum's buffer chain),
+// with the next 16 LDS words in flight while the current 16 are added
+__device__ __forceinline__ double lds_chain_sum(double s, const double* a, const int cnt) {
+    constexpr int B = 16;
+    int k = 0;
+    if (cnt >= B) {
+        double cur[B];
+#pragma unroll
+        for (int j = 0; j < B; ++j) cur[j] = a[j];
+        for (; k + 2 * B <= cnt; k += B) {
+            double nxt[B];
+#pragma unroll
+            for (int j = 0; j < B; ++j) nxt[j] = a[k + B + j];
+#pragma unroll
+            for (int j = 0; j < B; ++j) s = s + cur[j];
+#pragma unroll
+            for (int j = 0; j < B; ++j) cur[j] = nxt[j];
+        }
+#pragma unroll
+        for (int j = 0; j < B; ++j) s = s + cur[j];
+        k += B;
+    }
+    for (; k < cnt; ++k) s = s + a[k];
+    return s;
+}
+
 // register block k of lane t (k < kFinRegBlocks): neighbour pairs, increasing in k
 __device__ __forceinline__ int64_t fin_blk(const int t, const int k) {
     static_assert(kFinRegBlocks % 2 == 0, "pairs of blocks");
@@ -182,7 +208,7 @@ __global__ __launch_bounds__(kFinThreads) void finalize_deferred_kernel(
         if (part == 0 && tid / kFinLeafLanes < cnt) sh[tid / kFinLeafLanes] = v;
         __syncthreads();
         if (c0 + kFinBufPerRound < nfull && tid == 0) {  // not the last round: fold it now
-            for (int k = 0; k < cnt; ++k) s = s + sh[k];
+            s = lds_chain_sum(s, sh, (int)cnt);
         }
     }
     if (nfull == 0) __syncthreads();                     // s_wmax visible
@@ -196,7 +222,7 @@ __global__ __launch_bounds__(kFinThreads) void finalize_deferred_kernel(
         // rescale their partials and fetch the argmax candidates)
         __builtin_amdgcn_s_setprio(3);
         if (nfull > 0)
-            for (int k = 0; k < last_cnt; ++k) s = s + sh[k];
+            s = lds_chain_sum(s, sh, (int)last_cnt);
         __builtin_amdgcn_s_setprio(0);
     }
     {
