@@ -520,6 +520,35 @@ class Agreement:
             raise ShardedFailure(phase, mine)
 
 
+def timed_runs(filt, ctl, warmup, steps, barrier_sync, ag=None):
+    """Every step graph captured first (graph_capture_ms, never inside a timed
+    run), `warmup` untimed steps, `steps` timed steps between barrier +
+    synchronize, then a kernel-timing pass over `steps` more steps (HIP events
+    on the filter's stream around every launch).  With an Agreement (the
+    sharded mode) a rank's failure is caught, every rank still reaches every
+    barrier, and the ranks agree on it at the next checkpoint."""
+    call = ag.attempt if ag is not None else (lambda fn, *a, **kw: fn(*a, **kw))
+    cap_ms = call(filt.prepare_graphs)
+    if warmup:
+        call(filt.run, 0, ctl[:warmup], want_results=False)
+    if ag is not None:
+        ag.checkpoint("warm-up")
+    barrier_sync()
+    t0 = time.perf_counter()
+    out = call(filt.run, warmup, ctl[warmup:warmup + steps])
+    barrier_sync()
+    elapsed = time.perf_counter() - t0
+    if ag is not None:
+        ag.checkpoint("run")
+    call(filt.enable_timing, True)
+    call(filt.run, warmup + steps, ctl[warmup + steps:])
+    timing = call(lambda: {k: filt.timing(k) for k in range(4)})
+    call(filt.enable_timing, False)
+    if ag is not None:
+        ag.checkpoint("timing")
+    return elapsed, out, timing, cap_ms
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -580,23 +609,6 @@ def main():
             dist.barrier()
             torch.cuda.synchronize()
 
-    def timed_runs(filt):
-        # W untimed warm-up steps (they also capture the step graphs), K timed
-        # steps between barrier + synchronize, then a kernel-timing pass over K
-        # more steps (HIP events on the filter's stream around every launch)
-        if args.warmup:
-            filt.run(0, ctl[:args.warmup], want_results=False)
-        barrier_sync()
-        t0 = time.perf_counter()
-        out = filt.run(args.warmup, ctl[args.warmup:args.warmup + args.steps])
-        barrier_sync()
-        elapsed = time.perf_counter() - t0
-        filt.enable_timing(True)
-        filt.run(args.warmup + args.steps, ctl[args.warmup + args.steps:])
-        timing = {k: filt.timing(k) for k in range(4)}
-        filt.enable_timing(False)
-        return elapsed, out, timing
-
     def measure_sharded(likelihood, n_global):
         # one filter over n_global particles (BASELINE configs[2]): this rank's
         # shard through slamhip.dist.DistFilter -- the device-resident step
@@ -636,9 +648,7 @@ def main():
                 ag.checkpoint("connect")
             ag.attempt(filt.load_observations, zs)
             ag.checkpoint("load")
-            res = ag.attempt(timed_runs, filt)
-            ag.checkpoint("run")
-            return res
+            return timed_runs(filt, ctl, args.warmup, args.steps, barrier_sync, ag)
         finally:
             if filt is not None:
                 filt.close()
@@ -652,7 +662,7 @@ def main():
                                   likelihood=likelihood, seed=1234 + rank, device=local_rank)
         try:
             pf.load_observations(zs)
-            return timed_runs(pf)
+            return timed_runs(pf, ctl, args.warmup, args.steps, barrier_sync)
         finally:
             pf.close()
 
@@ -665,6 +675,7 @@ def main():
         try:
             pf.use_numpy_stream(np.random.RandomState(1234))
             pf.load_truth(simulate_world.poses)
+            pf.prepare_graphs()
             if args.warmup:
                 pf.run(0, ctl[:args.warmup], want_results=False)
             barrier_sync()
@@ -683,7 +694,7 @@ def main():
         # measure independent replicas instead, and the line says so
         # (config.parallelism, sharded_error)
         try:
-            elapsed, out, timing = measure(args.likelihood)
+            elapsed, out, timing, cap_ms = measure(args.likelihood)
         except ShardedFailure as e:
             phase, mine = e.args
             print(f"bench: sharded mode failed at {phase} ({mine or 'another rank'})", file=sys.stderr)
@@ -691,9 +702,9 @@ def main():
             dist.all_gather_object(errs, mine)
             sharded_error = f"{phase}: " + ("; ".join(x for x in errs if x) or "another rank failed")
             args.mode = "replicas"
-            elapsed, out, timing = measure(args.likelihood)
+            elapsed, out, timing, cap_ms = measure(args.likelihood)
     else:
-        elapsed, out, timing = measure(args.likelihood)
+        elapsed, out, timing, cap_ms = measure(args.likelihood)
     fused_ms, fused_n = timing[0]
     red_ms, red_n = timing[1]
     res_ms, res_n = timing[2]
@@ -740,12 +751,13 @@ def main():
                                   "reduce": red_ms / max(red_n, 1),
                                   "resample": res_ms / max(res_n, 1),
                                   "step_events": step_ms / max(step_n, 1)},
+        "graph_capture_ms": cap_ms,
         "resample_steps": int(sum(o["resampled"] for o in out)),
         "ess_near_steps": int(sum(o.get("ess_near", False) for o in out)),
         "closed_form_fallback_waves": int(sum(o.get("dd_waves", 0) for o in out)),
     }
     if world == 1 and args.likelihood != "product" and not strong:
-        e2, _, t2 = measure("product")
+        e2, _, t2, _ = measure("product")
         f2 = t2[0][0] / 1e3 / max(t2[0][1], 1)
         line["alt_modes"] = {"product": {"value": n_rank * NL * args.steps / e2,
                                          "ms_per_step": e2 * 1e3 / args.steps,
@@ -758,13 +770,13 @@ def main():
                     "np.random) drawn on the device with the observations simulated there"}
     if world == 1 and args.mode == "replicas" and not strong:
         # the sharded step's kernels on one shard (its overhead over the single handle)
-        e3, _, t3 = measure_sharded(args.likelihood, NP_PER_GPU)
+        e3, _, t3, _ = measure_sharded(args.likelihood, NP_PER_GPU)
         line["sharded1"] = {"ms_per_step": e3 * 1e3 / args.steps,
                             "over_single": e3 / elapsed,
                             "fused_avg_ms": t3[0][0] / max(t3[0][1], 1)}
         # strong-scaling reference: one handle of 2^23 particles (BASELINE configs[2]'s
         # total) -- the single-GPU line that `--total-particles 8388608 --gpus N` divides
-        e5, o5, t5 = measure(args.likelihood, STRONG_TOTAL)
+        e5, o5, t5, _ = measure(args.likelihood, STRONG_TOTAL)
         line["strong_single"] = {"particles": STRONG_TOTAL,
                                  "value": STRONG_TOTAL * NL * args.steps / e5,
                                  "ms_per_step": e5 * 1e3 / args.steps,

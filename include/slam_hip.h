@@ -131,6 +131,12 @@ int slam_pf_enable_timing(slam_pf* h, int32_t on);
 int slam_pf_timing(slam_pf* h, int32_t kernel, double* total_ms, int64_t* launches);
 /* slam_pf_run replays one captured hipGraph per step (default on). */
 int slam_pf_set_graphs(slam_pf* h, int32_t on);
+/* Capture every graph slam_pf_run will replay (8-step and 1-step graphs for
+ * both ping-pong parities) without running them, so that no capture lands in
+ * a timed run; *capture_ms (may be NULL) = host time spent.  Graphs are
+ * dropped (and captured again on demand) by the calls that change a step's
+ * launches (set_stream, set_scan_merged, set_ess_band, the device stream). */
+int slam_pf_prepare_graphs(slam_pf* h, double* capture_ms);
 /* Exact cumsum of a resample step in one launch (on = default where the grid
  * is co-resident; SLAM_ERR_ARG elsewhere) or in two; bit-identical results. */
 int slam_pf_set_scan_merged(slam_pf* h, int32_t on);
@@ -209,6 +215,8 @@ int slam_dist_step(slam_dist* d, const double* control, const double* z, slam_pf
 int slam_dist_load_observations(slam_dist* d, int32_t n_steps, const double* z_all);
 int slam_dist_run(slam_dist* d, int32_t first_step, int32_t n_steps, const double* controls,
                   slam_pf_result* results);
+/* slam_pf_prepare_graphs for the sharded step (after connect) */
+int slam_dist_prepare_graphs(slam_dist* d, double* capture_ms);
 /* resample exchange form: 1 = one launch (the default with one held shard whose
  * scan grid is co-resident), 0 = five launches; on < 0 only reports */
 int slam_dist_set_merged(slam_dist* d, int32_t on, int32_t* active);

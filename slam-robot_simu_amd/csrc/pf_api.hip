@@ -4,6 +4,7 @@
 // (or one shard of a multi-GPU filter), one HIP stream, SoA particle state
 // resident in HBM.
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
@@ -237,6 +238,27 @@ void drop_graphs(slam_pf* h) {
                 (void)hipGraphExecDestroy(gs[k]);
                 gs[k] = nullptr;
             }
+}
+
+int launch_step(slam_pf* h, bool host_noise);
+
+// One captured hipGraph of `steps` device-resident steps (slam_pf_run) for the
+// handle's current ping-pong parity; the step context lives in device memory,
+// so a replay needs no host input.  There is one graph per parity for
+// kGraphSteps steps (even: the parity comes back) and one for a single step.
+int capture_steps(slam_pf* h, hipGraphExec_t& ge, int steps) {
+    const int cur0 = h->cur;
+    hipGraph_t g;
+    SLAM_HIP_TRY(hipStreamBeginCapture(h->stream, hipStreamCaptureModeThreadLocal));
+    int rc = SLAM_OK;
+    for (int k = 0; k < steps && rc == SLAM_OK; ++k) rc = launch_step(h, false);
+    const hipError_t e = hipStreamEndCapture(h->stream, &g);
+    h->cur = cur0;
+    if (rc) return rc;
+    if (e != hipSuccess) return fail(SLAM_ERR_HIP, "hipStreamEndCapture failed");
+    SLAM_HIP_TRY(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
+    (void)hipGraphDestroy(g);
+    return SLAM_OK;
 }
 
 void release(slam_pf* h, void* p) {
@@ -1048,29 +1070,12 @@ int slam_pf_run(slam_pf* h, int32_t first_step, int32_t n_steps, const double* c
     if (!h->mt && (rc = launch_prestep(h))) return rc;         // the first step's closed-form words
     if (h->resample_next && (rc = launch_bsum(h))) return rc;   // prefix for the first step's scan
     const bool graphs = h->use_graph && !h->timing;
-    // one captured hipGraph per ping-pong parity for kGraphSteps steps (even:
-    // the parity comes back) and for a single step; the step context lives in
-    // device memory, so a replay needs no host input.
-    auto capture = [&](hipGraphExec_t& ge, int steps) -> int {
-        const int cur0 = h->cur;
-        hipGraph_t g;
-        SLAM_HIP_TRY(hipStreamBeginCapture(h->stream, hipStreamCaptureModeThreadLocal));
-        int rc2 = SLAM_OK;
-        for (int k = 0; k < steps && rc2 == SLAM_OK; ++k) rc2 = launch_step(h, false);
-        hipError_t e = hipStreamEndCapture(h->stream, &g);
-        h->cur = cur0;
-        if (rc2) return rc2;
-        if (e != hipSuccess) return fail(SLAM_ERR_HIP, "hipStreamEndCapture failed");
-        SLAM_HIP_TRY(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
-        (void)hipGraphDestroy(g);
-        return SLAM_OK;
-    };
     int32_t k = 0;
     while (k < n_steps) {
         if (graphs) {
             const bool multi = n_steps - k >= kGraphSteps;
             hipGraphExec_t& ge = multi ? h->graph_multi[h->cur] : h->graph[h->cur];
-            if (!ge && (rc = capture(ge, multi ? kGraphSteps : 1))) return rc;
+            if (!ge && (rc = capture_steps(h, ge, multi ? kGraphSteps : 1))) return rc;
             SLAM_HIP_TRY(hipGraphLaunch(ge, h->stream));
             const int done = multi ? kGraphSteps : 1;
             if (done & 1) h->cur = 1 - h->cur;
@@ -1085,6 +1090,26 @@ int slam_pf_run(slam_pf* h, int32_t first_step, int32_t n_steps, const double* c
         }
     }
     return sync_results(h, first_step, n_steps, results);
+}
+
+int slam_pf_prepare_graphs(slam_pf* h, double* capture_ms) {
+    SLAM_ARG_CHECK(h, "slam_pf_prepare_graphs: NULL handle");
+    SLAM_ARG_CHECK(h->n == h->n_global, "slam_pf_prepare_graphs: sharded handle");
+    SLAM_HIP_TRY(hipSetDevice(h->device));
+    const auto t0 = std::chrono::steady_clock::now();
+    int rc = SLAM_OK;
+    if (h->use_graph) {
+        const int cur0 = h->cur;
+        for (int par = 0; par < 2 && rc == SLAM_OK; ++par) {
+            h->cur = par;
+            if (!h->graph_multi[par]) rc = capture_steps(h, h->graph_multi[par], kGraphSteps);
+            if (!rc && !h->graph[par]) rc = capture_steps(h, h->graph[par], 1);
+        }
+        h->cur = cur0;
+    }
+    if (capture_ms)
+        *capture_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return rc;
 }
 
 int slam_pf_set_rng_mt19937(slam_pf* h, const uint32_t* key, int32_t pos, int32_t has_gauss,

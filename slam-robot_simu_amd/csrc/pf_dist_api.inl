@@ -139,6 +139,24 @@ int dist_sync_results(slam_dist* d, int32_t first, int32_t count, slam_pf_result
     return rc;
 }
 
+// One captured hipGraph of `steps` sharded steps for the shards' current
+// parity (slam_dist_run, slam_dist_prepare_graphs).
+int dist_capture(slam_dist* d, hipGraphExec_t& ge, int steps) {
+    hipStream_t s = d->sh[0]->stream;
+    std::vector<int> cur0;
+    for (auto* h : d->sh) cur0.push_back(h->cur);
+    hipGraph_t g;
+    SLAM_HIP_TRY(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+    int rc = SLAM_OK;
+    for (int k = 0; k < steps && rc == SLAM_OK; ++k) rc = dist_enqueue_step(d);
+    const hipError_t e = hipStreamEndCapture(s, &g);
+    for (int i = 0; i < d->nloc; ++i) d->sh[i]->cur = cur0[i];
+    if (rc) return rc;
+    if (e != hipSuccess) return fail(SLAM_ERR_HIP, "slam_dist_run: hipStreamEndCapture failed");
+    SLAM_HIP_TRY(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
+    (void)hipGraphDestroy(g);
+    return SLAM_OK;
+}
 }  // namespace
 
 extern "C" {
@@ -473,21 +491,6 @@ int slam_dist_run(slam_dist* d, int32_t first_step, int32_t n_steps, const doubl
     }
     const bool graphs = d->sh[0]->use_graph && !d->sh[0]->timing;
     hipStream_t s = d->sh[0]->stream;          // LOCAL: the shared stream; else the shard's
-    auto capture = [&](hipGraphExec_t& ge, int steps) -> int {
-        std::vector<int> cur0;
-        for (auto* h : d->sh) cur0.push_back(h->cur);
-        hipGraph_t g;
-        SLAM_HIP_TRY(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
-        int rc2 = SLAM_OK;
-        for (int k = 0; k < steps && rc2 == SLAM_OK; ++k) rc2 = dist_enqueue_step(d);
-        const hipError_t e = hipStreamEndCapture(s, &g);
-        for (int i = 0; i < d->nloc; ++i) d->sh[i]->cur = cur0[i];
-        if (rc2) return rc2;
-        if (e != hipSuccess) return fail(SLAM_ERR_HIP, "slam_dist_run: hipStreamEndCapture failed");
-        SLAM_HIP_TRY(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
-        (void)hipGraphDestroy(g);
-        return SLAM_OK;
-    };
     int rc;
     int32_t k = 0;
     while (k < n_steps) {
@@ -495,7 +498,7 @@ int slam_dist_run(slam_dist* d, int32_t first_step, int32_t n_steps, const doubl
         if (graphs) {
             const bool multi = n_steps - k >= kGraphSteps;
             hipGraphExec_t& ge = multi ? d->graph[par] : d->graph1[par];
-            if (!ge && (rc = capture(ge, multi ? kGraphSteps : 1))) return rc;
+            if (!ge && (rc = dist_capture(d, ge, multi ? kGraphSteps : 1))) return rc;
             SLAM_HIP_TRY(hipGraphLaunch(ge, s));
             const int done = multi ? kGraphSteps : 1;
             if (done & 1)
@@ -509,6 +512,26 @@ int slam_dist_run(slam_dist* d, int32_t first_step, int32_t n_steps, const doubl
         }
     }
     return dist_sync_results(d, first_step, n_steps, results);
+}
+
+int slam_dist_prepare_graphs(slam_dist* d, double* capture_ms) {
+    SLAM_ARG_CHECK(d && d->connected, "slam_dist_prepare_graphs: bad argument");
+    SLAM_HIP_TRY(hipSetDevice(d->device));
+    const auto t0 = std::chrono::steady_clock::now();
+    int rc = SLAM_OK;
+    if (d->sh[0]->use_graph) {
+        std::vector<int> cur0;
+        for (auto* h : d->sh) cur0.push_back(h->cur);
+        for (int par = 0; par < 2 && rc == SLAM_OK; ++par) {
+            for (auto* h : d->sh) h->cur = par;
+            if (!d->graph[par]) rc = dist_capture(d, d->graph[par], kGraphSteps);
+            if (!rc && !d->graph1[par]) rc = dist_capture(d, d->graph1[par], 1);
+        }
+        for (int i = 0; i < d->nloc; ++i) d->sh[i]->cur = cur0[i];
+    }
+    if (capture_ms)
+        *capture_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return rc;
 }
 
 }  // extern "C"

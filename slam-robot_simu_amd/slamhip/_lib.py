@@ -96,6 +96,7 @@ SIGNATURES = {
     "slam_pf_enable_timing": (C.c_int, [_P, C.c_int32]),
     "slam_pf_timing": (C.c_int, [_P, C.c_int32, _D, _I64]),
     "slam_pf_set_graphs": (C.c_int, [_P, C.c_int32]),
+    "slam_pf_prepare_graphs": (C.c_int, [_P, _D]),
     "slam_pf_set_scan_merged": (C.c_int, [_P, C.c_int32]),
     "slam_pf_set_ess_band": (C.c_int, [_P, C.c_double]),
     "slam_pf_set_resample_next": (C.c_int, [_P, C.c_int32]),
@@ -135,6 +136,7 @@ SIGNATURES = {
     "slam_dist_step": (C.c_int, [_P, _D, _D, C.POINTER(PFResult)]),
     "slam_dist_load_observations": (C.c_int, [_P, C.c_int32, _D]),
     "slam_dist_run": (C.c_int, [_P, C.c_int32, C.c_int32, _D, C.POINTER(PFResult)]),
+    "slam_dist_prepare_graphs": (C.c_int, [_P, _D]),
     "slam_dist_set_merged": (C.c_int, [_P, C.c_int32, C.POINTER(C.c_int32)]),
     "slam_ekf_create": (C.c_int, [C.POINTER(EKFConfig), C.c_int64, C.c_int, C.POINTER(_P)]),
     "slam_ekf_destroy": (C.c_int, [_P]),

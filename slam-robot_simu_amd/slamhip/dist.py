@@ -161,6 +161,12 @@ class DistFilter:
         check(self._lib.slam_dist_load_observations(self._d, z_all.shape[0], dptr(z_all)),
               "slam_dist_load_observations")
 
+    def prepare_graphs(self):
+        """DeviceParticleFilter.prepare_graphs for the sharded step."""
+        ms = C.c_double(0.0)
+        check(self._lib.slam_dist_prepare_graphs(self._d, C.byref(ms)), "slam_dist_prepare_graphs")
+        return ms.value
+
     def run(self, first_step, controls, want_results=True):
         controls = _f64(controls).reshape(-1, 2)
         k = controls.shape[0]

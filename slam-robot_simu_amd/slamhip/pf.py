@@ -208,6 +208,14 @@ class DeviceParticleFilter:
               "slam_pf_load_observations")
         self._z_steps = z_all.shape[0]
 
+    def prepare_graphs(self):
+        """Capture every step graph ``run`` replays (both parities, 8-step and
+        1-step) now, so that no capture lands in a timed run; returns the
+        capture time in ms."""
+        ms = C.c_double(0.0)
+        check(self._lib.slam_pf_prepare_graphs(self._h, C.byref(ms)), "slam_pf_prepare_graphs")
+        return ms.value
+
     def run(self, first_step, controls, want_results=True, confirm_ess=False):
         """Device-resident steps [first_step, first_step + len(controls)) from
         the loaded observations (hipGraph replays, no host decision).  Each

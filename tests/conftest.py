@@ -31,6 +31,34 @@ def _torch_hip_first(request):
     yield
 
 
+@pytest.fixture(scope="session")
+def c2_trajectory():
+    """The oracle's C2 trajectory (BASELINE configs[1]: 2^20 particles x 100
+    landmarks, velocity model, 8 steps with resamples): per step the input
+    state, the injected normals / observations / offset and the oracle's
+    outputs.  Shared by tests/test_gpu_c2.py and tests/test_gpu_zz_order.py."""
+    import pf_oracle as po
+    n, nl, n_steps = 1 << 20, 100, 8
+    rs = np.random.RandomState(1)
+    lm = rs.uniform(-10, 10, (nl, 2))
+    p = po.PFParams(n_particles=n, landmarks=lm, motion="velocity")
+    orc, world = po.PFOracle(p), po.PFWorld(p)
+    np.random.seed(2)
+    steps = []
+    for _ in range(n_steps):
+        world.advance()
+        state = (orc.x.copy(), orc.y.copy(), orc.th.copy(), orc.w.copy())
+        u = np.random.rand() if orc.needs_resample() else None
+        g = np.random.standard_normal(3 * n).reshape(n, 3)
+        z = world.observe()
+        out = orc.step(z, g, None if u is None else u * p.np_recip)
+        steps.append(dict(state=state, u=u, g=g, z=z, out=out,
+                          post=(orc.x.copy(), orc.y.copy(), orc.th.copy(), orc.w.copy()),
+                          resample_next=orc.needs_resample()))
+    assert sum(s["out"]["resampled"] for s in steps) >= 1
+    return p, steps
+
+
 def golden(name):
     return np.load(os.path.join(GOLDEN, name + ".npz"))
 

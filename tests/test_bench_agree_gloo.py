@@ -45,11 +45,24 @@ def _worker(rank, world, port, fail_rank, fail_phase, q):
         ag.checkpoint("handle exchange")
         ag.attempt(work, "connect")
         ag.checkpoint("connect")
-        ag.attempt(work, "warmup")
-        dist.barrier()                                      # timed region: barrier on every rank
-        ag.attempt(work, "timed")
-        dist.barrier()
-        ag.checkpoint("run")
+        # the real bench.timed_runs over a stand-in filter: a failure in any of
+        # its phases must still pair every barrier and reach the agreement
+        import numpy as np
+
+        class Filt:
+            def prepare_graphs(self):
+                return work("prepare")
+
+            def run(self, first, ctl, want_results=True):
+                return work({0: "warmup", 2: "timed"}.get(first, "timing run"))
+
+            def enable_timing(self, on):
+                work("enable timing")
+
+            def timing(self, k):
+                return (0.0, 0)
+
+        bench.timed_runs(Filt(), np.zeros((6, 2)), 2, 2, dist.barrier, ag)
         return "sharded"
 
     try:
@@ -67,7 +80,9 @@ def _worker(rank, world, port, fail_rank, fail_phase, q):
 
 @pytest.mark.parametrize("fail_rank,fail_phase,expect_phase",
                          [(None, None, None), (1, "connect", "connect"), (0, "export", "handle exchange"),
-                          (1, "timed", "run"), (0, "create", "shard create")])
+                          (1, "timed", "run"), (0, "create", "shard create"),
+                          (0, "prepare", "warm-up"), (1, "warmup", "warm-up"),
+                          (0, "timing run", "timing")])
 def test_one_rank_failure_agreed(fail_rank, fail_phase, expect_phase):
     import socket
     world = 2
