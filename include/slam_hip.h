@@ -78,7 +78,8 @@ typedef struct {
     int32_t ess_near;     /* |ess - ESS_TH| <= band * ESS_TH: the reference's `1 / (pw @ pw.T)`
                              (particle_filter.py:210, BLAS order) could decide resample_next
                              differently; the drop-in confirms such steps on the host */
-    int32_t dd_waves;     /* closed-form log-sum: wavefronts that took the double-double form */
+    int32_t dd_waves;     /* closed-form log-sum: wavefronts that took the double-double form
+                             (a sharded step's result: the first held shard's count only) */
 } slam_pf_result;
 
 /* ParticleFilter.__init__ (particle_filter.py:21-84).  landmarks: n_landmarks x 2 row-major. */
@@ -212,6 +213,11 @@ int slam_dist_connect(slam_dist* d, const void* all_blobs);
 int slam_dist_connect_comm(slam_dist* d, slam_comm* comm);      /* export + RCCL all-gather + connect */
 /* one step from host inputs (observations staged in slot 0, device RNG) */
 int slam_dist_step(slam_dist* d, const double* control, const double* z, slam_pf_result* res);
+/* Every wait on a peer is bounded (~2^24 polls); one that expires returns
+ * SLAM_ERR_COMM and marks the handle dead: every later step or run of it fails
+ * at once with SLAM_ERR_COMM (the shards' exchange state is no longer
+ * consistent).  Recover by destroying and recreating every shard and the
+ * slam_dist on every rank. */
 int slam_dist_load_observations(slam_dist* d, int32_t n_steps, const double* z_all);
 int slam_dist_run(slam_dist* d, int32_t first_step, int32_t n_steps, const double* controls,
                   slam_pf_result* results);
@@ -375,8 +381,10 @@ int slam_graph_set_edges(slam_graph* h, int64_t n_edges, const slam_graph_edge* 
  * cond} (:514).  On the PCG path det is NaN (not formed at this size) and cond
  * is the LOBPCG estimate lambda_max / lambda_min of H (inf when H is not
  * positive definite; NaN with SLAM_GRAPH_COND_OFF): is_calc = 1 means PCG
- * converged with positive curvature and cond < cond_max (:496), 0 that the
- * gate rejected H or PCG hit pcg_max_iter (poses unchanged either way). */
+ * converged with positive curvature and a converged estimate gave cond <
+ * cond_max (:496), 0 that the gate rejected H -- including an estimate that
+ * reached cond_max_iter unconverged (cond_info status 3: its ratio only bounds
+ * cond from below) -- or PCG hit pcg_max_iter (poses unchanged either way). */
 int slam_graph_update(slam_graph* h, double* stats);
 /* estimateOpticalTrajectory's loop: update until sum delta^2 < delta_sum_th
  * (:692-706) or max_iter; stats: max_iter x 4 (or NULL).  Returns

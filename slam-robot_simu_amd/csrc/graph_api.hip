@@ -562,7 +562,11 @@ int solve_pcg(slam_graph* h, double* stats, bool* solved, int32_t* iters) {
                                 ? std::numeric_limits<double>::infinity()
                                 : cs.lam[1] / cs.lam[0];
         stats[3] = cond;
-        gate = cond < h->cfg.cond_max;                        // :496
+        // :496 -- only a converged estimate certifies cond < cond_max: Ritz
+        // values lie inside [lambda_min, lambda_max], so an estimate stopped
+        // at cond_max_iter (status 3) only bounds cond from below and cannot
+        // pass the gate; status 2 / 4 reject for certain
+        gate = (cs.status == 1) && cond < h->cfg.cond_max;
         h->cond_warm = (cs.status == 1 || cs.status == 3);
         h->cond_last_iters = (cs.status == 1) ? cs.iter : 0;
         h->cond_info[0] = cs.iter;

@@ -50,6 +50,7 @@ struct MtBuffers {
     uint32_t* q = nullptr;          // x^(R S) mod phi: its set bits as 16-bit offsets (R > 1)
     int32_t n_idx = 0;              // offsets (a multiple of 16, padded)
     unsigned* bcnt = nullptr;       // accepted candidates per count block
+    unsigned* bpre = nullptr;       // [nb + 1] their exclusive prefix (many blocks only)
     double* normals = nullptr;      // G normals of the last request
     double* pre = nullptr;          // n_pre doubles of the last request (standalone use)
     int64_t g_cap = 0;              // normals per request this allocation holds

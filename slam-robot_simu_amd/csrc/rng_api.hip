@@ -36,6 +36,9 @@ constexpr int kMtGenThreads = 640;   // one lane per word of a block
 constexpr int kMtCandPerThread = 4;
 constexpr int kMtCountThreads = 256;
 constexpr int kMtCandPerBlock = kMtCountThreads * kMtCandPerThread;
+// emit blocks sum their predecessors' counts themselves up to this many blocks
+// (O(nb^2) reads in all); beyond, one prefix launch
+constexpr int kMtEmitSumMax = 4096;
 // requests one parallel round feeds: the jump (~160 us, LDS-bound) is paid
 // once per round, the sequential generation grows with it; 4 -> 16 took the
 // device stream from 0.229 to 0.201 ms per 2^20-particle step, 16 -> 32 from
@@ -246,20 +249,54 @@ __global__ __launch_bounds__(kMtCountThreads) void mt_count_kernel(
     }
 }
 
+// exclusive prefix of the count blocks' accepted pairs (one workgroup)
+__global__ __launch_bounds__(1024) void mt_bcnt_prefix_kernel(const unsigned* __restrict__ bcnt,
+                                                              const int64_t nb,
+                                                              unsigned* __restrict__ bpre) {
+    __shared__ unsigned s_w[16];
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    const int64_t per = (nb + 1023) / 1024, b0 = (int64_t)t * per;
+    unsigned loc = 0;
+    for (int64_t k = 0; k < per; ++k)
+        if (b0 + k < nb) loc += bcnt[b0 + k];
+    unsigned inc = loc;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const unsigned o = __shfl_up(inc, d, 64);
+        if (lane >= d) inc += o;
+    }
+    if (lane == 63) s_w[wave] = inc;
+    __syncthreads();
+    unsigned base = 0;
+    for (int w = 0; w < wave; ++w) base += s_w[w];
+    unsigned ex = base + inc - loc;
+    for (int64_t k = 0; k < per; ++k)
+        if (b0 + k < nb) {
+            bpre[b0 + k] = ex;
+            ex += bcnt[b0 + k];
+        }
+    if (t == 1023) bpre[nb] = base + inc;
+}
+
 __global__ __launch_bounds__(kMtCountThreads) void mt_emit_kernel(
     MtDeviceState* __restrict__ st, const uint32_t* __restrict__ X, const int64_t cap,
     const int32_t* __restrict__ pre_flag, const int64_t n_pre, const int64_t ncand,
-    const unsigned* __restrict__ bcnt, const int64_t nb, const int64_t g,
-    const GlibcLogTable* __restrict__ tab, double* __restrict__ normals, int32_t* __restrict__ status) {
+    const unsigned* __restrict__ bcnt, const unsigned* __restrict__ bpre, const int64_t nb,
+    const int64_t g, const GlibcLogTable* __restrict__ tab, double* __restrict__ normals,
+    int32_t* __restrict__ status) {
     const int64_t pw = mt_pre_words(pre_flag, n_pre);
     const int64_t w0 = st->p + pw;
     const int h = st->has_gauss ? 1 : 0;
     const int64_t P = mt_pairs(st, g);
     const int64_t c0 = (int64_t)blockIdx.x * kMtCandPerBlock + threadIdx.x * kMtCandPerThread;
     // the accepted pairs of the blocks before this one (integer sums: any order);
-    // block 0 sums every block's count for the short-draw check
-    const int64_t nsum = blockIdx.x == 0 ? nb : (int64_t)blockIdx.x;
+    // block 0 sums every block's count for the short-draw check.  Up to
+    // kMtEmitSumMax blocks each block sums its predecessors' counts itself
+    // (no scan launch); beyond, mt_bcnt_prefix_kernel's prefix (bpre) keeps
+    // the reads linear in the block count
+    const int64_t nsum = bpre ? 0 : (blockIdx.x == 0 ? nb : (int64_t)blockIdx.x);
     int64_t part = 0;
+    if (bpre && threadIdx.x == 0) part = bpre[blockIdx.x == 0 ? nb : blockIdx.x];
     for (int64_t i = threadIdx.x; i < nsum; i += kMtCountThreads) part += bcnt[i];
     double x1[kMtCandPerThread], x2[kMtCandPerThread], r2[kMtCandPerThread];
     bool acc[kMtCandPerThread];
@@ -584,7 +621,7 @@ int glibc_log_table(GlibcLogTable* out) {
 }
 
 void mt_free(MtBuffers& b) {
-    void* ps[] = {b.st, b.tab, b.X, b.seg, b.q, b.bcnt, b.normals, b.pre};
+    void* ps[] = {b.st, b.tab, b.X, b.seg, b.q, b.bcnt, b.bpre, b.normals, b.pre};
     for (void* p : ps)
         if (p) (void)hipFree(p);
     b = MtBuffers{};
@@ -657,6 +694,7 @@ int mt_reserve(MtBuffers& b, int64_t g_cap, int64_t pre_cap, int device) {
     SLAM_HIP_TRY(hipMalloc(&b.seg, sizeof(uint32_t) * kMtN * (size_t)b.R));
     SLAM_HIP_TRY(hipMalloc(&b.q, sizeof(uint32_t) * (kMtDeg / 2 + 16)));
     SLAM_HIP_TRY(hipMalloc(&b.bcnt, sizeof(unsigned) * (size_t)std::max<int64_t>(b.nb_count, 1)));
+    SLAM_HIP_TRY(hipMalloc(&b.bpre, sizeof(unsigned) * (size_t)(b.nb_count + 1)));
     SLAM_HIP_TRY(hipMalloc(&b.normals, sizeof(double) * (size_t)std::max<int64_t>(g_cap, 1)));
     SLAM_HIP_TRY(hipMalloc(&b.pre, sizeof(double) * (size_t)std::max<int64_t>(pre_cap, 1)));
     SLAM_HIP_TRY(hipMemcpy(b.tab, &T, sizeof(T), hipMemcpyHostToDevice));
@@ -747,10 +785,12 @@ int mt_enqueue(const MtBuffers& b, int64_t n_pre, const int32_t* pre_flag, doubl
     const unsigned nbc = (unsigned)((ncand + kMtCandPerBlock - 1) / kMtCandPerBlock);
     mt_count_kernel<<<std::max(nbc, 1u), kMtCountThreads, 0, s>>>(b.st, b.X, b.cap, pre_flag, n_pre,
                                                                    ncand, b.bcnt, RS, b.need);
+    const bool pre_scan = nbc > (unsigned)kMtEmitSumMax;
+    if (pre_scan) mt_bcnt_prefix_kernel<<<1, 1024, 0, s>>>(b.bcnt, (int64_t)nbc, b.bpre);
     if (nbc > 0)
         mt_emit_kernel<<<nbc, kMtCountThreads, 0, s>>>(b.st, b.X, b.cap, pre_flag, n_pre, ncand,
-                                                       b.bcnt, (int64_t)nbc, g, b.tab, b.normals,
-                                                       status);
+                                                       b.bcnt, pre_scan ? b.bpre : nullptr,
+                                                       (int64_t)nbc, g, b.tab, b.normals, status);
     SLAM_HIP_TRY(hipGetLastError());
     mt_finish_kernel<<<1, kMtGenThreads, 0, s>>>(b.st, b.X, b.cap, pre_flag, n_pre, pre_scale, pre_out,
                                                  pre_index, g, b.normals);

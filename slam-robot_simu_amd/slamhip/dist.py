@@ -66,7 +66,12 @@ def shard_range(n_global, world, rank):
 
 
 class DistFilter:
-    """One particle filter over ``world`` shards."""
+    """One particle filter over ``world`` shards.
+
+    Every wait on a peer is bounded; one that expires raises (SLAM_ERR_COMM)
+    and leaves this filter permanently unusable -- every later step or run
+    fails at once.  Recover by closing and recreating the DistFilter on every
+    rank (slam_hip.h, slam_dist_step)."""
 
     def __init__(self, n_global, landmarks, *, world, rank=None, comm=None, all_gather=None,
                  device=0, connect=True, **cfg_kw):

@@ -137,3 +137,44 @@ def test_c5_cond_estimate_matches_scipy():
     assert abs(last["lambda_min"] / lmin - 1) < 1e-3, (last, lmin)
     # the second update of the edge set starts from the first one's vectors
     assert infos[1]["iterations"] < infos[0]["iterations"], infos
+
+
+@pytest.mark.parametrize("solver", ["pcg", "dense"])
+def test_gate_anchor_removed_matches_numpy_cond(solver):
+    """the anchor (:475) removed leaves H with the gauge null space
+    (singular up to rounding), where lambda_min converges slowest.  is_calc of
+    both paths equals the reference's decision from numpy's exact det / cond
+    of the same H (:494-496)."""
+    from slamhip.graph import DeviceGraph
+    init, _, edges = _graph(300)
+    g = DeviceGraph(solver=solver, anchor=0.0, pcg_max_iter=4000)
+    try:
+        g.set_poses(init)
+        g.set_edges(edges)
+        ok, dsum, det, cond = g.update()
+        _, H, _, _ = g.get_system(dense=True)
+        info = g.cond_info() if solver == "pcg" else None
+    finally:
+        g.close()
+    ref = bool((0.1 < np.linalg.det(H)) and (np.linalg.cond(H) < 1e15))
+    assert bool(ok) == ref, (solver, ok, ref, det, cond, np.linalg.cond(H), info)
+    assert not ref
+
+
+def test_gate_rejects_unconverged_estimate():
+    """An estimate stopped at cond_max_iter (status 3) only bounds cond from
+    below, so it cannot pass the gate: is_calc 0 and the poses unchanged, on
+    the well-conditioned T = 300 graph whose converged estimate passes."""
+    from slamhip.graph import DeviceGraph
+    init, _, edges = _graph(300)
+    g = DeviceGraph(solver="pcg", cond_max_iter=20)
+    try:
+        g.set_poses(init)
+        g.set_edges(edges)
+        ok, dsum, det, cond = g.update()
+        info = g.cond_info()
+        assert info["status"] == 3, info
+        assert not ok and dsum == 0.0, (ok, dsum, cond, info)
+        np.testing.assert_array_equal(g.get_poses(), init)
+    finally:
+        g.close()
