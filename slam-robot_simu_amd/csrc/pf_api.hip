@@ -426,10 +426,19 @@ int launch_reduce(slam_pf* h, int32_t resampled_known) {
         DeferParts dp = h->dp;
         dp.fold = 0;
         dp.resampled_known = resampled_known;
+#ifdef SLAM_STEPEND_ONE
         stepend_kernel<<<1, kEndThreads, 0, s>>>(n, dp, h->w_un, h->s_cur, h->tail_leaves,
                                                  h->tail_ops, h->n_tail_leaves, h->n_tail_ops,
                                                  h->x[c], h->y[c], h->th[c], h->refp, h->flags,
                                                  step_io(h), h->pc.np_recip);
+#else
+        const int64_t groups = ((int64_t)h->nb_part + kGroupBlocks - 1) / kGroupBlocks;
+        const unsigned nbk = (unsigned)((groups + kEndThreads / 16 - 1) / (kEndThreads / 16));
+        stepend_groups_kernel<<<nbk, kEndThreads, 0, s>>>(
+            n, dp, h->w_un, h->s_cur, h->tail_leaves, h->tail_ops, h->n_tail_leaves,
+            h->n_tail_ops, h->x[c], h->y[c], h->th[c], h->refp, h->flags, step_io(h),
+            h->pc.np_recip);
+#endif
         toc(h, 1);
         SLAM_HIP_TRY(hipGetLastError());
         return SLAM_OK;
@@ -688,6 +697,9 @@ int create_impl(const slam_pf_config* cfg, int64_t n_local, int64_t n_global, in
         h->dp.ess_th = cfg->ess_threshold;
         h->dp.boff = h->boff;
         h->fold_ok = deferred && n_local == n_global && n_local % kSumChunk == 0;
+#ifdef SLAM_NO_FOLD                                           // A/B diagnostic
+        h->fold_ok = false;
+#endif
     }
     SLAM_HIP_TRY(hipMemsetAsync(h->dp.mark, 0xff, sizeof(int64_t) * npad, h->stream));
     SLAM_HIP_TRY(hipMemsetAsync(h->dp.carry, 0, sizeof(int32_t) * (h->nb_part + 1), h->stream));

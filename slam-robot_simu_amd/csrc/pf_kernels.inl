@@ -1337,7 +1337,11 @@ __global__ __launch_bounds__(256) SLAM_FUSED_ATTR void pf_fused_kernel(
         predict_particle<MOTION>(x[k], y[k], th[k], v, om, g[k][0], g[k][1], g[k][2], pc, xv[k],
                                  yv[k], tv[k], sp[k], cp[k]);
     if (DEFER) {                       // padded arrays: the pair is stored whole
+#ifdef SLAM_FOLD_PLAIN                                        // A/B diagnostic: not exact
+        if (false) {
+#else
         if (dp.fold) {                 // write-through: the folded step end may read them
+#endif
             const uint32_t bytes = gridDim.x * (uint32_t)(256 * P * 8);
             const auto rx = __builtin_amdgcn_make_buffer_rsrc(xo, 0, (int)bytes, kBufRsrcWord3);
             const auto ry = __builtin_amdgcn_make_buffer_rsrc(yo, 0, (int)bytes, kBufRsrcWord3);
@@ -1385,7 +1389,11 @@ __global__ __launch_bounds__(256) SLAM_FUSED_ATTR void pf_fused_kernel(
         wv[k] = valid[k] ? pw * bn[k] : 0.0;                     // particle_filter.py:194
     }
     if constexpr (DEFER) {
+#ifdef SLAM_FOLD_PLAIN
+        if (false) {
+#else
         if (dp.fold) {
+#endif
             const uint32_t bytes = gridDim.x * (uint32_t)(256 * P * 8);
             const auto rw = __builtin_amdgcn_make_buffer_rsrc(w_un, 0, (int)bytes, kBufRsrcWord3);
 #pragma unroll
@@ -1915,6 +1923,29 @@ __global__ __launch_bounds__(kEndThreads) void stepend_kernel(
                                      : 0.0;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    step_end_final(dp, G, nfull, tail, nb, n, w_un, xs, ys, ts, s_cur, refp, flags, io, np_recip);
+}
+
+// The step end as a launch of its own with the group records in parallel:
+// block k folds buffers 16k .. 16k + 15 (a 16-lane row each), takes a ticket,
+// and the last block runs step_end_final (after the np.sum of a last partial
+// buffer from its raw weights) -- the same arithmetic as the folded form.
+__global__ __launch_bounds__(kEndThreads) void stepend_groups_kernel(
+    const int64_t n, const DeferParts dp, const double* __restrict__ w_un, double* s_cur,
+    const int32_t* __restrict__ tail_leaves, const int32_t* __restrict__ tail_ops,
+    const int32_t n_tail_leaves, const int32_t n_tail_ops, const double* __restrict__ xs,
+    const double* __restrict__ ys, const double* __restrict__ ts, double* refp,
+    int32_t* __restrict__ flags, StepIO io, const double np_recip) {
+    __shared__ double sh[kSumChunk / 128 + 1];
+    const int lane = (int)__lane_id(), wave = (int)(threadIdx.x >> 6);
+    const int64_t nb = (n + kPartPer - 1) / kPartPer, G = (nb + kGroupBlocks - 1) / kGroupBlocks;
+    const int64_t nfull = n / kSumChunk;
+    const int64_t g = (int64_t)blockIdx.x * (kEndThreads / 16) + 4 * wave + (lane >> 4);
+    group_fold_rows(dp, g < G ? g : -1, nb, dp.grec);
+    if (!arrive_last_n(dp.gtk + G, gridDim.x)) return;
+    const double tail = (nfull < G) ? tail_chunk_sum(w_un + nfull * kSumChunk, tail_leaves, tail_ops,
+                                                     n_tail_leaves, n_tail_ops, sh)
+                                     : 0.0;
     step_end_final(dp, G, nfull, tail, nb, n, w_un, xs, ys, ts, s_cur, refp, flags, io, np_recip);
 }
 

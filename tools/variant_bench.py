@@ -26,4 +26,7 @@ pf.enable_timing(True)
 pf.run(2 * steps, ctl[2 * steps:])
 f = pf.timing(0)
 r = pf.timing(1)
-print(f"{os.environ.get('SLAM_HIP_LIB', 'default')}: step {el / steps * 1e3:.4f} ms  fused {f[0] / f[1] * 1e3:.1f} us  reduce {r[0] / r[1] * 1e3:.1f} us")
+s = pf.timing(2)
+print(f"{os.environ.get('SLAM_HIP_LIB', 'default')}: step {el / steps * 1e3:.4f} ms  "
+      f"fused {f[0] / max(f[1], 1) * 1e3:.1f} us  reduce {r[0] / max(r[1], 1) * 1e3:.1f} us  "
+      f"scan {s[0] / max(s[1], 1) * 1e3:.1f} us")
