@@ -112,7 +112,6 @@ struct slam_pf {
     double* s_cur = nullptr;
     DeferParts dp{};
     int32_t nb_part = 0;
-    bool fold_ok = false;       // the fused kernel ends the step itself (pf_stepend.inl)
     // NumPy's RandomState stream on the device (slam_pf_set_rng_mt19937)
     bool mt = false;
     MtBuffers mtb;
@@ -370,10 +369,7 @@ int launch_scans(slam_pf* h, int32_t force, bool with_s1) {
     return SLAM_OK;
 }
 
-// fold: the fused kernel runs the step end itself (h->fold_ok handles; no
-// launch_reduce then); resampled_known: the result's `resampled` (-1: the flag)
-int launch_fused(slam_pf* h, int motion, bool host_noise, bool fold = false,
-                 int32_t resampled_known = -1) {
+int launch_fused(slam_pf* h, int motion, bool host_noise) {
     const int64_t n = h->n;
     const int src = h->cur, dst = 1 - h->cur;
     hipStream_t s = h->stream;
@@ -383,15 +379,12 @@ int launch_fused(slam_pf* h, int motion, bool host_noise, bool fold = false,
     tic(h, 0);
     const double* w_in = h->deferred ? nullptr : h->w;     // deferred: read from w_un
     const double* nsrc = h->noise_src ? h->noise_src : h->noise;
-    DeferParts dp = h->dp;
-    dp.fold = (fold && h->fold_ok) ? 1 : 0;
-    dp.resampled_known = resampled_known;
 #define SLAM_FUSED_D(M, L, HN, D)                                                                \
     pf_fused_kernel<M, L, HN, D><<<g, 256, 0, s>>>(n, h->x[src], h->y[src], h->th[src],         \
                                                    h->x[dst], h->y[dst], h->th[dst], w_in,      \
                                                    h->w_un, h->c, h->flags, nsrc, h->lm, io,     \
                                                    h->pc, h->lc, h->cfg.seed, h->s_cur, h->refp, \
-                                                   dp)
+                                                   h->dp)
 #define SLAM_FUSED(M, L, HN) SLAM_FUSED_D(M, L, HN, true)     /* every handle is deferred */
     if (motion == kMotionNone) {
         if (lik == SLAM_LIK_PRODUCT) SLAM_FUSED(2, 0, false); else SLAM_FUSED(2, 1, false);
@@ -423,22 +416,10 @@ int launch_reduce(slam_pf* h, int32_t resampled_known) {
     const int c = h->cur;
     tic(h, 1);
     if (h->deferred) {
-        DeferParts dp = h->dp;
-        dp.fold = 0;
-        dp.resampled_known = resampled_known;
-#ifdef SLAM_STEPEND_ONE
-        stepend_kernel<<<1, kEndThreads, 0, s>>>(n, dp, h->w_un, h->s_cur, h->tail_leaves,
-                                                 h->tail_ops, h->n_tail_leaves, h->n_tail_ops,
-                                                 h->x[c], h->y[c], h->th[c], h->refp, h->flags,
-                                                 step_io(h), h->pc.np_recip);
-#else
-        const int64_t groups = ((int64_t)h->nb_part + kGroupBlocks - 1) / kGroupBlocks;
-        const unsigned nbk = (unsigned)((groups + kEndThreads / 16 - 1) / (kEndThreads / 16));
-        stepend_groups_kernel<<<nbk, kEndThreads, 0, s>>>(
-            n, dp, h->w_un, h->s_cur, h->tail_leaves, h->tail_ops, h->n_tail_leaves,
-            h->n_tail_ops, h->x[c], h->y[c], h->th[c], h->refp, h->flags, step_io(h),
-            h->pc.np_recip);
-#endif
+        finalize_deferred_kernel<<<1, kFinThreads, 0, s>>>(
+            n, h->dp, h->w_un, h->s_cur, h->tail_leaves, h->tail_ops, h->n_tail_leaves,
+            h->n_tail_ops, h->x[c], h->y[c], h->th[c], h->refp, h->flags, h->cfg.ess_threshold,
+            step_io(h), resampled_known, h->pc.np_recip, h->boff);
         toc(h, 1);
         SLAM_HIP_TRY(hipGetLastError());
         return SLAM_OK;
@@ -572,8 +553,8 @@ int launch_step(slam_pf* h, bool host_noise) {
     tic(h, 2);
     if ((rc = launch_scans(h, 0, false))) return rc;
     toc(h, 2);
-    if ((rc = launch_fused(h, h->cfg.motion, host_noise, true, -1))) return rc;
-    return h->fold_ok ? SLAM_OK : launch_reduce(h, -1);
+    if ((rc = launch_fused(h, h->cfg.motion, host_noise))) return rc;
+    return launch_reduce(h, -1);
 }
 
 int sync_results(slam_pf* h, int32_t first, int32_t count, slam_pf_result* out) {
@@ -686,21 +667,6 @@ int create_impl(const slam_pf_config* cfg, int64_t n_local, int64_t n_global, in
     A(h->dp.leaf, (size_t)(kPartPer / 128) * h->nb_part);
     A(h->dp.mark, npad);
     A(h->dp.carry, h->nb_part + 1);
-    {
-        // step-end group records (one per np.sum buffer) and their tickets
-        const int64_t groups = ((int64_t)h->nb_part + kGroupBlocks - 1) / kGroupBlocks;
-        double* grec = nullptr;
-        A(grec, 16 * groups);
-        h->dp.grec = reinterpret_cast<GroupRec*>(grec);
-        A(h->dp.gtk, groups + 1);
-        SLAM_HIP_TRY(hipMemsetAsync(h->dp.gtk, 0, sizeof(unsigned) * (groups + 1), h->stream));
-        h->dp.ess_th = cfg->ess_threshold;
-        h->dp.boff = h->boff;
-        h->fold_ok = deferred && n_local == n_global && n_local % kSumChunk == 0;
-#ifdef SLAM_NO_FOLD                                           // A/B diagnostic
-        h->fold_ok = false;
-#endif
-    }
     SLAM_HIP_TRY(hipMemsetAsync(h->dp.mark, 0xff, sizeof(int64_t) * npad, h->stream));
     SLAM_HIP_TRY(hipMemsetAsync(h->dp.carry, 0, sizeof(int32_t) * (h->nb_part + 1), h->stream));
     // tile totals: 2048-element tiles (shards) or 512-element wave tiles (deferred)
@@ -936,8 +902,8 @@ int slam_pf_step(slam_pf* h, const double* control, const double* z, const doubl
         if ((rc = launch_scans(h, 1, true))) return rc;
         toc(h, 2);
     }
-    if ((rc = launch_fused(h, h->cfg.motion, noise != nullptr, true, resampling))) return rc;
-    if (!h->fold_ok && (rc = launch_reduce(h, resampling))) return rc;
+    if ((rc = launch_fused(h, h->cfg.motion, noise != nullptr))) return rc;
+    if ((rc = launch_reduce(h, resampling))) return rc;
     toc(h, 3);
     h->stepno++;
     return sync_results(h, 0, 1, res);
@@ -1035,8 +1001,8 @@ int slam_pf_update(slam_pf* h, const double* z, slam_pf_result* res) {
     const double ctl[2] = {0.0, 0.0};
     if ((rc = stage_inputs(h, ctl, z, nullptr, std::nan("")))) return rc;
     if ((rc = set_flag(h, kFlagResample, 0))) return rc;
-    if ((rc = launch_fused(h, kMotionNone, false, true, 0))) return rc;
-    if (!h->fold_ok && (rc = launch_reduce(h, 0))) return rc;
+    if ((rc = launch_fused(h, kMotionNone, false))) return rc;
+    if ((rc = launch_reduce(h, 0))) return rc;
     return sync_results(h, 0, 1, res);
 }
 
@@ -1191,8 +1157,8 @@ int slam_pf_step_truth(slam_pf* h, const double* control, const double* truth, d
         if ((rc = launch_scans(h, 1, true))) return rc;
         toc(h, 2);
     }
-    if ((rc = launch_fused(h, h->cfg.motion, true, true, resampling))) return rc;
-    if (!h->fold_ok && (rc = launch_reduce(h, resampling))) return rc;
+    if ((rc = launch_fused(h, h->cfg.motion, true))) return rc;
+    if ((rc = launch_reduce(h, resampling))) return rc;
     toc(h, 3);
     h->stepno++;
     if (z_out && h->nl)

@@ -1,12 +1,54 @@
-// pf_finalize.inl -- layout constants of the one-workgroup reductions over the
-// fused blocks' partials, shared by the sharded step's record (pf_dist.inl:
-// dist_reduce_kernel).  The single-GPU step end is pf_stepend.inl.
+// pf_finalize.inl -- end of a deferred-normalisation PF step (included by
+// pf_kernels.inl).  One workgroup of 512 lanes (8 waves, two per SIMD: the
+// serial parts of the step end -- np.sum's left-to-right buffer chain, the
+// result record -- run on a wave that shares its SIMD with one other wave
+// only).
+//
+// Work: np.sum of the unnormalised weights from the fused blocks' leaf sums
+// (particle_filter.py:234), the block partials rescaled to the global max and
+// combined in a fixed order (ESS :210 and the weighted covariance), the exact
+// max / first argmax of w = w_un / s (:115-117), the result record, the step
+// context, s for the next step, and -- when the next step resamples -- the
+// prefix of the fused-block weight totals for its exact cumsum (:212).
+//
+// Latency plan: every lane issues the loads of its four fused blocks and its
+// sixteen leaves first (NP <= 2^20: one memory round trip); the argmax
+// records of the few candidate blocks are fetched while lane 0 runs the
+// serial buffer chain.  Argmax: fl(w_un / s) is monotone in w_un, so the
+// first block b with fl(M_b / s) == fl(M / s) holds it; inside b the first
+// index of M_b is the answer unless a smaller weight before it rounds to the
+// same value (fl(pre_b / s) == fl(M / s)), which is then checked element by
+// element.  A non-positive or non-finite s (all weights NaN -> 1/NP, :236)
+// takes a slow whole-array pass.
 
-constexpr int kFinThreads = 512;
+#ifdef SLAM_FIN_PROBE
+__device__ long long g_fin_probe[16];
+#define FIN_STAMP(k) do { if (threadIdx.x == 0) g_fin_probe[k] = wall_clock64(); } while (0)
+#else
+#define FIN_STAMP(k) do { } while (0)
+#endif
+
+#ifndef SLAM_FIN_THREADS
+#define SLAM_FIN_THREADS 512
+#endif
+constexpr int kFinThreads = SLAM_FIN_THREADS;
 constexpr int kFinWaves = kFinThreads / 64;
 constexpr int kFinRegBlocks = 2048 / kFinThreads;   // fused blocks held in registers per lane (2048)
 constexpr int kFinLeafLanes = 4;            // lanes per 8192-element buffer (16 leaves each)
 constexpr int kFinBufPerRound = kFinThreads / kFinLeafLanes;   // 128 buffers per round
+constexpr int kFinCand = 8;                 // argmax candidate records staged in LDS
+
+struct FinRecord {
+    double pre, xe[3];
+    int64_t pi;
+};
+
+__device__ __forceinline__ void fin_load_record(const DeferParts& dp, const int64_t b, FinRecord& f) {
+    f.pre = dp.ppre[b];
+    f.pi = dp.pidx[b];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) f.xe[j] = dp.pxe[j][b];
+}
 
 // A lane of the np.sum pass takes 4 consecutive fused blocks of a buffer: each
 // block left the pairwise sum of its four 128-element leaves (a perfect
@@ -14,8 +56,352 @@ constexpr int kFinBufPerRound = kFinThreads / kFinLeafLanes;   // 128 buffers pe
 // 16-leaf subtree.
 static_assert(kSumChunk == 16 * kPartPer, "a buffer is 16 fused blocks, 4 per np.sum lane");
 
+// s + a[0] + a[1] + ... + a[cnt - 1], left to right (np.sum's buffer chain),
+// with the next 16 LDS words in flight while the current 16 are added
+__device__ __forceinline__ double lds_chain_sum(double s, const double* a, const int cnt) {
+    constexpr int B = 16;
+    int k = 0;
+    if (cnt >= B) {
+        double cur[B];
+#pragma unroll
+        for (int j = 0; j < B; ++j) cur[j] = a[j];
+        for (; k + 2 * B <= cnt; k += B) {
+            double nxt[B];
+#pragma unroll
+            for (int j = 0; j < B; ++j) nxt[j] = a[k + B + j];
+#pragma unroll
+            for (int j = 0; j < B; ++j) s = s + cur[j];
+#pragma unroll
+            for (int j = 0; j < B; ++j) cur[j] = nxt[j];
+        }
+#pragma unroll
+        for (int j = 0; j < B; ++j) s = s + cur[j];
+        k += B;
+    }
+    for (; k < cnt; ++k) s = s + a[k];
+    return s;
+}
+
 // register block k of lane t (k < kFinRegBlocks): neighbour pairs, increasing in k
 __device__ __forceinline__ int64_t fin_blk(const int t, const int k) {
     static_assert(kFinRegBlocks % 2 == 0, "pairs of blocks");
     return 2 * (int64_t)t + (k & 1) + 2 * (int64_t)kFinThreads * (k >> 1);
+}
+
+__global__ __launch_bounds__(kFinThreads) void finalize_deferred_kernel(
+    const int64_t n, const DeferParts dp, const double* __restrict__ w_un,
+    double* __restrict__ s_cur, const int32_t* __restrict__ tail_leaves,
+    const int32_t* __restrict__ tail_ops, const int32_t n_tail_leaves, const int32_t n_tail_ops,
+    const double* __restrict__ xs, const double* __restrict__ ys, const double* __restrict__ ts,
+    double* __restrict__ refp, int32_t* __restrict__ flags, const double ess_th, StepIO io,
+    const int32_t resampled_known, const double np_recip, double* __restrict__ boff) {
+    __shared__ double sh[2048];                      // buffer sums / tail leaves / block totals
+    __shared__ double s_q[11][kFinThreads];
+    __shared__ BlockPartial shp[kFinWaves];
+    __shared__ double s_wmax[kFinWaves];
+    __shared__ double s_tot[11];
+    __shared__ double s_s;
+    __shared__ unsigned long long s_min;
+    __shared__ int32_t s_flag;
+    __shared__ int64_t s_mi;
+    __shared__ double s_xe[3];
+    __shared__ int s_ncand;
+    __shared__ int64_t s_cblk[kFinCand];
+    __shared__ FinRecord s_crec[kFinCand];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int64_t nb = (n + kPartPer - 1) / kPartPer;
+    const int64_t nfull = n / kSumChunk;
+    const int64_t nch = (n + kSumChunk - 1) / kSumChunk;
+    FIN_STAMP(0);
+    if (tid == 0) {
+        s_ncand = 0;
+        s_min = ~0ull;
+        s_flag = 0;
+    }
+    // ---- loads, issued up front: this lane's blocks fin_blk(tid, k) (pairs of
+    // neighbours, one 16-byte load per array: the partial arrays hold nb + 1
+    // entries) and its leaves
+    double pm[kFinRegBlocks], q[kFinRegBlocks][11];
+    bool has[kFinRegBlocks];
+#pragma unroll
+    for (int kp = 0; kp < kFinRegBlocks / 2; ++kp) {
+        const int64_t b = fin_blk(tid, 2 * kp);
+        has[2 * kp] = b < nb;
+        has[2 * kp + 1] = b + 1 < nb;
+        const int64_t bb = has[2 * kp] ? b : 0;
+        const double2 t = *reinterpret_cast<const double2*>(dp.pmax + bb);
+        pm[2 * kp] = t.x;
+        pm[2 * kp + 1] = t.y;
+#pragma unroll
+        for (int j = 0; j < 11; ++j) {
+            const double2 u = *reinterpret_cast<const double2*>(dp.ps[j] + bb);
+            q[2 * kp][j] = u.x;
+            q[2 * kp + 1][j] = u.y;
+        }
+    }
+    const int part = tid & (kFinLeafLanes - 1);
+    double L[4];                                   // fused-block subtree sums
+    {
+        const int64_t c = tid / kFinLeafLanes;
+        const double* Lp = dp.leaf + 16 * (c < nfull ? c : 0) + 4 * part;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) L[j] = Lp[j];
+    }
+    // ---- lane partial sums scaled to the lane's max (rescaled to the global
+    // max once that is known); q dies here except the totals q[k][0]
+    double mlane = -1.0;
+#pragma unroll
+    for (int k = 0; k < kFinRegBlocks; ++k)
+        if (has[k]) mlane = fmax(mlane, pm[k]);
+    // NP > 2^20: blocks beyond the registers (two passes: max, then sums)
+    const int64_t bx0 = tid + (int64_t)kFinThreads * kFinRegBlocks;
+    for (int64_t b = bx0; b < nb; b += kFinThreads) mlane = fmax(mlane, dp.pmax[b]);
+    double acc[11];
+#pragma unroll
+    for (int j = 0; j < 11; ++j) acc[j] = 0.0;
+    if (mlane > 0.0) {
+        const double rm = 1.0 / mlane;
+#pragma unroll
+        for (int k = 0; k < kFinRegBlocks; ++k) {
+            if (has[k]) {
+                const double r = pm[k] * rm;
+                acc[0] += r * q[k][0];
+                acc[1] += (r * r) * q[k][1];
+#pragma unroll
+                for (int j = 2; j < 11; ++j) acc[j] += r * q[k][j];
+            }
+        }
+        for (int64_t b = bx0; b < nb; b += kFinThreads) {
+            const double r = dp.pmax[b] * rm;
+            acc[0] += r * dp.ps[0][b];
+            acc[1] += (r * r) * dp.ps[1][b];
+#pragma unroll
+            for (int j = 2; j < 11; ++j) acc[j] += r * dp.ps[j][b];
+        }
+    }
+    const double mx = wave_max_f64(mlane);
+    if (lane == 0) s_wmax[wave] = mx;
+    // ---- np.sum: 8192-element buffers, 128 per round, pairwise inside
+    double s = 0.0;
+    for (int64_t c0 = 0; c0 < nfull; c0 += kFinBufPerRound) {
+        const int64_t cnt = (nfull - c0 < kFinBufPerRound) ? nfull - c0 : kFinBufPerRound;
+        const int64_t c = c0 + tid / kFinLeafLanes;
+        double v = 0.0;
+        if (tid / kFinLeafLanes < cnt) {
+            if (c0 > 0) {
+                const double* Lp = dp.leaf + 16 * c + 4 * part;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) L[j] = Lp[j];
+            }
+            v = (L[0] + L[1]) + (L[2] + L[3]);
+        }
+        static_assert(kFinLeafLanes == 4, "two quad swaps");
+        {
+            const double o = dpp_f64<kDppXor1>(v);
+            v = (part & 1) ? (o + v) : (v + o);          // left operand = lower lane
+        }
+        {
+            const double o = dpp_f64<kDppXor2>(v);
+            v = (part & 2) ? (o + v) : (v + o);
+        }
+        if (c0 > 0) __syncthreads();                     // lane 0 is done with the previous round
+        if (part == 0 && tid / kFinLeafLanes < cnt) sh[tid / kFinLeafLanes] = v;
+        __syncthreads();
+        if (c0 + kFinBufPerRound < nfull && tid == 0) {  // not the last round: fold it now
+            s = lds_chain_sum(s, sh, (int)cnt);
+        }
+    }
+    if (nfull == 0) __syncthreads();                     // s_wmax visible
+    const int64_t last_cnt = nfull - ((nfull - 1) / kFinBufPerRound) * kFinBufPerRound;
+    double M = s_wmax[0];
+#pragma unroll
+    for (int w = 1; w < kFinWaves; ++w) M = fmax(M, s_wmax[w]);
+    FIN_STAMP(1);
+    if (tid == 0) {
+        // the last round's buffers left to right (the other waves meanwhile
+        // rescale their partials and fetch the argmax candidates)
+        __builtin_amdgcn_s_setprio(3);
+        if (nfull > 0)
+            s = lds_chain_sum(s, sh, (int)last_cnt);
+        __builtin_amdgcn_s_setprio(0);
+    }
+    {
+        const double rl = (mlane > 0.0 && M > 0.0) ? mlane / M : 0.0;
+        acc[0] *= rl;
+        acc[1] *= rl * rl;
+#pragma unroll
+        for (int j = 2; j < 11; ++j) acc[j] *= rl;
+#pragma unroll
+        for (int j = 0; j < 11; ++j) s_q[j][tid] = acc[j];
+    }
+    // argmax records of the candidate blocks (fl(M_b / s) == fl(M / s) needs
+    // M_b within 2 ulp of M), staged in LDS
+#pragma unroll
+    for (int k = 0; k < kFinRegBlocks; ++k) {
+        if (has[k] && pm[k] >= M * (1.0 - 0x1p-48)) {
+            const int slot = atomicAdd(&s_ncand, 1);
+            if (slot < kFinCand) {
+                const int64_t b = fin_blk(tid, k);
+                FinRecord f;
+                fin_load_record(dp, b, f);
+                s_cblk[slot] = b;
+                s_crec[slot] = f;
+            }
+        }
+    }
+    if (nch > nfull) {
+        __syncthreads();                                  // sh reused by the tail
+        const double tsum = tail_chunk_sum(w_un + nfull * kSumChunk, tail_leaves, tail_ops,
+                                           n_tail_leaves, n_tail_ops, sh);
+        if (tid == 0) s = s + tsum;
+    }
+    if (tid == 0) s_s = s;
+    __syncthreads();
+    s = s_s;
+    FIN_STAMP(2);
+    const bool ok = (s > 0.0) && !isinf(s) && (M > 0.0);
+    BlockPartial tot;
+    bp_zero(tot);
+    if (ok) {
+        // ---- the 11 sums: wave w reduces quantities w and w + 8 (lane-strided
+        // reads, then a butterfly with the lower lane on the left)
+        for (int j = wave; j < 11; j += kFinWaves) {
+            double r = s_q[j][lane];
+#pragma unroll
+            for (int m = 1; m < kFinThreads / 64; ++m) r = r + s_q[j][lane + 64 * m];
+#pragma unroll
+            for (int d = 1; d < 64; d <<= 1) {
+                const double o = xor_f64(r, d);
+                r = (lane & d) ? (o + r) : (r + o);
+            }
+            if (lane == 0) s_tot[j] = r;
+        }
+        // ---- argmax: the first block whose max rounds to fl(M / s)
+        const double mval = M / s;
+        unsigned long long cb = ~0ull;
+#pragma unroll
+        for (int k = kFinRegBlocks - 1; k >= 0; --k)
+            if (has[k] && pm[k] >= M * (1.0 - 0x1p-48) && pm[k] / s == mval)
+                cb = (unsigned long long)fin_blk(tid, k);
+        for (int64_t b = tid + (int64_t)kFinThreads * kFinRegBlocks; b < nb; b += kFinThreads)
+            if (cb == ~0ull && dp.pmax[b] / s == mval) cb = (unsigned long long)b;
+        if (cb != ~0ull) atomicMin(&s_min, cb);
+        __syncthreads();
+        const int64_t bc = (int64_t)s_min;
+        if (tid == 0) {
+            // block bc's record: staged, or loaded if bc was not a staged candidate
+            int slot = -1;
+            const int nc = min(s_ncand, kFinCand);
+            for (int j = 0; j < nc; ++j)
+                if (s_cblk[j] == bc) slot = j;
+            FinRecord f;
+            if (slot >= 0) f = s_crec[slot];
+            else fin_load_record(dp, bc, f);
+            s_mi = f.pi;
+            s_xe[0] = f.xe[0];
+            s_xe[1] = f.xe[1];
+            s_xe[2] = f.xe[2];
+            s_flag = (f.pre / s == mval) ? 1 : 0;
+            if (s_flag) s_min = ~0ull;
+        }
+        __syncthreads();
+        if (s_flag) {
+            // a smaller weight ahead of the block max rounds to the same maximum:
+            // the first index of the block whose w equals mval
+            for (int e = tid; e < kPartPer; e += kFinThreads) {
+                const int64_t i = bc * kPartPer + e;
+                if (i < n && norm_w(w_un[i], s, np_recip) == mval)
+                    atomicMin(&s_min, (unsigned long long)i);
+            }
+            __syncthreads();
+            if (tid == 0) {
+                const int64_t i = (int64_t)s_min;
+                s_mi = i;
+                s_xe[0] = xs[i];
+                s_xe[1] = ys[i];
+                s_xe[2] = ts[i];
+            }
+        }
+        if (tid == 0) {
+            const double f = M / s;                      // back from max-relative to w_un / s
+            tot.maxv = mval;
+            tot.maxi = s_mi;
+            tot.sw = s_tot[0] * f;
+            tot.sw2 = s_tot[1] * (f * f);
+            for (int j = 0; j < 3; ++j) tot.m1[j] = s_tot[2 + j] * f;
+            for (int j = 0; j < 6; ++j) tot.m2[j] = s_tot[5 + j] * f;
+        }
+    } else {
+        // ---- every weight through the reference's division (slow, degenerate case)
+        BlockPartial a;
+        bp_zero(a);
+        const double r0 = refp[0], r1 = refp[1], r2 = refp[2];
+        for (int64_t i = tid; i < n; i += kFinThreads) {
+            const double v = norm_w(w_un[i], s, np_recip);
+            BlockPartial o;
+            o.maxv = v;
+            o.maxi = i;
+            o.sw = v;
+            o.sw2 = v * v;
+            const double d0 = xs[i] - r0, d1 = ys[i] - r1, d2 = ts[i] - r2;
+            const double v0 = v * d0, v1 = v * d1, v2 = v * d2;
+            o.m1[0] = v0; o.m1[1] = v1; o.m1[2] = v2;
+            o.m2[0] = v0 * d0; o.m2[1] = v0 * d1; o.m2[2] = v0 * d2;
+            o.m2[3] = v1 * d1; o.m2[4] = v1 * d2; o.m2[5] = v2 * d2;
+            bp_merge(a, o);
+        }
+        tot = bp_block_reduce(a, shp);
+        if (tid == 0) {
+            s_xe[0] = xs[tot.maxi];
+            s_xe[1] = ys[tot.maxi];
+            s_xe[2] = ts[tot.maxi];
+        }
+    }
+    FIN_STAMP(3);
+    if (tid == 0) {
+        const int32_t st = io.ctr[0];
+        write_result_xe(tot, s_xe, refp, s, flags, ess_th, io.ess_band, io.res + st, resampled_known);
+        s_flag = flags[kFlagResample];
+        io.ctr[0] = st + 1;
+        io.ctr[1] = io.ctr[1] + 1;
+        *s_cur = s;
+    }
+    __syncthreads();
+    FIN_STAMP(4);
+    if (s_flag) {
+        // fused-block totals of w for the next step's exact cumsum (S1), moved
+        // through LDS so that lane t owns the contiguous blocks [t per, (t+1) per)
+        auto btot_slow = [&](int64_t b) {
+            double v = 0.0;
+            const int64_t e = (b + 1) * kPartPer < n ? (b + 1) * kPartPer : n;
+            for (int64_t i = b * kPartPer; i < e; ++i) v += norm_w(w_un[i], s, np_recip);
+            return v;
+        };
+        const bool in_lds = ok && nb <= 2048;
+        if (in_lds) {
+#pragma unroll
+            for (int k = 0; k < kFinRegBlocks; ++k)
+                if (has[k]) sh[fin_blk(tid, k)] = (pm[k] / s) * q[k][0];
+        }
+        __syncthreads();
+        auto btot = [&](int64_t b) {
+            if (in_lds) return sh[b];
+            if (ok) return (dp.pmax[b] / s) * dp.ps[0][b];
+            return btot_slow(b);
+        };
+        const int per = (int)((nb + kFinThreads - 1) / kFinThreads);
+        const int64_t b0 = (int64_t)tid * per;
+        double loc = 0.0;
+        for (int k = 0; k < per; ++k)
+            if (b0 + k < nb) loc += btot(b0 + k);
+        double total;
+        double ex = block_excl_scan<double, kFinThreads>(loc, s_q[0], total);
+        for (int k = 0; k < per; ++k)
+            if (b0 + k < nb) {
+                boff[b0 + k] = ex;
+                ex = ex + btot(b0 + k);
+            }
+        if (tid == 0) boff[nb] = total;
+    }
+    FIN_STAMP(5);
 }

@@ -55,13 +55,6 @@ struct DeferParts {
     double* leaf;           // [blocks] the block's np.sum subtree (its kPartPer / 128 leaves, pairwise)
     int64_t* mark;          // [npad] resample-run starts: (RNG step << 32) | source (expand pass)
     int32_t* carry;         // [blocks] source of each fused block's first position
-    // the step end (pf_stepend.inl)
-    struct GroupRec* grec;  // [groups] np.sum-buffer records (16 fused blocks each)
-    unsigned* gtk;          // [groups + 1] arrival tickets (the last arriver re-zeroes)
-    double* boff;           // [blocks + 1] next resample step's block-total prefix
-    double ess_th;
-    int32_t fold;           // 1: the fused kernel ends the step itself (no step-end launch)
-    int32_t resampled_known;  // result.resampled: >= 0 known, -1 from the device flag
 };
 
 // particle_filter.py:179-181 + the mlab.bivariate_normal constants

@@ -139,13 +139,6 @@ __device__ __forceinline__ void st_wt_i(int32_t* p, int32_t v) {
 __device__ __forceinline__ int32_t ld_wt_i(const int32_t* p) {
     return __hip_atomic_load((int32_t*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-// 16-byte write-through store (buffer store, cache bits sc1: the R1 form of
-// the microarch guide); kBufRsrcWord3: gfx9 raw-buffer descriptor word 3
-constexpr int kBufRsrcWord3 = 0x00020000;
-__device__ __forceinline__ void st2_sc1(__amdgpu_buffer_rsrc_t r, uint32_t off, double a, double b) {
-    typedef unsigned v4u __attribute__((ext_vector_type(4)));
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, double2{a, b}), r, (int)off, 0, 16);
-}
 template <typename S>
 __device__ __forceinline__ void st_wt_struct(S* dst, const S& v) {
     static_assert(sizeof(S) % 8 == 0, "8-byte granules");
@@ -428,9 +421,9 @@ __device__ void defer_epilogue(const int64_t base, const int64_t n, const double
         const int64_t i = base + kDeferPPT * t + k;
         if (i < bi) pre = fmax(pre, wv[k]);
         if (i == bi) {
-            st_wt_d(dp.pxe[0] + blk, xv[k]);           // write-through: the step end
-            st_wt_d(dp.pxe[1] + blk, yv[k]);           // may read them in this launch
-            st_wt_d(dp.pxe[2] + blk, tv[k]);
+            dp.pxe[0][blk] = xv[k];
+            dp.pxe[1][blk] = yv[k];
+            dp.pxe[2][blk] = tv[k];
         }
     }
     pre = wave_max_f64(pre);
@@ -454,7 +447,7 @@ __device__ void defer_epilogue(const int64_t base, const int64_t n, const double
     if (t < kQ) {
         double acc = s_seg[16 * t];
         for (int mm = 1; mm < 16; ++mm) acc = acc + s_seg[16 * t + mm];
-        st_wt_d(dp.ps[t] + blk, acc);
+        dp.ps[t][blk] = acc;
     } else if (t >= 64 && t < 128) {
         // the block's np.sum subtree: its kLeaves leaves, then their pair sums
         // (wave 1; lane l < kLeaves holds leaf l)
@@ -468,11 +461,11 @@ __device__ void defer_epilogue(const int64_t base, const int64_t n, const double
             const double o = xor_f64(v, d);
             v = (lane & d) ? (o + v) : (v + o);
         }
-        if (t == 64) st_wt_d(dp.leaf + blk, v);
+        if (t == 64) dp.leaf[blk] = v;
     } else if (t == 128) {
-        st_wt_d(dp.pmax + blk, M);
-        st_wt(dp.pidx + blk, (uint64_t)bi);
-        st_wt_d(dp.ppre + blk, fmax(fmax(s_pre[0], s_pre[1]), fmax(s_pre[2], s_pre[3])));
+        dp.pmax[blk] = M;
+        dp.pidx[blk] = bi;
+        dp.ppre[blk] = fmax(fmax(s_pre[0], s_pre[1]), fmax(s_pre[2], s_pre[3]));
     }
 }
 
@@ -1044,73 +1037,6 @@ __device__ __forceinline__ int likelihood_lanes(const double* xn, const double* 
     return lane_dd;
 }
 
-// ====================================================================
-// normalise (particle_filter.py:226-237) + reductions; the last block
-// combines the block partials in block order and writes the step result.
-// ====================================================================
-__device__ __forceinline__ void bp_zero(BlockPartial& a) {
-    a.maxv = -1.0;
-    a.maxi = INT64_MAX;
-    a.sw = a.sw2 = 0.0;
-    for (int k = 0; k < 3; ++k) a.m1[k] = 0.0;
-    for (int k = 0; k < 6; ++k) a.m2[k] = 0.0;
-}
-
-__device__ __forceinline__ void bp_merge(BlockPartial& r, const BlockPartial& o) {
-    if (o.maxv > r.maxv || (o.maxv == r.maxv && o.maxi < r.maxi)) {
-        r.maxv = o.maxv;
-        r.maxi = o.maxi;
-    }
-    r.sw += o.sw;
-    r.sw2 += o.sw2;
-    for (int q = 0; q < 3; ++q) r.m1[q] += o.m1[q];
-    for (int q = 0; q < 6; ++q) r.m2[q] += o.m2[q];
-}
-
-// xor-butterfly over the 64 lanes (lower lane always on the left: a fixed tree)
-template <int W = 64>
-__device__ __forceinline__ void bp_wave_reduce(BlockPartial& a) {
-#pragma unroll
-    for (int d = 1; d < W; d <<= 1) {
-        BlockPartial o;
-        o.maxv = __shfl_xor(a.maxv, d, 64);
-        o.maxi = __shfl_xor(a.maxi, d, 64);
-        o.sw = __shfl_xor(a.sw, d, 64);
-        o.sw2 = __shfl_xor(a.sw2, d, 64);
-#pragma unroll
-        for (int k = 0; k < 3; ++k) o.m1[k] = __shfl_xor(a.m1[k], d, 64);
-#pragma unroll
-        for (int k = 0; k < 6; ++k) o.m2[k] = __shfl_xor(a.m2[k], d, 64);
-        if (threadIdx.x & d) {
-            bp_merge(o, a);
-            a = o;
-        } else {
-            bp_merge(a, o);
-        }
-    }
-}
-
-// block-level fixed-order reduction of per-thread partials (result in thread 0):
-// a butterfly inside every wave, then a butterfly over the wave partials in wave 0
-__device__ __forceinline__ BlockPartial bp_block_reduce(BlockPartial a, BlockPartial* shp) {
-    bp_wave_reduce(a);
-    const int nw = (int)(blockDim.x >> 6);
-    if ((threadIdx.x & 63) == 0) shp[threadIdx.x >> 6] = a;
-    __syncthreads();
-    BlockPartial r;
-    if (threadIdx.x < 64) {
-        if ((int)threadIdx.x < nw) r = shp[threadIdx.x];
-        else bp_zero(r);
-        if (nw > 8) bp_wave_reduce<16>(r);
-        else if (nw > 4) bp_wave_reduce<8>(r);
-        else bp_wave_reduce<4>(r);
-    }
-    __syncthreads();
-    return r;
-}
-
-#include "pf_stepend.inl"
-
 // The fused step kernel: [resample gather +] predict + likelihood + weight.
 // DEFER = false (shards): one particle per lane, previous weights normalised
 // in w_in.  DEFER = true (single GPU, gbase = 0, particle arrays padded to
@@ -1135,7 +1061,7 @@ __global__ __launch_bounds__(256) SLAM_FUSED_ATTR void pf_fused_kernel(
     double* __restrict__ to, const double* __restrict__ w_in, double* __restrict__ w_un,
     const double* __restrict__ c, int32_t* __restrict__ flags, const double* __restrict__ noise,
     const double* __restrict__ lm, StepIO io, PredictConst pc, LikConst lc, uint64_t seed,
-    const double* s_in, const double* refp, DeferParts dp) {
+    const double* __restrict__ s_in, const double* __restrict__ refp, DeferParts dp) {
     static_assert(!DEFER || kDeferPPT % 2 == 0, "the deferred path moves particle pairs");
     const int32_t st = io.ctr[0];
     const uint32_t rstep = (uint32_t)io.ctr[1];
@@ -1337,29 +1263,11 @@ __global__ __launch_bounds__(256) SLAM_FUSED_ATTR void pf_fused_kernel(
         predict_particle<MOTION>(x[k], y[k], th[k], v, om, g[k][0], g[k][1], g[k][2], pc, xv[k],
                                  yv[k], tv[k], sp[k], cp[k]);
     if (DEFER) {                       // padded arrays: the pair is stored whole
-#ifdef SLAM_FOLD_PLAIN                                        // A/B diagnostic: not exact
-        if (false) {
-#else
-        if (dp.fold) {                 // write-through: the folded step end may read them
-#endif
-            const uint32_t bytes = gridDim.x * (uint32_t)(256 * P * 8);
-            const auto rx = __builtin_amdgcn_make_buffer_rsrc(xo, 0, (int)bytes, kBufRsrcWord3);
-            const auto ry = __builtin_amdgcn_make_buffer_rsrc(yo, 0, (int)bytes, kBufRsrcWord3);
-            const auto rt = __builtin_amdgcn_make_buffer_rsrc(to, 0, (int)bytes, kBufRsrcWord3);
 #pragma unroll
-            for (int h = 0; h < P; h += 2) {
-                const uint32_t off = (uint32_t)(i0 + h) * 8u;
-                st2_sc1(rx, off, xv[h], xv[h + 1]);
-                st2_sc1(ry, off, yv[h], yv[h + 1]);
-                st2_sc1(rt, off, tv[h], tv[h + 1]);
-            }
-        } else {
-#pragma unroll
-            for (int h = 0; h < P; h += 2) {
-                *reinterpret_cast<double2*>(xo + i0 + h) = double2{xv[h], xv[h + 1]};
-                *reinterpret_cast<double2*>(yo + i0 + h) = double2{yv[h], yv[h + 1]};
-                *reinterpret_cast<double2*>(to + i0 + h) = double2{tv[h], tv[h + 1]};
-            }
+        for (int h = 0; h < P; h += 2) {
+            *reinterpret_cast<double2*>(xo + i0 + h) = double2{xv[h], xv[h + 1]};
+            *reinterpret_cast<double2*>(yo + i0 + h) = double2{yv[h], yv[h + 1]};
+            *reinterpret_cast<double2*>(to + i0 + h) = double2{tv[h], tv[h + 1]};
         }
     } else if (valid[0]) {
         xo[i0] = xv[0];
@@ -1389,20 +1297,9 @@ __global__ __launch_bounds__(256) SLAM_FUSED_ATTR void pf_fused_kernel(
         wv[k] = valid[k] ? pw * bn[k] : 0.0;                     // particle_filter.py:194
     }
     if constexpr (DEFER) {
-#ifdef SLAM_FOLD_PLAIN
-        if (false) {
-#else
-        if (dp.fold) {
-#endif
-            const uint32_t bytes = gridDim.x * (uint32_t)(256 * P * 8);
-            const auto rw = __builtin_amdgcn_make_buffer_rsrc(w_un, 0, (int)bytes, kBufRsrcWord3);
 #pragma unroll
-            for (int h = 0; h < P; h += 2) st2_sc1(rw, (uint32_t)(i0 + h) * 8u, wv[h], wv[h + 1]);
-        } else {
-#pragma unroll
-            for (int h = 0; h < P; h += 2)
-                *reinterpret_cast<double2*>(w_un + i0 + h) = double2{wv[h], wv[h + 1]};
-        }
+        for (int h = 0; h < P; h += 2)
+            *reinterpret_cast<double2*>(w_un + i0 + h) = double2{wv[h], wv[h + 1]};
 #ifndef SLAM_NO_EPILOGUE
         defer_epilogue(base, n, wv, xv, yv, tv, refp, dp, wave_s);
 #endif
@@ -1421,18 +1318,6 @@ __global__ __launch_bounds__(256) SLAM_FUSED_ATTR void pf_fused_kernel(
                 closed_prep_reference(refp, 2, io.ctl[2 * sn], io.ctl[2 * sn + 1], pc.dt, io.motion,
                                       px, py, pth);
                 closed_prep_constants(s_prep, lc.nl, px, py, pth, io.zc + (size_t)sn * kZcWords);
-            }
-        }
-        // the folded step end (pf_stepend.inl): the 16th block of an np.sum
-        // buffer to finish folds the buffer's partials, the last buffer's
-        // folder runs the step end
-        if (dp.fold) {
-            const int64_t nb = gridDim.x, G = nb / kGroupBlocks, g = blockIdx.x / kGroupBlocks;
-            if (arrive_last_n(dp.gtk + g, kGroupBlocks)) {
-                if (wave_s == 0) group_fold_rows(dp, (__lane_id() < 16) ? g : -1, nb, dp.grec);
-                if (arrive_last_n(dp.gtk + G, (unsigned)G))
-                    step_end_final(dp, G, G, 0.0, nb, n, w_un, xo, yo, to, const_cast<double*>(s_in),
-                                   const_cast<double*>(refp), flags, io, pc.np_recip);
             }
         }
     } else if (valid[0]) {
@@ -1644,6 +1529,71 @@ __device__ void block_scan_pair(const uint64_t* kin, uint64_t* kout, uint64_t* k
     }
 }
 
+// ====================================================================
+// normalise (particle_filter.py:226-237) + reductions; the last block
+// combines the block partials in block order and writes the step result.
+// ====================================================================
+__device__ __forceinline__ void bp_zero(BlockPartial& a) {
+    a.maxv = -1.0;
+    a.maxi = INT64_MAX;
+    a.sw = a.sw2 = 0.0;
+    for (int k = 0; k < 3; ++k) a.m1[k] = 0.0;
+    for (int k = 0; k < 6; ++k) a.m2[k] = 0.0;
+}
+
+__device__ __forceinline__ void bp_merge(BlockPartial& r, const BlockPartial& o) {
+    if (o.maxv > r.maxv || (o.maxv == r.maxv && o.maxi < r.maxi)) {
+        r.maxv = o.maxv;
+        r.maxi = o.maxi;
+    }
+    r.sw += o.sw;
+    r.sw2 += o.sw2;
+    for (int q = 0; q < 3; ++q) r.m1[q] += o.m1[q];
+    for (int q = 0; q < 6; ++q) r.m2[q] += o.m2[q];
+}
+
+// xor-butterfly over the 64 lanes (lower lane always on the left: a fixed tree)
+template <int W = 64>
+__device__ __forceinline__ void bp_wave_reduce(BlockPartial& a) {
+#pragma unroll
+    for (int d = 1; d < W; d <<= 1) {
+        BlockPartial o;
+        o.maxv = __shfl_xor(a.maxv, d, 64);
+        o.maxi = __shfl_xor(a.maxi, d, 64);
+        o.sw = __shfl_xor(a.sw, d, 64);
+        o.sw2 = __shfl_xor(a.sw2, d, 64);
+#pragma unroll
+        for (int k = 0; k < 3; ++k) o.m1[k] = __shfl_xor(a.m1[k], d, 64);
+#pragma unroll
+        for (int k = 0; k < 6; ++k) o.m2[k] = __shfl_xor(a.m2[k], d, 64);
+        if (threadIdx.x & d) {
+            bp_merge(o, a);
+            a = o;
+        } else {
+            bp_merge(a, o);
+        }
+    }
+}
+
+// block-level fixed-order reduction of per-thread partials (result in thread 0):
+// a butterfly inside every wave, then a butterfly over the wave partials in wave 0
+__device__ __forceinline__ BlockPartial bp_block_reduce(BlockPartial a, BlockPartial* shp) {
+    bp_wave_reduce(a);
+    const int nw = (int)(blockDim.x >> 6);
+    if ((threadIdx.x & 63) == 0) shp[threadIdx.x >> 6] = a;
+    __syncthreads();
+    BlockPartial r;
+    if (threadIdx.x < 64) {
+        if ((int)threadIdx.x < nw) r = shp[threadIdx.x];
+        else bp_zero(r);
+        if (nw > 8) bp_wave_reduce<16>(r);
+        else if (nw > 4) bp_wave_reduce<8>(r);
+        else bp_wave_reduce<4>(r);
+    }
+    __syncthreads();
+    return r;
+}
+
 // result record from the combined partial (x_est = particle at the argmax)
 __device__ void write_result(const BlockPartial& r, const double* xs, const double* ys,
                              const double* ts, const int64_t gbase, double* refp,
@@ -1703,15 +1653,12 @@ __device__ void write_result_xe(const BlockPartial& r, const double* xe, double*
         for (int b = 0; b < 3; ++b) o.cov[3 * a + b] = m2[3 * a + b] * inv - mu[a] * mu[b];
     o.ess = 1.0 / r.sw2;
     o.weight_sum = s;
-    // the words other workgroups of this launch update atomically (status
-    // bits, double-double wave count) read at agent scope: the folded step
-    // end runs in the fused launch itself
-    o.resampled = resampled_known >= 0 ? resampled_known : (ld_wt_i(&flags[kFlagResample]) != 0);
+    o.resampled = resampled_known >= 0 ? resampled_known : (flags[kFlagResample] != 0);
     o.resample_next = (o.ess < ess_th) ? 1 : 0;
     o.ess_near = (fabs(o.ess - ess_th) <= ess_band * ess_th) ? 1 : 0;
-    o.status = ld_wt_i(&flags[kFlagStatus]);
-    o.n_special = ld_wt_i(&flags[kFlagNSpecial]);
-    o.dd_waves = ld_wt_i(&flags[kFlagDDWaves]);
+    o.status = flags[kFlagStatus];
+    o.n_special = flags[kFlagNSpecial];
+    o.dd_waves = flags[kFlagDDWaves];
     flags[kFlagDDWaves] = 0;
     flags[kFlagResample] = o.resample_next;
     flags[kFlagMarkGen] = flags[kFlagMarkGen] + 1;
@@ -1897,56 +1844,6 @@ __device__ double tail_chunk_sum(const double* __restrict__ w, const int32_t* __
     }
     __syncthreads();
     return out;
-}
-
-// The step end as its own launch (sync-mode steps, NP not a multiple of 8192,
-// the likelihood-only update): the group records by the 16-lane rows of every
-// wave, the np.sum of a last partial buffer from its raw weights, then
-// step_end_final -- the folded step end's arithmetic, bit for bit.
-__global__ __launch_bounds__(kEndThreads) void stepend_kernel(
-    const int64_t n, const DeferParts dp, const double* __restrict__ w_un, double* s_cur,
-    const int32_t* __restrict__ tail_leaves, const int32_t* __restrict__ tail_ops,
-    const int32_t n_tail_leaves, const int32_t n_tail_ops, const double* __restrict__ xs,
-    const double* __restrict__ ys, const double* __restrict__ ts, double* refp,
-    int32_t* __restrict__ flags, StepIO io, const double np_recip) {
-    __shared__ double sh[kSumChunk / 128 + 1];
-    const int lane = (int)__lane_id(), wave = (int)(threadIdx.x >> 6);
-    const int64_t nb = (n + kPartPer - 1) / kPartPer, G = (nb + kGroupBlocks - 1) / kGroupBlocks;
-    const int64_t nfull = n / kSumChunk;
-    constexpr int kRows = kEndThreads / 16;
-    for (int64_t g0 = 0; g0 < G; g0 += kRows) {
-        const int64_t g = g0 + 4 * wave + (lane >> 4);
-        group_fold_rows(dp, g < G ? g : -1, nb, dp.grec);
-    }
-    const double tail = (nfull < G) ? tail_chunk_sum(w_un + nfull * kSumChunk, tail_leaves, tail_ops,
-                                                     n_tail_leaves, n_tail_ops, sh)
-                                     : 0.0;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    step_end_final(dp, G, nfull, tail, nb, n, w_un, xs, ys, ts, s_cur, refp, flags, io, np_recip);
-}
-
-// The step end as a launch of its own with the group records in parallel:
-// block k folds buffers 16k .. 16k + 15 (a 16-lane row each), takes a ticket,
-// and the last block runs step_end_final (after the np.sum of a last partial
-// buffer from its raw weights) -- the same arithmetic as the folded form.
-__global__ __launch_bounds__(kEndThreads) void stepend_groups_kernel(
-    const int64_t n, const DeferParts dp, const double* __restrict__ w_un, double* s_cur,
-    const int32_t* __restrict__ tail_leaves, const int32_t* __restrict__ tail_ops,
-    const int32_t n_tail_leaves, const int32_t n_tail_ops, const double* __restrict__ xs,
-    const double* __restrict__ ys, const double* __restrict__ ts, double* refp,
-    int32_t* __restrict__ flags, StepIO io, const double np_recip) {
-    __shared__ double sh[kSumChunk / 128 + 1];
-    const int lane = (int)__lane_id(), wave = (int)(threadIdx.x >> 6);
-    const int64_t nb = (n + kPartPer - 1) / kPartPer, G = (nb + kGroupBlocks - 1) / kGroupBlocks;
-    const int64_t nfull = n / kSumChunk;
-    const int64_t g = (int64_t)blockIdx.x * (kEndThreads / 16) + 4 * wave + (lane >> 4);
-    group_fold_rows(dp, g < G ? g : -1, nb, dp.grec);
-    if (!arrive_last_n(dp.gtk + G, gridDim.x)) return;
-    const double tail = (nfull < G) ? tail_chunk_sum(w_un + nfull * kSumChunk, tail_leaves, tail_ops,
-                                                     n_tail_leaves, n_tail_ops, sh)
-                                     : 0.0;
-    step_end_final(dp, G, nfull, tail, nb, n, w_un, xs, ys, ts, s_cur, refp, flags, io, np_recip);
 }
 
 #include "pf_finalize.inl"
