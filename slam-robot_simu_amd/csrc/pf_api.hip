@@ -93,6 +93,7 @@ struct slam_pf {
     double* ofs = nullptr;
     slam_pf_result* res_dev = nullptr;
     slam_pf_result* res_host = nullptr;   // pinned
+    double* ctl_pin = nullptr;            // pinned staging of a batch's controls
     int32_t* ctr = nullptr;               // [0] step in batch, [1] RNG step
     int32_t z_steps = 0;
     LikConst lc;
@@ -280,6 +281,8 @@ int ensure_steps(slam_pf* h, int32_t steps) {
     release(h, h->res_dev);
     if (h->res_host) (void)hipHostFree(h->res_host);
     h->res_host = nullptr;
+    if (h->ctl_pin) (void)hipHostFree(h->ctl_pin);
+    h->ctl_pin = nullptr;
     int rc;
     const size_t nlz = 2 * (size_t)std::max<int32_t>(h->nl, 1);
     if ((rc = dalloc(h, &h->ctl, 2 * (size_t)steps)) || (rc = dalloc(h, &h->z_all, nlz * steps)) ||
@@ -288,21 +291,32 @@ int ensure_steps(slam_pf* h, int32_t steps) {
         (rc = dalloc(h, &h->res_dev, (size_t)steps)))
         return rc;
     SLAM_HIP_TRY(hipHostMalloc((void**)&h->res_host, sizeof(slam_pf_result) * steps));
+    SLAM_HIP_TRY(hipHostMalloc((void**)&h->ctl_pin, 2 * sizeof(double) * steps));
     h->cap = steps;
     h->z_steps = 0;
     h->truth_steps = 0;
     return SLAM_OK;
 }
 
+// Device words set by memset nodes (the value travels in the call; no host
+// buffer, so the host does not wait as for a pageable copy)
 int set_ctr(slam_pf* h, int32_t step) {
-    const int32_t v[2] = {step, (int32_t)h->stepno};
-    SLAM_HIP_TRY(hipMemcpyAsync(h->ctr, v, sizeof(v), hipMemcpyHostToDevice, h->stream));
+    SLAM_HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)h->ctr, step, 1, h->stream));
+    SLAM_HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)(h->ctr + 1), (int)h->stepno, 1, h->stream));
     return SLAM_OK;
 }
 
 int set_flag(slam_pf* h, int word, int32_t v) {
-    SLAM_HIP_TRY(hipMemcpyAsync(h->flags + word, &v, sizeof(int32_t), hipMemcpyHostToDevice,
-                                h->stream));
+    SLAM_HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)(h->flags + word), v, 1, h->stream));
+    return SLAM_OK;
+}
+
+// controls of a device-resident batch through pinned staging (an asynchronous
+// copy; every run ends with a stream synchronize, so the staging is free again)
+int upload_controls(slam_pf* h, int32_t first_step, int32_t n_steps, const double* controls) {
+    std::memcpy(h->ctl_pin, controls, 2 * (size_t)n_steps * sizeof(double));
+    SLAM_HIP_TRY(hipMemcpyAsync(h->ctl + 2 * first_step, h->ctl_pin, 2 * (size_t)n_steps * sizeof(double),
+                                hipMemcpyHostToDevice, h->stream));
     return SLAM_OK;
 }
 
@@ -802,6 +816,7 @@ int slam_pf_destroy(slam_pf* h) {
     mt_free(h->mtb);
     for (void* p : h->allocs) (void)hipFree(p);
     if (h->res_host) (void)hipHostFree(h->res_host);
+    if (h->ctl_pin) (void)hipHostFree(h->ctl_pin);
     for (int k = 0; k < 4; ++k)
         for (auto& pr : h->tm.ev[k]) {
             (void)hipEventDestroy(pr.first);
@@ -1065,8 +1080,7 @@ int slam_pf_run(slam_pf* h, int32_t first_step, int32_t n_steps, const double* c
                          : "slam_pf_run: steps outside the loaded observations");
     SLAM_HIP_TRY(hipSetDevice(h->device));
     int rc;
-    SLAM_HIP_TRY(hipMemcpyAsync(h->ctl + 2 * first_step, controls, 2 * n_steps * sizeof(double),
-                                hipMemcpyHostToDevice, h->stream));
+    if ((rc = upload_controls(h, first_step, n_steps, controls))) return rc;
     if ((rc = set_ctr(h, first_step)) || (rc = set_flag(h, kFlagResample, h->resample_next))) return rc;
     if (!h->mt && (rc = launch_prestep(h))) return rc;         // the first step's closed-form words
     if (h->resample_next && (rc = launch_bsum(h))) return rc;   // prefix for the first step's scan

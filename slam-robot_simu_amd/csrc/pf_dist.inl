@@ -1307,8 +1307,7 @@ __device__ __forceinline__ void dist_finalize(const int64_t n, const DeferParts&
             sh[e] = ld_sys_d(&ch[g - s_nc[q]]);
         }
         __syncthreads();
-        if (tid == 0)
-            for (int64_t k = 0; k < cnt; ++k) s = s + sh[k];
+        if (tid == 0) s = lds_chain_sum(s, sh, (int)cnt);     // same adds, next 16 words in flight
         __syncthreads();
     }
     if (tid == 0) {

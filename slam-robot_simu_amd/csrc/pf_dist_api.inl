@@ -485,9 +485,8 @@ int slam_dist_run(slam_dist* d, int32_t first_step, int32_t n_steps, const doubl
     for (auto* h : d->sh) {
         SLAM_ARG_CHECK(first_step >= 0 && first_step + n_steps <= h->z_steps,
                        "slam_dist_run: steps outside the loaded observations");
-        SLAM_HIP_TRY(hipMemcpyAsync(h->ctl + 2 * first_step, controls, 2 * n_steps * sizeof(double),
-                                    hipMemcpyHostToDevice, h->stream));
-        int rc = set_ctr(h, first_step);
+        int rc = upload_controls(h, first_step, n_steps, controls);
+        if (!rc) rc = set_ctr(h, first_step);
         if (rc || (rc = launch_prestep(h))) return rc;       // the first step's closed-form words
     }
     const bool graphs = d->sh[0]->use_graph && !d->sh[0]->timing;
