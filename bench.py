@@ -520,28 +520,66 @@ class Agreement:
             raise ShardedFailure(phase, mine)
 
 
-def timed_runs(filt, ctl, warmup, steps, barrier_sync, ag=None):
+def connect_exchange(ag, connect, use_collectives=None):
+    """The sharded filter's exchange: the peer-memory connect on every rank; if
+    it failed on any rank (a peer's region that cannot be mapped), every rank
+    switches to the collective exchange (RCCL all-gathers and grouped
+    send/recv between the step's kernels) when use_collectives is given.
+    Returns (mode, why): "peer" or "rccl", and the agreed failure that led to
+    the fallback.  Raises ShardedFailure when no exchange could be set up."""
+    ag.attempt(connect)
+    try:
+        ag.checkpoint("connect")
+        return "peer", None
+    except ShardedFailure as e:
+        if use_collectives is None:
+            raise
+        ag.err = None                       # every rank knows; start the fallback together
+        ag.attempt(use_collectives)
+        ag.checkpoint("collectives")
+        return "rccl", e.args
+
+
+SETTLE_BATCH = 31      # 16 + 8 + 4 + 2 + 1: every captured graph shape once per batch
+
+
+def settle(run, ctl, n):
+    """`n` untimed steps (whole SETTLE_BATCH batches) before the warm-up: the
+    device's clocks come up under load over ~20 ms and the first replay of each
+    graph shape pays a one-time cost; without this a 5-step warm-up leaves
+    both inside a 20-step timed run.  A fixed count, so that every
+    rank of a sharded run replays the same steps."""
+    for s0 in range(0, n - n % SETTLE_BATCH, SETTLE_BATCH):
+        run(s0, ctl[s0:s0 + SETTLE_BATCH], want_results=False)
+    return n - n % SETTLE_BATCH
+
+
+def timed_runs(filt, ctl, warmup, steps, barrier_sync, ag=None, settle_steps=0):
     """Every step graph captured first (graph_capture_ms, never inside a timed
-    run), `warmup` untimed steps, `steps` timed steps between barrier +
-    synchronize, then a kernel-timing pass over `steps` more steps (HIP events
-    on the filter's stream around every launch).  With an Agreement (the
+    run), `settle_steps` untimed steps (settle), `warmup` untimed steps, `steps`
+    timed steps between barrier + synchronize, then a kernel-timing pass over
+    `steps` more steps (HIP events on the filter's stream around every launch).
+    ctl holds settle_steps + warmup + 2 steps rows.  With an Agreement (the
     sharded mode) a rank's failure is caught, every rank still reaches every
     barrier, and the ranks agree on it at the next checkpoint."""
     call = ag.attempt if ag is not None else (lambda fn, *a, **kw: fn(*a, **kw))
     cap_ms = call(filt.prepare_graphs)
+    s0 = call(settle, filt.run, ctl, settle_steps) if settle_steps else 0
+    s0 = s0 or 0                                   # (a failed attempt returns None)
+    ctl = ctl[s0:]
     if warmup:
-        call(filt.run, 0, ctl[:warmup], want_results=False)
+        call(filt.run, s0, ctl[:warmup], want_results=False)
     if ag is not None:
         ag.checkpoint("warm-up")
     barrier_sync()
     t0 = time.perf_counter()
-    out = call(filt.run, warmup, ctl[warmup:warmup + steps])
+    out = call(filt.run, s0 + warmup, ctl[warmup:warmup + steps])
     barrier_sync()
     elapsed = time.perf_counter() - t0
     if ag is not None:
         ag.checkpoint("run")
     call(filt.enable_timing, True)
-    call(filt.run, warmup + steps, ctl[warmup + steps:])
+    call(filt.run, s0 + warmup + steps, ctl[warmup + steps:warmup + 2 * steps])
     timing = call(lambda: {k: filt.timing(k) for k in range(4)})
     call(filt.enable_timing, False)
     if ag is not None:
@@ -561,6 +599,9 @@ def main():
     ap.add_argument("--total-particles", type=int, default=None,
                     help="strong scaling: one filter of this many particles over the N ranks")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--settle-steps", type=int, default=20 * SETTLE_BATCH,
+                    help="untimed steps before the warm-up (whole batches of 31: every graph "
+                         "shape; device clocks up); reported as settle_steps")
     ap.add_argument("--no-secondary", action="store_true",
                     help="skip the EKF / EKF-SLAM / graph-SLAM rows (rank 0, N = 1 only)")
     args = ap.parse_args()
@@ -599,7 +640,8 @@ def main():
         return int(t.item()) == 1
 
     from slamhip.pf import DeviceParticleFilter
-    total_steps = args.warmup + 2 * args.steps
+    settle_steps = args.settle_steps - args.settle_steps % SETTLE_BATCH
+    total_steps = settle_steps + args.warmup + 2 * args.steps
     lm, zs, (vel, omega, dt) = simulate_world(total_steps)
     ctl = np.tile([vel, omega], (total_steps, 1))
 
@@ -608,6 +650,8 @@ def main():
             import torch
             dist.barrier()
             torch.cuda.synchronize()
+
+    exchange_mode = ["peer"]
 
     def measure_sharded(likelihood, n_global):
         # one filter over n_global particles (BASELINE configs[2]): this rank's
@@ -642,13 +686,20 @@ def main():
                 else:
                     blobs = comm.all_gather_bytes(blob if blob is not None else bytes(len_blob(filt)))
                 ag.checkpoint("handle exchange")
-                ag.attempt(filt.connect, blobs)
+
+                def connect():
+                    filt.connect(blobs)
+                    if os.environ.get("SLAM_BENCH_FAIL_CONNECT_RANK") == str(rank):   # tests
+                        raise RuntimeError(f"injected connect failure on rank {rank}")
+                mode, why = connect_exchange(
+                    ag, connect, (lambda: filt.use_collectives(comm)) if comm is not None else None)
+                exchange_mode[0] = mode if why is None else f"{mode} (peer-memory connect failed: {why[1] or 'another rank'})"
                 if fail_rank is not None and int(fail_rank) == rank:
                     ag.attempt(_raise, RuntimeError(f"injected failure on rank {rank} after connect"))
-                ag.checkpoint("connect")
+                ag.checkpoint("connect done")
             ag.attempt(filt.load_observations, zs)
             ag.checkpoint("load")
-            return timed_runs(filt, ctl, args.warmup, args.steps, barrier_sync, ag)
+            return timed_runs(filt, ctl, args.warmup, args.steps, barrier_sync, ag, settle_steps)
         finally:
             if filt is not None:
                 filt.close()
@@ -662,7 +713,7 @@ def main():
                                   likelihood=likelihood, seed=1234 + rank, device=local_rank)
         try:
             pf.load_observations(zs)
-            return timed_runs(pf, ctl, args.warmup, args.steps, barrier_sync)
+            return timed_runs(pf, ctl, args.warmup, args.steps, barrier_sync, settle_steps=settle_steps)
         finally:
             pf.close()
 
@@ -676,11 +727,12 @@ def main():
             pf.use_numpy_stream(np.random.RandomState(1234))
             pf.load_truth(simulate_world.poses)
             pf.prepare_graphs()
+            s0 = settle(pf.run, ctl, settle_steps)
             if args.warmup:
-                pf.run(0, ctl[:args.warmup], want_results=False)
+                pf.run(s0, ctl[s0:s0 + args.warmup], want_results=False)
             barrier_sync()
             t0 = time.perf_counter()
-            pf.run(args.warmup, ctl[args.warmup:args.warmup + args.steps])
+            pf.run(s0 + args.warmup, ctl[s0 + args.warmup:s0 + args.warmup + args.steps])
             barrier_sync()
             return time.perf_counter() - t0
         finally:
@@ -752,6 +804,7 @@ def main():
                                   "resample": res_ms / max(res_n, 1),
                                   "step_events": step_ms / max(step_n, 1)},
         "graph_capture_ms": cap_ms,
+        "settle_steps": settle_steps,
         "resample_steps": int(sum(o["resampled"] for o in out)),
         "ess_near_steps": int(sum(o.get("ess_near", False) for o in out)),
         "closed_form_fallback_waves": int(sum(o.get("dd_waves", 0) for o in out)),
@@ -795,6 +848,10 @@ def main():
         line["cpu_baseline_vectorised"] = vb
     if sharded_error is not None:
         line["sharded_error"] = sharded_error
+    if args.mode == "sharded" and multi:
+        # peer: the kernels' stores into IPC-mapped peer regions over xGMI;
+        # rccl: the fallback's all-gathers / grouped send-recv (slam_dist_set_collective)
+        line["config"]["exchange"] = exchange_mode[0]
     if rank == 0:
         print(json.dumps(line), flush=True)
     if dist is not None:

@@ -211,6 +211,17 @@ int slam_dist_export(slam_dist* d, void* blob);                 /* n_held x hand
  * reachable (hipDeviceCanAccessPeer), else SLAM_ERR_COMM before any IPC mapping. */
 int slam_dist_connect(slam_dist* d, const void* all_blobs);
 int slam_dist_connect_comm(slam_dist* d, slam_comm* comm);      /* export + RCCL all-gather + connect */
+/* Collective exchange instead of the peer-memory stores (the fallback when a peer's
+ * region cannot be mapped; replaces connect): every step's record all-gather
+ * (particle_filter.py:234 normalisation across shards: the ranks' np.sum buffer
+ * partials gathered, then folded in rank order on every rank -- bit-identical to
+ * one GPU) and, on resample steps, the specials' and items' exchanges as RCCL
+ * all-gathers and grouped send/recv between the step's kernels.  comm: an RCCL
+ * communicator of the filter's world (one held shard, rank = comm rank); NULL with
+ * every shard held (LOCAL), the collectives then being device copies.  Steps are
+ * host-orchestrated (no hipGraphs; the host reads the resample flag each step and
+ * the exchanged counts on resample steps). */
+int slam_dist_set_collective(slam_dist* d, slam_comm* comm);
 /* one step from host inputs (observations staged in slot 0, device RNG) */
 int slam_dist_step(slam_dist* d, const double* control, const double* z, slam_pf_result* res);
 /* Every wait on a peer is bounded (~2^24 polls); one that expires returns

@@ -38,3 +38,8 @@ int comm_exchange(const Comm& c, const std::vector<const void*>& send_ptr,
                   const std::vector<size_t>& recv_bytes, hipStream_t stream);
 
 }  // namespace slam
+
+// the C-ABI's communicator handle (slam_hip.h: slam_comm)
+struct slam_comm {
+    slam::Comm c;
+};

@@ -121,10 +121,6 @@ int comm_exchange(const Comm& c, const std::vector<const void*>& send_ptr,
 
 using namespace slam;
 
-struct slam_comm {
-    Comm c;
-};
-
 extern "C" {
 
 int slam_comm_unique_id(uint8_t* id_out) {

@@ -11,6 +11,7 @@
 #include <limits>
 #include <vector>
 
+#include "comm.hpp"
 #include "mt_stream.hpp"
 #include "pf_kernels.inl"
 #include "pf_dist.inl"
@@ -32,7 +33,9 @@ static void build_tail(int lo, int n, std::vector<int32_t>& leaves, std::vector<
     ops.push_back(-1);
 }
 
-constexpr int kGraphSteps = 8;     // steps per multi-step graph (even)
+constexpr int kGraphLevels = 4;    // captured step graphs of 1, 2, 4 and 8 steps
+constexpr int kGraphSteps = 1 << (kGraphLevels - 1);
+constexpr int32_t kSetupCopyMax = 4096;   // batch controls the setup kernel copies itself
 
 struct Timer {
     std::vector<std::pair<hipEvent_t, hipEvent_t>> ev[4];
@@ -92,8 +95,10 @@ struct slam_pf {
     double* zc = nullptr;                 // [cap][kZcWords] closed-form words (device-formed per step)
     double* ofs = nullptr;
     slam_pf_result* res_dev = nullptr;
-    slam_pf_result* res_host = nullptr;   // pinned
-    double* ctl_pin = nullptr;            // pinned staging of a batch's controls
+    slam_pf_result* res_host = nullptr;   // pinned, coherent: the export kernel stores into it
+    double* ctl_pin = nullptr;            // pinned, coherent staging of a batch's controls
+    slam_pf_result* res_host_dev = nullptr;   // the two pinned buffers' device addresses
+    double* ctl_pin_dev = nullptr;
     int32_t* ctr = nullptr;               // [0] step in batch, [1] RNG step
     int32_t z_steps = 0;
     LikConst lc;
@@ -102,8 +107,7 @@ struct slam_pf {
     int32_t resample_next = 0;            // host mirror of the device flag
     bool timing = false;
     bool use_graph = true;
-    hipGraphExec_t graph[2] = {nullptr, nullptr};
-    hipGraphExec_t graph_multi[2] = {nullptr, nullptr};
+    hipGraphExec_t graph[kGraphLevels][2] = {};   // [log2 steps][ping-pong parity]
     Timer tm;
     double ofs_host = 0.0;          // pinned-free staging of one step's resample offset
     // deferred normalisation (single-GPU handles): current weights = w_un / s_cur
@@ -121,6 +125,12 @@ struct slam_pf {
     int32_t truth_steps = 0;
     const double* noise_src = nullptr;   // fused kernel's host-noise input (default h->noise)
     double ess_band = 1e-9;              // result.ess_near band (relative to ESS_TH)
+    // the closed-form words of step prep_step were formed by the previous
+    // batch's last step end for the control prep_ctl (the setup kernel wrote
+    // it as the guess for the next batch's first step); -1: none.  Any call
+    // that can change the observations, landmarks or controls clears it.
+    int32_t prep_step = -1;
+    double prep_ctl[2] = {0.0, 0.0};
 };
 
 namespace {
@@ -204,6 +214,7 @@ StepIO step_io(slam_pf* h) {
     io.zc = h->zc;
     io.ofs = h->ofs;
     io.res = h->res_dev;
+    io.res_host = h->res_host_dev;
     io.ctr = h->ctr;
     io.cap = h->cap;
     io.motion = h->cfg.motion;
@@ -233,11 +244,11 @@ void toc(slam_pf* h, int k) {
 inline unsigned grid_for(int64_t n, int bs) { return (unsigned)((n + bs - 1) / bs); }
 
 void drop_graphs(slam_pf* h) {
-    for (auto* gs : {h->graph, h->graph_multi})
-        for (int k = 0; k < 2; ++k)
-            if (gs[k]) {
-                (void)hipGraphExecDestroy(gs[k]);
-                gs[k] = nullptr;
+    for (auto& gs : h->graph)
+        for (auto& g : gs)
+            if (g) {
+                (void)hipGraphExecDestroy(g);
+                g = nullptr;
             }
 }
 
@@ -245,8 +256,9 @@ int launch_step(slam_pf* h, bool host_noise);
 
 // One captured hipGraph of `steps` device-resident steps (slam_pf_run) for the
 // handle's current ping-pong parity; the step context lives in device memory,
-// so a replay needs no host input.  There is one graph per parity for
-// kGraphSteps steps (even: the parity comes back) and one for a single step.
+// so a replay needs no host input.  There is one graph per parity for each of
+// 1, 2, 4 and 8 steps: a batch replays its binary decomposition, largest first
+// (the even ones bring the parity back).
 int capture_steps(slam_pf* h, hipGraphExec_t& ge, int steps) {
     const int cur0 = h->cur;
     hipGraph_t g;
@@ -290,8 +302,14 @@ int ensure_steps(slam_pf* h, int32_t steps) {
         (rc = dalloc(h, &h->ofs, (size_t)steps)) || (rc = dalloc(h, &h->truth, 4 * (size_t)steps)) ||
         (rc = dalloc(h, &h->res_dev, (size_t)steps)))
         return rc;
-    SLAM_HIP_TRY(hipHostMalloc((void**)&h->res_host, sizeof(slam_pf_result) * steps));
-    SLAM_HIP_TRY(hipHostMalloc((void**)&h->ctl_pin, 2 * sizeof(double) * steps));
+    // fine-grained host memory: the setup kernel reads the controls and the
+    // export kernel stores the results over the host link, uncached
+    SLAM_HIP_TRY(hipHostMalloc((void**)&h->res_host, sizeof(slam_pf_result) * steps,
+                               hipHostMallocMapped | hipHostMallocCoherent));
+    SLAM_HIP_TRY(hipHostMalloc((void**)&h->ctl_pin, 2 * sizeof(double) * steps,
+                               hipHostMallocMapped | hipHostMallocCoherent));
+    SLAM_HIP_TRY(hipHostGetDevicePointer((void**)&h->res_host_dev, h->res_host, 0));
+    SLAM_HIP_TRY(hipHostGetDevicePointer((void**)&h->ctl_pin_dev, h->ctl_pin, 0));
     h->cap = steps;
     h->z_steps = 0;
     h->truth_steps = 0;
@@ -308,15 +326,6 @@ int set_ctr(slam_pf* h, int32_t step) {
 
 int set_flag(slam_pf* h, int word, int32_t v) {
     SLAM_HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)(h->flags + word), v, 1, h->stream));
-    return SLAM_OK;
-}
-
-// controls of a device-resident batch through pinned staging (an asynchronous
-// copy; every run ends with a stream synchronize, so the staging is free again)
-int upload_controls(slam_pf* h, int32_t first_step, int32_t n_steps, const double* controls) {
-    std::memcpy(h->ctl_pin, controls, 2 * (size_t)n_steps * sizeof(double));
-    SLAM_HIP_TRY(hipMemcpyAsync(h->ctl + 2 * first_step, h->ctl_pin, 2 * (size_t)n_steps * sizeof(double),
-                                hipMemcpyHostToDevice, h->stream));
     return SLAM_OK;
 }
 
@@ -512,6 +521,73 @@ int launch_prestep(slam_pf* h) {
     return SLAM_OK;
 }
 
+// A device-resident batch's setup in one launch (slam_pf_run): the batch's
+// controls read from the coherent pinned staging over the host link (ncopy of
+// them; 0 when a copy already moved them), the step counters and the resample
+// flag (rflag < 0: left as it is), then -- unless the device observes (NumPy stream) -- the first step's
+// closed-form words as pf_prestep_kernel forms them.  One stream operation in
+// place of a host-to-device copy, three memsets and the prestep.
+__global__ __launch_bounds__(512) void pf_run_setup_kernel(
+    const double* __restrict__ ctl_host, const int32_t nsteps, const int32_t ncopy, const int32_t first,
+    const int32_t stepno, const int32_t rflag, double* __restrict__ ctl, int32_t* __restrict__ ctr,
+    int32_t* __restrict__ flags, double* __restrict__ ctl_next, const int32_t prep,
+    const double* __restrict__ lm,
+    const double* __restrict__ z_all, const int32_t nl, const double* __restrict__ refp,
+    const double dt, const int32_t motion, double* __restrict__ zc) {
+    for (int k = (int)threadIdx.x; k < 2 * ncopy; k += (int)blockDim.x)
+        ctl[2 * (size_t)first + k] = ctl_host[k];
+    // the guess for the next batch's first control (this batch's last): the
+    // last step end forms that step's closed-form words with it, and the next
+    // setup skips its own forming when the guess was right
+    if (ctl_next && threadIdx.x < 2) ctl_next[threadIdx.x] = ctl_host[2 * (nsteps - 1) + threadIdx.x];
+    if (threadIdx.x == 0) {
+        ctr[0] = first;
+        ctr[1] = stepno;
+        ctr[2] = first;
+        ctr[3] = first + nsteps - 1;
+        if (rflag >= 0) flags[kFlagResample] = rflag;
+    }
+    if (prep)
+        closed_prep_block(lm, z_all + (size_t)first * 2 * nl, nl, refp, ctl_host[0], ctl_host[1], dt,
+                          motion, zc + (size_t)first * kZcWords);
+}
+
+int launch_run_setup(slam_pf* h, int32_t first_step, int32_t n_steps, const double* controls,
+                     int32_t rflag, int32_t* prep_next = nullptr) {
+    std::memcpy(h->ctl_pin, controls, 2 * (size_t)n_steps * sizeof(double));
+    // the first step's words: already formed by the previous batch's last
+    // step end when it continued this one with the same control
+    const bool formed = h->prep_step == first_step && h->prep_ctl[0] == controls[0] &&
+                        h->prep_ctl[1] == controls[1];
+    const int32_t next = first_step + n_steps;
+    const bool guess = prep_next && h->deferred && !h->mt && h->lc.closed && next < h->cap;
+    h->prep_step = -1;                      // (re)armed by the caller once the batch succeeded
+    if (prep_next) *prep_next = guess ? next : -1;
+    int32_t ncopy = n_steps;
+    if (n_steps > kSetupCopyMax) {                 // long batches: one DMA copy instead
+        SLAM_HIP_TRY(hipMemcpyAsync(h->ctl + 2 * first_step, h->ctl_pin,
+                                    2 * (size_t)n_steps * sizeof(double), hipMemcpyHostToDevice,
+                                    h->stream));
+        ncopy = 0;
+    }
+    pf_run_setup_kernel<<<1, 512, 0, h->stream>>>(
+        h->ctl_pin_dev, n_steps, ncopy, first_step, (int32_t)h->stepno, rflag, h->ctl, h->ctr,
+        h->flags, guess ? h->ctl + 2 * (size_t)next : nullptr,
+        (!h->mt && h->lc.closed && !formed) ? 1 : 0, h->lm, h->z_all, h->nl, h->refp, h->pc.dt,
+        h->cfg.motion, h->zc);
+    SLAM_HIP_TRY(hipGetLastError());
+    return SLAM_OK;
+}
+
+// The batch's result records into the coherent pinned buffer (stores over the
+// host link; visible to the host once the stream has synchronised)
+__global__ __launch_bounds__(256) void pf_export_kernel(const uint64_t* __restrict__ src,
+                                                        const int64_t words,
+                                                        uint64_t* __restrict__ dst) {
+    for (int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x; k < words; k += 256 * (int64_t)gridDim.x)
+        dst[k] = src[k];
+}
+
 // mvn(0, Q, NP) (particle_filter.py:165): noise = normals @ M, OpenBLAS's order
 __global__ __launch_bounds__(256) void pf_mt_noise_kernel(const int64_t n,
                                                           const double* __restrict__ g,
@@ -571,22 +647,32 @@ int launch_step(slam_pf* h, bool host_noise) {
     return launch_reduce(h, -1);
 }
 
-int sync_results(slam_pf* h, int32_t first, int32_t count, slam_pf_result* out) {
-    SLAM_HIP_TRY(hipMemcpyAsync(h->res_host, h->res_dev + first, sizeof(slam_pf_result) * count,
-                                hipMemcpyDeviceToHost, h->stream));
+// The records of steps [first, first + count) from the coherent host buffer:
+// stored there by the batch's last step end (exported: slam_pf_run on a
+// deferred handle) or by one export launch here.
+int sync_results(slam_pf* h, int32_t first, int32_t count, slam_pf_result* out, bool exported = false) {
+    static_assert(sizeof(slam_pf_result) % 8 == 0, "result records move as 8-byte words");
+    if (!exported) {
+        const int64_t words = (int64_t)count * (int64_t)(sizeof(slam_pf_result) / 8);
+        pf_export_kernel<<<std::min<unsigned>(grid_for(words, 256), 64u), 256, 0, h->stream>>>(
+            reinterpret_cast<const uint64_t*>(h->res_dev + first), words,
+            reinterpret_cast<uint64_t*>(h->res_host_dev + first));
+        SLAM_HIP_TRY(hipGetLastError());
+    }
     SLAM_HIP_TRY(hipStreamSynchronize(h->stream));
+    const slam_pf_result* r = h->res_host + first;
     int rc = SLAM_OK;
     for (int i = 0; i < count; ++i) {
-        if (out) out[i] = h->res_host[i];
-        if (h->res_host[i].status & 8)
+        if (out) out[i] = r[i];
+        if (r[i].status & 8)
             rc = fail(SLAM_ERR_HIP, "exact-cumsum launch: release token timed out");
-        if (h->res_host[i].status & 256)
+        if (r[i].status & 256)
             rc = fail(SLAM_ERR_HIP, "mt19937 draw: candidate bound exhausted");
-        if (h->res_host[i].status & 1)
+        if (r[i].status & 1)
             rc = fail(SLAM_ERR_INDEX, "resample position beyond the last cumulative weight "
                                       "(IndexError in particle_filter.py:219); clamped to NP-1");
     }
-    h->resample_next = h->res_host[count - 1].resample_next;
+    h->resample_next = r[count - 1].resample_next;
     return rc;
 }
 
@@ -793,6 +879,13 @@ extern "C" int slam_probe_slow_count(unsigned long long* out) {
 }
 #endif
 
+#ifdef SLAM_PROBE_FUSED
+extern "C" int slam_fprobe_read(unsigned long long* out, int count) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_fprobe), sizeof(unsigned long long) * count) == hipSuccess
+               ? 0 : -1;
+}
+#endif
+
 #ifdef SLAM_PROBE
 extern "C" int slam_probe_read(unsigned long long* out, int count) {
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_probe), sizeof(unsigned long long) * count) != hipSuccess) return -1;
@@ -829,6 +922,7 @@ int slam_pf_destroy(slam_pf* h) {
 
 int slam_pf_set_stream(slam_pf* h, void* stream, int32_t external) {
     SLAM_ARG_CHECK(h, "slam_pf_set_stream: NULL handle");
+    h->prep_step = -1;
     SLAM_HIP_TRY(hipSetDevice(h->device));
     SLAM_HIP_TRY(hipStreamSynchronize(h->stream));
     drop_graphs(h);
@@ -845,6 +939,7 @@ int slam_pf_set_stream(slam_pf* h, void* stream, int32_t external) {
 
 int slam_pf_set_landmarks(slam_pf* h, const double* landmarks) {
     SLAM_ARG_CHECK(h && (landmarks || h->nl == 0), "slam_pf_set_landmarks: NULL argument");
+    h->prep_step = -1;
     SLAM_HIP_TRY(hipSetDevice(h->device));
     if (h->nl) {
         SLAM_HIP_TRY(hipMemcpyAsync(h->lm, landmarks, 2 * h->nl * sizeof(double),
@@ -857,6 +952,7 @@ int slam_pf_set_landmarks(slam_pf* h, const double* landmarks) {
 int slam_pf_set_state(slam_pf* h, const double* x, const double* y, const double* th,
                       const double* w) {
     SLAM_ARG_CHECK(h, "slam_pf_set_state: NULL handle");
+    h->prep_step = -1;
     SLAM_HIP_TRY(hipSetDevice(h->device));
     const size_t b = h->n * sizeof(double);
     const int c = h->cur;
@@ -906,6 +1002,7 @@ int slam_pf_get_state(slam_pf* h, double* x, double* y, double* th, double* w) {
 int slam_pf_step(slam_pf* h, const double* control, const double* z, const double* noise,
                  double u_resample, slam_pf_result* res) {
     SLAM_ARG_CHECK(h && control && (z || h->nl == 0), "slam_pf_step: NULL argument");
+    h->prep_step = -1;
     SLAM_ARG_CHECK(h->n == h->n_global, "slam_pf_step: sharded handle (use the shard entry points)");
     SLAM_HIP_TRY(hipSetDevice(h->device));
     int rc;
@@ -926,6 +1023,7 @@ int slam_pf_step(slam_pf* h, const double* control, const double* z, const doubl
 
 int slam_pf_resample(slam_pf* h, double u_resample, int32_t force, int32_t* resampled) {
     SLAM_ARG_CHECK(h, "slam_pf_resample: NULL handle");
+    h->prep_step = -1;
     SLAM_ARG_CHECK(h->n == h->n_global, "slam_pf_resample: sharded handle");
     SLAM_HIP_TRY(hipSetDevice(h->device));
     const int32_t go = force ? 1 : h->resample_next;
@@ -957,6 +1055,7 @@ int slam_pf_resample(slam_pf* h, double u_resample, int32_t force, int32_t* resa
 
 int slam_pf_resample_indices(slam_pf* h, double u_resample, int64_t* idx_out, int32_t* n_special) {
     SLAM_ARG_CHECK(h && idx_out, "slam_pf_resample_indices: NULL argument");
+    h->prep_step = -1;
     SLAM_ARG_CHECK(h->n == h->n_global, "slam_pf_resample_indices: sharded handle");
     SLAM_HIP_TRY(hipSetDevice(h->device));
     int rc = launch_scans(h, 1, true);
@@ -982,6 +1081,7 @@ int slam_pf_resample_indices(slam_pf* h, double u_resample, int64_t* idx_out, in
 
 int slam_pf_predict(slam_pf* h, const double* control, const double* noise) {
     SLAM_ARG_CHECK(h && control, "slam_pf_predict: NULL argument");
+    h->prep_step = -1;
     SLAM_HIP_TRY(hipSetDevice(h->device));
     // predict only: fused kernel with zero landmarks and no resample gather;
     // the weights pass through unchanged (w_un = w * 1).
@@ -1010,6 +1110,7 @@ int slam_pf_predict(slam_pf* h, const double* control, const double* noise) {
 int slam_pf_update(slam_pf* h, const double* z, slam_pf_result* res) {
     // __likelihood + estimate on the current particles (no motion, no resample)
     SLAM_ARG_CHECK(h && (z || h->nl == 0), "slam_pf_update: NULL argument");
+    h->prep_step = -1;
     SLAM_ARG_CHECK(h->n == h->n_global, "slam_pf_update: sharded handle");
     SLAM_HIP_TRY(hipSetDevice(h->device));
     int rc;
@@ -1056,6 +1157,7 @@ int slam_pf_weight_sum(slam_pf* h, double* sum_out) {
 
 int slam_pf_load_observations(slam_pf* h, int32_t n_steps, const double* z_all) {
     SLAM_ARG_CHECK(h && n_steps > 0 && (z_all || h->nl == 0), "slam_pf_load_observations: bad argument");
+    h->prep_step = -1;
     SLAM_HIP_TRY(hipSetDevice(h->device));
     int rc = ensure_steps(h, n_steps);
     if (rc) return rc;
@@ -1080,19 +1182,20 @@ int slam_pf_run(slam_pf* h, int32_t first_step, int32_t n_steps, const double* c
                          : "slam_pf_run: steps outside the loaded observations");
     SLAM_HIP_TRY(hipSetDevice(h->device));
     int rc;
-    if ((rc = upload_controls(h, first_step, n_steps, controls))) return rc;
-    if ((rc = set_ctr(h, first_step)) || (rc = set_flag(h, kFlagResample, h->resample_next))) return rc;
-    if (!h->mt && (rc = launch_prestep(h))) return rc;         // the first step's closed-form words
+    int32_t prep_next = -1;
+    if ((rc = launch_run_setup(h, first_step, n_steps, controls, h->resample_next, &prep_next)))
+        return rc;
     if (h->resample_next && (rc = launch_bsum(h))) return rc;   // prefix for the first step's scan
     const bool graphs = h->use_graph && !h->timing;
     int32_t k = 0;
     while (k < n_steps) {
         if (graphs) {
-            const bool multi = n_steps - k >= kGraphSteps;
-            hipGraphExec_t& ge = multi ? h->graph_multi[h->cur] : h->graph[h->cur];
-            if (!ge && (rc = capture_steps(h, ge, multi ? kGraphSteps : 1))) return rc;
+            int lv = kGraphLevels - 1;
+            while ((1 << lv) > n_steps - k) --lv;
+            hipGraphExec_t& ge = h->graph[lv][h->cur];
+            if (!ge && (rc = capture_steps(h, ge, 1 << lv))) return rc;
             SLAM_HIP_TRY(hipGraphLaunch(ge, h->stream));
-            const int done = multi ? kGraphSteps : 1;
+            const int done = 1 << lv;
             if (done & 1) h->cur = 1 - h->cur;
             k += done;
             h->stepno += done;
@@ -1104,7 +1207,13 @@ int slam_pf_run(slam_pf* h, int32_t first_step, int32_t n_steps, const double* c
             h->stepno++;
         }
     }
-    return sync_results(h, first_step, n_steps, results);
+    rc = sync_results(h, first_step, n_steps, results, h->deferred);
+    if (rc == SLAM_OK && prep_next >= 0) {
+        h->prep_step = prep_next;
+        h->prep_ctl[0] = controls[2 * (n_steps - 1)];
+        h->prep_ctl[1] = controls[2 * (n_steps - 1) + 1];
+    }
+    return rc;
 }
 
 int slam_pf_prepare_graphs(slam_pf* h, double* capture_ms) {
@@ -1117,8 +1226,8 @@ int slam_pf_prepare_graphs(slam_pf* h, double* capture_ms) {
         const int cur0 = h->cur;
         for (int par = 0; par < 2 && rc == SLAM_OK; ++par) {
             h->cur = par;
-            if (!h->graph_multi[par]) rc = capture_steps(h, h->graph_multi[par], kGraphSteps);
-            if (!rc && !h->graph[par]) rc = capture_steps(h, h->graph[par], 1);
+            for (int lv = 0; lv < kGraphLevels && rc == SLAM_OK; ++lv)
+                if (!h->graph[lv][par]) rc = capture_steps(h, h->graph[lv][par], 1 << lv);
         }
         h->cur = cur0;
     }
@@ -1130,6 +1239,7 @@ int slam_pf_prepare_graphs(slam_pf* h, double* capture_ms) {
 int slam_pf_set_rng_mt19937(slam_pf* h, const uint32_t* key, int32_t pos, int32_t has_gauss,
                             double gauss, const double* r_factor) {
     SLAM_ARG_CHECK(h && key && r_factor, "slam_pf_set_rng_mt19937: NULL argument");
+    h->prep_step = -1;
     SLAM_ARG_CHECK(h->n == h->n_global, "slam_pf_set_rng_mt19937: sharded handle");
     SLAM_ARG_CHECK(h->nl <= 2048, "slam_pf_set_rng_mt19937: at most 2048 landmarks");
     SLAM_HIP_TRY(hipSetDevice(h->device));
@@ -1155,6 +1265,7 @@ int slam_pf_get_rng_mt19937(slam_pf* h, uint32_t* key, int32_t* pos, int32_t* ha
 int slam_pf_step_truth(slam_pf* h, const double* control, const double* truth, double* z_out,
                        slam_pf_result* res) {
     SLAM_ARG_CHECK(h && control && truth, "slam_pf_step_truth: NULL argument");
+    h->prep_step = -1;
     SLAM_ARG_CHECK(h->mt, "slam_pf_step_truth: enable the device stream first (slam_pf_set_rng_mt19937)");
     SLAM_HIP_TRY(hipSetDevice(h->device));
     int rc;
@@ -1183,6 +1294,7 @@ int slam_pf_step_truth(slam_pf* h, const double* control, const double* truth, d
 
 int slam_pf_load_truth(slam_pf* h, int32_t n_steps, const double* truth) {
     SLAM_ARG_CHECK(h && n_steps > 0 && truth, "slam_pf_load_truth: bad argument");
+    h->prep_step = -1;
     SLAM_HIP_TRY(hipSetDevice(h->device));
     int rc = ensure_steps(h, n_steps);
     if (rc) return rc;

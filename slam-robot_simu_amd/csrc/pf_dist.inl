@@ -78,7 +78,14 @@ struct alignas(16) DistItem {
 
 struct DistPeers {
     char* base[kDistMaxWorld];  // every rank's exchange region as mapped in this process
+                                // (collective mode: only this rank's own)
     DistItem* self_items;       // items this rank sends itself (regular memory, cap_item)
+    // collective mode (slam_dist_set_collective): every push stays in this
+    // rank's own region / send area and the host moves it with RCCL
+    // collectives (or device copies between held shards) between the launches
+    DistItem* item_out;         // [world][cap_item] items per destination rank
+    int64_t* cnt_out;           // [world] item counts per destination rank
+    int32_t coll;
     int64_t gb[kDistMaxWorld + 1];
     DistLayout L;
     int32_t world, rank;
@@ -103,6 +110,11 @@ __device__ __forceinline__ uint64_t* dist_flags(const DistPeers& P, const int q)
     return reinterpret_cast<uint64_t*>(P.base[q] + P.L.flags);
 }
 
+// the ranks a push reaches: every peer's region, or (collective mode) only
+// this rank's own slot, which the collective then carries to the peers
+__device__ __forceinline__ int dist_push_lo(const DistPeers& P) { return P.coll ? P.rank : 0; }
+__device__ __forceinline__ int dist_push_hi(const DistPeers& P) { return P.coll ? P.rank + 1 : P.world; }
+
 // publish `epoch` in flag word [kind][my rank] of every peer (after the data).
 // One system-scope release per block: on gfx950 it writes back the L2, so
 // every lane's stores complete first (barrier), then lane 0 fences once and
@@ -114,7 +126,7 @@ __device__ __forceinline__ void dist_signal(const DistPeers& P, const int kind, 
     __syncthreads();
     if (threadIdx.x == 0) {
         __threadfence_system();
-        for (int q = 0; q < P.world; ++q)
+        for (int q = dist_push_lo(P); q < dist_push_hi(P); ++q)
             __hip_atomic_store(dist_flags(P, q) + kind * kDistMaxWorld + P.rank, epoch,
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
@@ -201,6 +213,15 @@ __device__ __forceinline__ void dist_store_item(const DistPeers& P, const int d,
         st_wt(p + 4, (uint64_t)hi);
         return;
     }
+    if (P.coll) {                       // the send area for rank d (a collective moves it)
+        DistItem* it = P.item_out + (int64_t)d * P.L.cap_item + slot;
+        it->x = x;
+        it->y = y;
+        it->th = th;
+        it->lo = lo;
+        it->hi = hi;
+        return;
+    }
     uint64_t* p = reinterpret_cast<uint64_t*>(reinterpret_cast<DistItem*>(P.base[d] + P.L.item) +
                                               (int64_t)P.rank * P.L.cap_item + slot);
     const uint64_t v[5] = {(uint64_t)__double_as_longlong(x), (uint64_t)__double_as_longlong(y),
@@ -251,7 +272,7 @@ __global__ __launch_bounds__(kScanThreads) void dist_emit_push_kernel(
     if (!arrive_last(counter)) return;
     const int32_t ns = *nspec_p;
     const uint64_t kt = *ktot_p;
-    for (int q = 0; q < P.world; ++q) {
+    for (int q = dist_push_lo(P); q < dist_push_hi(P); ++q) {
         char* rb = P.base[q];
         SpecialIn* dst = reinterpret_cast<SpecialIn*>(rb + P.L.spec) + (int64_t)P.rank * P.L.cap_spec;
         for (int32_t m = threadIdx.x; m < ns; m += blockDim.x) dst[m] = ld_wt_struct(&spec[m]);
@@ -454,11 +475,23 @@ __global__ __launch_bounds__(kScanThreads) void dist_pack_push_kernel(
     }
     if (!arrive_last(counter)) return;                      // (drains this block's item stores)
     if ((int)threadIdx.x < P.world) {
-        int64_t* hdr = reinterpret_cast<int64_t*>(P.base[threadIdx.x] + P.L.item_hdr) + 2 * P.rank;
-        hdr[0] = scr->dcnt[threadIdx.x];
+        if (!P.coll || (int)threadIdx.x == P.rank) {
+            int64_t* hdr = reinterpret_cast<int64_t*>(P.base[threadIdx.x] + P.L.item_hdr) + 2 * P.rank;
+            hdr[0] = scr->dcnt[threadIdx.x];
+        }
+        if (P.coll) P.cnt_out[threadIdx.x] = scr->dcnt[threadIdx.x];
     }
     __syncthreads();
     dist_signal(P, kXItem, dist_epoch(io));
+}
+
+// collective mode: the peers' data of `kind` has arrived (the collective ran
+// before this launch on the stream): publish it in this rank's flag words, so
+// that the waits of the following kernels pass
+__global__ void dist_publish_kernel(const DistPeers P, const int kind, const StepIO io) {
+    if ((int)threadIdx.x < P.world)
+        __hip_atomic_store(dist_flags(P, P.rank) + kind * kDistMaxWorld + threadIdx.x, dist_epoch(io),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // wait for every rank's items and hand them to the fused kernel's resample
@@ -1228,7 +1261,7 @@ __device__ __forceinline__ void dist_record(const int64_t n, const DeferParts& d
     // ---- push into every peer's slot (parity = epoch & 1)
     PROBE_AT(28);
     const int64_t words = (int64_t)sizeof(DistRec) / 8;
-    for (int qq = 0; qq < P.world; ++qq) {
+    for (int qq = dist_push_lo(P); qq < dist_push_hi(P); ++qq) {
         char* slot = P.base[qq] + P.L.g1 + ((int64_t)(epoch & 1) * P.world + P.rank) * P.L.rec_stride;
         uint64_t* dst = reinterpret_cast<uint64_t*>(slot);
         const uint64_t* src = reinterpret_cast<const uint64_t*>(&rec);

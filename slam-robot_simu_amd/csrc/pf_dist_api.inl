@@ -32,6 +32,13 @@ struct slam_dist {
     bool merged_ok = false;
     hipGraphExec_t graph[2] = {nullptr, nullptr};     // kGraphSteps steps per parity
     hipGraphExec_t graph1[2] = {nullptr, nullptr};    // one step per parity
+    // collective mode (slam_dist_set_collective): host-orchestrated steps, the
+    // exchanges as RCCL collectives (one held shard) or device copies between
+    // the held shards' regions (LOCAL)
+    bool coll = false;
+    slam_comm* comm = nullptr;
+    int64_t* cnt_mat = nullptr;               // [world][world] gathered item counts (device)
+    int64_t* hst = nullptr;                   // pinned host: counts / headers
 };
 
 namespace {
@@ -127,11 +134,190 @@ int dist_enqueue_step(slam_dist* d) {
     return SLAM_OK;
 }
 
+// ---- collective mode
+hipStream_t dist_stream(slam_dist* d) { return d->local ? d->stream : d->sh[0]->stream; }
+
+// rank r's slot [off + r bytes, + bytes) of every region into every region
+int coll_all_gather(slam_dist* d, int64_t off, int64_t bytes) {
+    hipStream_t s = dist_stream(d);
+    if (d->comm) {
+        char* reg = d->xbuf[0] + off;
+        return comm_all_gather(d->comm->c, reg + (int64_t)d->rank0 * bytes, reg, (size_t)bytes, s);
+    }
+    for (int i = 0; i < d->nloc; ++i)
+        for (int j = 0; j < d->nloc; ++j) {
+            if (i == j) continue;
+            const int64_t o = off + (int64_t)(d->rank0 + i) * bytes;
+            SLAM_HIP_TRY(hipMemcpyAsync(d->xbuf[j] + o, d->xbuf[i] + o, (size_t)bytes,
+                                        hipMemcpyDeviceToDevice, s));
+        }
+    return SLAM_OK;
+}
+
+// point-to-point: for every ordered pair (r -> q), q != r, bytes(r, q) from
+// src(r, q) (in r's memory) to dst(q, r) (in q's memory)
+template <typename Src, typename Dst, typename Bytes>
+int coll_exchange(slam_dist* d, Src src, Dst dst, Bytes bytes) {
+    hipStream_t s = dist_stream(d);
+    if (d->comm) {
+        const int r = d->rank0, w = d->world;
+        std::vector<const void*> sp(w, nullptr);
+        std::vector<void*> rp(w, nullptr);
+        std::vector<size_t> sb(w, 0), rb(w, 0);
+        for (int q = 0; q < w; ++q) {
+            if (q == r) continue;
+            sp[q] = src(0, q);
+            sb[q] = (size_t)bytes(r, q);
+            rp[q] = dst(0, q);
+            rb[q] = (size_t)bytes(q, r);
+        }
+        return comm_exchange(d->comm->c, sp, sb, rp, rb, s);
+    }
+    for (int i = 0; i < d->nloc; ++i)
+        for (int j = 0; j < d->nloc; ++j) {
+            const int ri = d->rank0 + i, rj = d->rank0 + j;
+            if (i == j || bytes(ri, rj) == 0) continue;
+            SLAM_HIP_TRY(hipMemcpyAsync(dst(j, ri), src(i, rj), (size_t)bytes(ri, rj),
+                                        hipMemcpyDeviceToDevice, s));
+        }
+    return SLAM_OK;
+}
+
+void coll_publish(slam_dist* d, int kind) {
+    for (int i = 0; i < d->nloc; ++i) {
+        slam_pf* h = d->sh[i];
+        dist_publish_kernel<<<1, 64, 0, h->stream>>>(d->peers[i], kind, step_io(h));
+    }
+}
+
+// One step with the exchanges as collectives between the launches (the
+// kernels are the device-resident step's; their pushes stay in the own region
+// or send area, and a publish launch stands for the peers' signals).  The
+// host decides the resample branch from its mirror of the device flag and
+// reads the specials' and items' counts it must move (two synchronisations
+// on a resample step).
+int dist_coll_step(slam_dist* d) {
+    const int m = d->nloc, w = d->world;
+    hipStream_t s = dist_stream(d);
+    const DistLayout& L = d->L;
+    const int64_t sz_spec = (int64_t)sizeof(SpecialIn), sz_item = (int64_t)sizeof(DistItem);
+    int rc;
+    if (d->sh[0]->resample_next) {
+        for (int i = 0; i < m; ++i) {                     // exact cumsum: classify, emit (own slot)
+            slam_pf* h = d->sh[i];
+            const double delta = 4.0 * (double)h->n_global * 0x1p-53 + 0x1p-45;
+            scan_classify_kernel<<<h->nb_scan, kScanThreads, 0, h->stream>>>(
+                h->w_un, h->n, h->boff, &d->scr[i]->base_off, h->c, h->kincl, h->fexcl, h->bk, h->bf,
+                h->boffk, h->bofff, h->ktot, h->nspec, delta, h->gbase, h->tk + 2 * kTicketWords,
+                h->flags, 0, h->s_cur, h->pc.np_recip, kPartPer);
+        }
+        for (int i = 0; i < m; ++i) {
+            slam_pf* h = d->sh[i];
+            dist_emit_push_kernel<<<h->nb_scan, kScanThreads, 0, h->stream>>>(
+                h->w_un, h->s_cur, h->pc.np_recip, h->n, h->c, h->kincl, h->fexcl, h->boffk, h->bofff,
+                h->spec_in, h->gbase, h->nspec, h->ktot, d->tk[i], h->flags, d->peers[i], step_io(h));
+        }
+        // the specials: every rank's (count, increment total), then the lists
+        if ((rc = coll_all_gather(d, L.spec_hdr, 16))) return rc;
+        SLAM_HIP_TRY(hipMemcpyAsync(d->hst, d->xbuf[0] + L.spec_hdr, 16 * (size_t)w,
+                                    hipMemcpyDeviceToHost, s));
+        SLAM_HIP_TRY(hipStreamSynchronize(s));
+        std::vector<int64_t> ns(w);
+        for (int q = 0; q < w; ++q) ns[q] = std::min<int64_t>(std::max<int64_t>(d->hst[2 * q], 0), L.cap_spec);
+        auto spec_slot = [&](int i, int q) { return d->xbuf[i] + L.spec + (int64_t)q * L.cap_spec * sz_spec; };
+        if ((rc = coll_exchange(
+                 d, [&](int i, int) { return (const void*)spec_slot(i, d->rank0 + i); },
+                 [&](int j, int from) { return (void*)spec_slot(j, from); },
+                 [&](int from, int) { return ns[from] * sz_spec; })))
+            return rc;
+        coll_publish(d, kXSpec);
+        for (int i = 0; i < m; ++i) {                     // fold, expand + hi + counts, pack
+            slam_pf* h = d->sh[i];
+            dist_fold_kernel<<<1, 256, 0, h->stream>>>(d->spec_g[i], d->spec_go[i], h->n_global,
+                                                       h->flags, d->scr[i], d->peers[i], step_io(h),
+                                                       h->pc.rstep, h->pc.np_recip, h->cfg.seed);
+        }
+        for (int i = 0; i < m; ++i) {
+            slam_pf* h = d->sh[i];
+            dist_expand_hi_kernel<<<h->nb_scan, kScanThreads, 0, h->stream>>>(
+                h->n, h->kincl, h->fexcl, h->boffk, h->bofff, d->spec_go[i], h->c, d->hi[i], d->bsel[i],
+                d->bsel_off[i], d->tk[i] + kTicketWords, h->flags, d->scr[i], d->peers[i], step_io(h),
+                h->n_global, h->pc.rstep, h->pc.np_recip, h->cfg.seed);
+        }
+        for (int i = 0; i < m; ++i) {
+            slam_pf* h = d->sh[i];
+            const int c = h->cur;
+            SLAM_HIP_TRY(hipMemsetAsync(d->peers[i].cnt_out, 0, 8 * (size_t)w, h->stream));
+            dist_pack_push_kernel<<<h->nb_scan, kScanThreads, 0, h->stream>>>(
+                h->n, h->x[c], h->y[c], h->th[c], d->hi[i], d->bsel_off[i], d->tk[i] + 2 * kTicketWords,
+                h->flags, d->scr[i], d->peers[i], step_io(h));
+        }
+        // the items: every rank's counts per destination, then the items
+        if (d->comm) {
+            if ((rc = comm_all_gather(d->comm->c, d->peers[0].cnt_out, d->cnt_mat, 8 * (size_t)w, s)))
+                return rc;
+        } else {
+            for (int i = 0; i < m; ++i)
+                SLAM_HIP_TRY(hipMemcpyAsync(d->cnt_mat + (int64_t)(d->rank0 + i) * w, d->peers[i].cnt_out,
+                                            8 * (size_t)w, hipMemcpyDeviceToDevice, s));
+        }
+        SLAM_HIP_TRY(hipMemcpyAsync(d->hst, d->cnt_mat, 8 * (size_t)w * w, hipMemcpyDeviceToHost, s));
+        SLAM_HIP_TRY(hipStreamSynchronize(s));
+        auto cnt = [&](int from, int to) {
+            return std::min<int64_t>(std::max<int64_t>(d->hst[(int64_t)from * w + to], 0), L.cap_item);
+        };
+        // item headers of every held region (count from each source), then the items
+        int64_t* hdr = d->hst + (int64_t)w * w;
+        for (int i = 0; i < m; ++i) {
+            int64_t* hi = hdr + 2 * (int64_t)w * i;
+            for (int q = 0; q < w; ++q) {
+                hi[2 * q] = cnt(q, d->rank0 + i);
+                hi[2 * q + 1] = 0;
+            }
+            SLAM_HIP_TRY(hipMemcpyAsync(d->xbuf[i] + L.item_hdr, hi, 16 * (size_t)w, hipMemcpyHostToDevice,
+                                        s));
+        }
+        if ((rc = coll_exchange(
+                 d, [&](int i, int to) { return (const void*)(d->peers[i].item_out + (int64_t)to * L.cap_item); },
+                 [&](int j, int from) {
+                     return (void*)(d->xbuf[j] + L.item + (int64_t)from * L.cap_item * sz_item);
+                 },
+                 [&](int from, int to) { return cnt(from, to) * sz_item; })))
+            return rc;
+        coll_publish(d, kXItem);
+        for (int i = 0; i < m; ++i) {
+            slam_pf* h = d->sh[i];
+            const int c = h->cur;
+            dist_unpack_kernel<<<std::min<unsigned>(grid_for(h->n, 256), 1024), 256, 0, h->stream>>>(
+                h->n, h->x[c], h->y[c], h->th[c], h->dp.mark, h->dp.carry, d->tk[i] + 3 * kTicketWords,
+                h->flags, d->scr[i], d->peers[i], step_io(h));
+        }
+        SLAM_HIP_TRY(hipGetLastError());
+    }
+    for (int i = 0; i < m; ++i)                           // predict + likelihood
+        if ((rc = launch_fused(d->sh[i], d->sh[i]->cfg.motion, false))) return rc;
+    auto reduce = [&](int i, auto kern) {
+        slam_pf* h = d->sh[i];
+        const int c = h->cur;
+        kern<<<1, kFinThreads, 0, h->stream>>>(
+            h->n, h->dp, h->w_un, h->tail_leaves, h->tail_ops, h->n_tail_leaves, h->n_tail_ops,
+            h->x[c], h->y[c], h->th[c], h->s_cur, h->refp, h->flags, h->cfg.ess_threshold,
+            step_io(h), h->pc.np_recip, h->boff, d->scr[i], d->peers[i]);
+    };
+    for (int i = 0; i < m; ++i) reduce(i, dist_reduce_kernel<true, false>);      // records (own slot)
+    const int par = (int)((d->sh[0]->stepno + 1) & 1);                         // dist_epoch parity
+    if ((rc = coll_all_gather(d, L.g1 + (int64_t)par * w * L.rec_stride, L.rec_stride))) return rc;
+    coll_publish(d, kXG1);
+    for (int i = 0; i < m; ++i) reduce(i, dist_reduce_kernel<false, true>);      // global finalize
+    SLAM_HIP_TRY(hipGetLastError());
+    return SLAM_OK;
+}
+
 int dist_sync_results(slam_dist* d, int32_t first, int32_t count, slam_pf_result* out) {
     for (int i = 0; i < d->nloc; ++i) SLAM_HIP_TRY(hipStreamSynchronize(d->sh[i]->stream));
     int rc = sync_results(d->sh[0], first, count, out);
     for (int i = 0; i < count; ++i) {
-        const int32_t st = d->sh[0]->res_host[i].status;
+        const int32_t st = d->sh[0]->res_host[first + i].status;
         if (st & kDistStWait) rc = fail(SLAM_ERR_COMM, "sharded step: a peer did not publish in time");
         if (st & kDistStItems) rc = fail(SLAM_ERR_COMM, "sharded resample: exchange inconsistent");
     }
@@ -420,6 +606,55 @@ int slam_dist_connect_comm(slam_dist* d, slam_comm* comm) {
     return slam_dist_connect(d, all.data());
 }
 
+// Exchange by collectives instead of peer-memory stores (the fallback when a
+// peer's exchange region cannot be mapped): one held shard with an RCCL
+// communicator of the filter's world (rank = comm rank), or every shard held
+// (LOCAL) with comm = NULL -- the collectives are then device copies between
+// the held regions.  The steps become host-orchestrated (no hipGraphs).
+int slam_dist_set_collective(slam_dist* d, slam_comm* comm) {
+    SLAM_ARG_CHECK(d, "slam_dist_set_collective: NULL handle");
+    if (comm) {
+        int32_t w = 0, r = 0;
+        int rc = slam_comm_info(comm, &w, &r);
+        if (rc) return rc;
+        SLAM_ARG_CHECK(d->nloc == 1 && w == d->world && r == d->rank0,
+                       "slam_dist_set_collective: one held shard, communicator of the filter's world and rank");
+    } else {
+        SLAM_ARG_CHECK(d->local, "slam_dist_set_collective: without a communicator every shard must be held");
+    }
+    SLAM_HIP_TRY(hipSetDevice(d->device));
+    dist_drop_graphs(d);
+    const int w = d->world;
+    if (!d->cnt_mat) {
+        void* p = nullptr;
+        int rc = dist_alloc(d, &p, 8 * (size_t)w * w);
+        if (rc) return rc;
+        d->cnt_mat = (int64_t*)p;
+        SLAM_HIP_TRY(hipHostMalloc((void**)&d->hst, 8 * (size_t)(3 * w * w + 16)));
+        for (int i = 0; i < d->nloc; ++i) {
+            void *io = nullptr, *co = nullptr;
+            if ((rc = dist_alloc(d, &io, sizeof(DistItem) * (size_t)w * (size_t)d->L.cap_item)) ||
+                (rc = dist_alloc(d, &co, 8 * (size_t)w)))
+                return rc;
+            d->peers[i].item_out = (DistItem*)io;
+            d->peers[i].cnt_out = (int64_t*)co;
+        }
+    }
+    for (int i = 0; i < d->nloc; ++i) {
+        DistPeers& P = d->peers[i];
+        P.coll = 1;
+        for (int q = 0; q < w; ++q) P.base[q] = (q == d->rank0 + i) ? d->xbuf[i] : nullptr;
+    }
+    // the shards' flag words start over (the epochs published by publish launches)
+    for (int i = 0; i < d->nloc; ++i)
+        SLAM_HIP_TRY(hipMemset(d->xbuf[i] + d->L.flags, 0, 3 * kDistMaxWorld * 8));
+    d->comm = comm;
+    d->coll = true;
+    d->merged = false;
+    d->connected = true;
+    return SLAM_OK;
+}
+
 int slam_dist_destroy(slam_dist* d) {
     if (!d) return SLAM_OK;
     (void)hipSetDevice(d->device);
@@ -428,6 +663,7 @@ int slam_dist_destroy(slam_dist* d) {
         if (h && h->stream) (void)hipStreamSynchronize(h->stream);
     dist_drop_graphs(d);
     for (void* p : d->opened) (void)hipIpcCloseMemHandle(p);
+    if (d->hst) (void)hipHostFree(d->hst);
     for (char* p : d->xbuf) (void)hipFree(p);
     for (void* p : d->dallocs) (void)hipFree(p);
     // LOCAL: the shards keep running on private streams again
@@ -446,8 +682,9 @@ int slam_dist_destroy(slam_dist* d) {
 int slam_dist_set_merged(slam_dist* d, int32_t on, int32_t* active) {
     SLAM_ARG_CHECK(d, "slam_dist_set_merged: NULL handle");
     if (on >= 0) {
-        SLAM_ARG_CHECK(!on || d->merged_ok,
-                       "slam_dist_set_merged: needs one held shard with a co-resident scan grid");
+        SLAM_ARG_CHECK(!on || (d->merged_ok && !d->coll),
+                       "slam_dist_set_merged: needs one held shard with a co-resident scan grid "
+                       "(and the peer-memory exchange)");
         if (d->merged != (on != 0)) dist_drop_graphs(d);
         d->merged = on != 0;
     }
@@ -461,7 +698,7 @@ int slam_dist_step(slam_dist* d, const double* control, const double* z, slam_pf
     int rc;
     for (auto* h : d->sh)
         if ((rc = stage_inputs(h, control, z, nullptr, std::nan("")))) return rc;
-    if ((rc = dist_enqueue_step(d))) return rc;
+    if ((rc = d->coll ? dist_coll_step(d) : dist_enqueue_step(d))) return rc;
     for (auto* h : d->sh) h->stepno++;
     return dist_sync_results(d, 0, 1, res);
 }
@@ -485,13 +722,22 @@ int slam_dist_run(slam_dist* d, int32_t first_step, int32_t n_steps, const doubl
     for (auto* h : d->sh) {
         SLAM_ARG_CHECK(first_step >= 0 && first_step + n_steps <= h->z_steps,
                        "slam_dist_run: steps outside the loaded observations");
-        int rc = upload_controls(h, first_step, n_steps, controls);
-        if (!rc) rc = set_ctr(h, first_step);
-        if (rc || (rc = launch_prestep(h))) return rc;       // the first step's closed-form words
+        // controls, counters and the first step's closed-form words (the
+        // exchange owns the resample flag)
+        const int rc = launch_run_setup(h, first_step, n_steps, controls, -1);
+        if (rc) return rc;
+    }
+    int rc;
+    if (d->coll) {                             // host-orchestrated steps, one result read each
+        for (int32_t k = 0; k < n_steps; ++k) {
+            if ((rc = dist_coll_step(d))) return rc;
+            for (auto* h : d->sh) h->stepno++;
+            if ((rc = dist_sync_results(d, first_step + k, 1, nullptr))) return rc;
+        }
+        return dist_sync_results(d, first_step, n_steps, results);
     }
     const bool graphs = d->sh[0]->use_graph && !d->sh[0]->timing;
     hipStream_t s = d->sh[0]->stream;          // LOCAL: the shared stream; else the shard's
-    int rc;
     int32_t k = 0;
     while (k < n_steps) {
         const int par = d->sh[0]->cur;
@@ -519,7 +765,7 @@ int slam_dist_prepare_graphs(slam_dist* d, double* capture_ms) {
     SLAM_HIP_TRY(hipSetDevice(d->device));
     const auto t0 = std::chrono::steady_clock::now();
     int rc = SLAM_OK;
-    if (d->sh[0]->use_graph) {
+    if (d->sh[0]->use_graph && !d->coll) {
         std::vector<int> cur0;
         for (auto* h : d->sh) cur0.push_back(h->cur);
         for (int par = 0; par < 2 && rc == SLAM_OK; ++par) {

@@ -113,6 +113,9 @@ __global__ __launch_bounds__(kFinThreads) void finalize_deferred_kernel(
     const int64_t nfull = n / kSumChunk;
     const int64_t nch = (n + kSumChunk - 1) / kSumChunk;
     FIN_STAMP(0);
+    // the step, and the batch's bounds (the last step exports the batch's records)
+    const int32_t st_now = io.ctr[0], b_first = io.ctr[2], b_last = io.ctr[3];
+    const bool exp = io.res_host != nullptr && st_now == b_last && b_first <= b_last;
     if (tid == 0) {
         s_ncand = 0;
         s_min = ~0ull;
@@ -360,7 +363,8 @@ __global__ __launch_bounds__(kFinThreads) void finalize_deferred_kernel(
     FIN_STAMP(3);
     if (tid == 0) {
         const int32_t st = io.ctr[0];
-        write_result_xe(tot, s_xe, refp, s, flags, ess_th, io.ess_band, io.res + st, resampled_known);
+        write_result_xe(tot, s_xe, refp, s, flags, ess_th, io.ess_band, io.res + st, resampled_known,
+                        exp ? io.res_host + st : nullptr);
         s_flag = flags[kFlagResample];
         io.ctr[0] = st + 1;
         io.ctr[1] = io.ctr[1] + 1;
@@ -368,6 +372,11 @@ __global__ __launch_bounds__(kFinThreads) void finalize_deferred_kernel(
     }
     __syncthreads();
     FIN_STAMP(4);
+    if (exp && tid >= 1 && tid < 64) {
+        // the batch's earlier records (stored by earlier launches) to the host
+        // buffer; this step's record went there from write_result_xe
+        for (int32_t k = b_first + tid - 1; k < st_now; k += 63) io.res_host[k] = io.res[k];
+    }
     if (s_flag) {
         // fused-block totals of w for the next step's exact cumsum (S1), moved
         // through LDS so that lane t owns the contiguous blocks [t per, (t+1) per)

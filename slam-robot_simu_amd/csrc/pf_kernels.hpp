@@ -99,7 +99,10 @@ struct StepIO {
     double* zc;             // [cap][kZcWords] closed-form words (formed on the device per step)
     const double* ofs;      // [cap] host resample offset (NaN: device RNG)
     slam_pf_result* res;    // [cap] result records
-    int32_t* ctr;           // [0] step within the batch, [1] global RNG step
+    slam_pf_result* res_host;   // [cap] coherent pinned copy (device address): the last step of
+                                // a device-resident batch stores the batch's records there
+    int32_t* ctr;           // [0] step within the batch, [1] global RNG step, [2] / [3] the
+                            // batch's first / last step (slam_pf_run's setup)
     int32_t cap;            // steps the arrays hold (the step end prepares step ctr[0] + 1 < cap)
     int32_t motion;         // the handle's motion model (reference pose of the expansion)
     double ess_band;        // result.ess_near: |ess - ESS_TH| <= ess_band * ESS_TH

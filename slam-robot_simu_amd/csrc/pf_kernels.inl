@@ -23,6 +23,18 @@ __device__ unsigned long long g_probe[32];
 
 namespace slam {
 
+// Fused-kernel phase stamps (probe builds only: -DSLAM_PROBE_FUSED): per block,
+// wave 0's wall clock at entry, after the table staging, after the normals,
+// after predict (its loads consumed), after the likelihood and at the end.
+#ifdef SLAM_PROBE_FUSED
+constexpr int kFProbeBlocks = 1 << 14;
+__device__ unsigned long long g_fprobe[kFProbeBlocks * 8];
+#define FPROBE(k, dep) do { asm volatile("" :: "v"(dep)); \
+    if (threadIdx.x == 0 && blockIdx.x < kFProbeBlocks) g_fprobe[blockIdx.x * 8 + (k)] = wall_clock64(); } while (0)
+#else
+#define FPROBE(k, dep) do { } while (0)
+#endif
+
 #ifdef SLAM_PROBE_COUNT_SLOW
 __device__ unsigned long long g_probe_slow[2];   // slow particles, blocks with any (probe builds)
 #endif
@@ -1071,6 +1083,7 @@ __global__ __launch_bounds__(256) SLAM_FUSED_ATTR void pf_fused_kernel(
     const int64_t base = (int64_t)blockIdx.x * (256 * P);
     const int64_t i0 = base + P * (int64_t)threadIdx.x;
     const int wave_s = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+    FPROBE(0, st);
     // the device RNG's tables in LDS (every lane reaches the barrier)
     __shared__ RngTabsLds s_rng;
     RngTabs rtab{};
@@ -1078,6 +1091,7 @@ __global__ __launch_bounds__(256) SLAM_FUSED_ATTR void pf_fused_kernel(
         rtab = rng_tabs_stage(&s_rng, (int)threadIdx.x, 256);
         __syncthreads();
     }
+    FPROBE(1, st);
     bool valid[P];
     int64_t idx[P];
 #pragma unroll
@@ -1255,6 +1269,7 @@ __global__ __launch_bounds__(256) SLAM_FUSED_ATTR void pf_fused_kernel(
         }
     }
 
+    FPROBE(2, g[P - 1][2]);
     // ---- predict (control of this step: particle_filter.py:46-58 / motion_model.py:40-45)
     const double v = io.ctl[2 * st], om = io.ctl[2 * st + 1];
     double xv[P], yv[P], tv[P], sp[P], cp[P];
@@ -1275,6 +1290,7 @@ __global__ __launch_bounds__(256) SLAM_FUSED_ATTR void pf_fused_kernel(
         to[i0] = tv[0];
     }
 
+    FPROBE(3, xv[P - 1] + sp[P - 1]);
     // ---- likelihood and weight (particle_filter.py:170-198)
     double bn[P];
 #ifdef SLAM_PROBE_NO_LIK                                   // timing probe only: not exact
@@ -1285,6 +1301,7 @@ __global__ __launch_bounds__(256) SLAM_FUSED_ATTR void pf_fused_kernel(
     const int lane_dd = likelihood_lanes<LIK, P>(xv, yv, sp, cp, lm, zs,
                                                  io.zc + (size_t)st * kZcWords, lc, bn, wave_s);
 #endif
+    FPROBE(4, bn[P - 1]);
     if (__ballot(lane_dd) != 0 && __lane_id() == 0) atomicAdd(&flags[kFlagDDWaves], 1);
     // previous weights: particle_filter.py:222 (a resampled step starts from
     // 1/NP) / :235-236 (deferred: w_un / s, NaN -> 1/NP)
@@ -1303,6 +1320,7 @@ __global__ __launch_bounds__(256) SLAM_FUSED_ATTR void pf_fused_kernel(
 #ifndef SLAM_NO_EPILOGUE
         defer_epilogue(base, n, wv, xv, yv, tv, refp, dp, wave_s);
 #endif
+        FPROBE(5, wv[0]);
         // block 0, after its own particles: the NEXT step's closed-form words
         // (StepIO.zc) -- its eight sums (two per wave) and its
         // expansion about this step's refp (the estimate two steps before it)
@@ -1639,7 +1657,7 @@ __device__ void write_result(const BlockPartial& r, const double* xs, const doub
 __device__ void write_result_xe(const BlockPartial& r, const double* xe, double* refp,
                                 const double s, int32_t* flags, const double ess_th,
                                 const double ess_band, slam_pf_result* res,
-                                const int32_t resampled_known) {
+                                const int32_t resampled_known, slam_pf_result* res_host = nullptr) {
     slam_pf_result o;
     o.max_idx = r.maxi;
     o.max_val = r.maxv;
@@ -1672,6 +1690,7 @@ __device__ void write_result_xe(const BlockPartial& r, const double* xe, double*
     }
     refp[7] = 2.0;
     *res = o;
+    if (res_host) *res_host = o;
 }
 
 // One normalise block = kNormPer particles (kNormThreads lanes x kNormEPT,

@@ -181,23 +181,37 @@ __device__ __forceinline__ uint32_t mt_word(const uint32_t* __restrict__ X, cons
     return mt_temper(X[k & (cap - 1)]);
 }
 
-// candidate pair at stream word w: words w .. w + 3 (two legacy doubles)
-__device__ __forceinline__ bool mt_candidate(const uint32_t* __restrict__ X, const int64_t w,
-                                             const int64_t cap, double& x1, double& x2,
-                                             double& r2) {
-    uint32_t v[4];
-    const int64_t k0 = w & (cap - 1);
-    if (k0 + 3 < cap) {                                  // the common case: no wrap
+// The kMtCandPerThread candidates of a lane, stream words w .. w + 15: five
+// 16-byte loads of the 4-word-aligned window (the ring holds a power of two of
+// words, so no load straddles its wrap) shifted by w & 3 (uniform across the
+// grid: w = w0 + 4 c), instead of sixteen 4-byte loads; same words: candidate c is
+// words w0 + 4c .. + 3 (two legacy doubles, the polar test)
+static_assert(kMtCandPerThread == 4, "four candidates = sixteen words per lane");
+__device__ __forceinline__ void mt_lane_candidates(const uint32_t* __restrict__ X, const int64_t w,
+                                                   const int64_t cap, double x1[4], double x2[4],
+                                                   double r2[4], bool ok[4]) {
+    const int64_t base = w & ~(int64_t)3;
+    const int a = (int)(w & 3);
+    uint32_t v[20];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) v[j] = mt_temper(X[k0 + j]);
-    } else {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) v[j] = mt_temper(X[(w + j) & (cap - 1)]);
+    for (int i = 0; i < 5; ++i) {
+        const uint4 q = *reinterpret_cast<const uint4*>(X + ((base + 4 * i) & (cap - 1)));
+        v[4 * i] = q.x;
+        v[4 * i + 1] = q.y;
+        v[4 * i + 2] = q.z;
+        v[4 * i + 3] = q.w;
     }
-    x1 = 2.0 * mt_legacy_double(v[0], v[1]) - 1.0;
-    x2 = 2.0 * mt_legacy_double(v[2], v[3]) - 1.0;
-    r2 = x1 * x1 + x2 * x2;
-    return !(r2 >= 1.0 || r2 == 0.0);
+    uint32_t u[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+        u[i] = mt_temper(a == 0 ? v[i] : a == 1 ? v[i + 1] : a == 2 ? v[i + 2] : v[i + 3]);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        x1[k] = 2.0 * mt_legacy_double(u[4 * k], u[4 * k + 1]) - 1.0;
+        x2[k] = 2.0 * mt_legacy_double(u[4 * k + 2], u[4 * k + 3]) - 1.0;
+        r2[k] = x1[k] * x1[k] + x2[k] * x2[k];
+        ok[k] = !(r2[k] >= 1.0 || r2[k] == 0.0);
+    }
 }
 
 __device__ __forceinline__ int64_t mt_pairs(const MtDeviceState* st, const int64_t g) {
@@ -234,12 +248,11 @@ __global__ __launch_bounds__(kMtCountThreads) void mt_count_kernel(
     const int64_t w0 = p + mt_pre_words(pre_flag, n_pre);
     const int64_t c0 = (int64_t)blockIdx.x * kMtCandPerBlock + threadIdx.x * kMtCandPerThread;
     int cnt = 0;
+    double x1[kMtCandPerThread], x2[kMtCandPerThread], r2[kMtCandPerThread];
+    bool ok[kMtCandPerThread];
+    mt_lane_candidates(X, w0 + 4 * c0, cap, x1, x2, r2, ok);
 #pragma unroll
-    for (int k = 0; k < kMtCandPerThread; ++k) {
-        const int64_t c = c0 + k;
-        double x1, x2, r2;
-        if (c < ncand && mt_candidate(X, w0 + 4 * c, cap, x1, x2, r2)) ++cnt;
-    }
+    for (int k = 0; k < kMtCandPerThread; ++k) cnt += (c0 + k < ncand && ok[k]) ? 1 : 0;
     int tot;
     (void)mt_block_scan(cnt, &tot);
     if (threadIdx.x == 0) {
@@ -301,10 +314,10 @@ __global__ __launch_bounds__(kMtCountThreads) void mt_emit_kernel(
     double x1[kMtCandPerThread], x2[kMtCandPerThread], r2[kMtCandPerThread];
     bool acc[kMtCandPerThread];
     int cnt = 0;
+    mt_lane_candidates(X, w0 + 4 * c0, cap, x1, x2, r2, acc);
 #pragma unroll
     for (int k = 0; k < kMtCandPerThread; ++k) {
-        const int64_t c = c0 + k;
-        acc[k] = c < ncand && mt_candidate(X, w0 + 4 * c, cap, x1[k], x2[k], r2[k]);
+        acc[k] = acc[k] && c0 + k < ncand;
         cnt += acc[k] ? 1 : 0;
     }
     __shared__ long long s_part[kMtCountThreads / 64];

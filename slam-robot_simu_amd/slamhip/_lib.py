@@ -133,6 +133,7 @@ SIGNATURES = {
     "slam_dist_export": (C.c_int, [_P, _P]),
     "slam_dist_connect": (C.c_int, [_P, _P]),
     "slam_dist_connect_comm": (C.c_int, [_P, _P]),
+    "slam_dist_set_collective": (C.c_int, [_P, _P]),
     "slam_dist_step": (C.c_int, [_P, _D, _D, C.POINTER(PFResult)]),
     "slam_dist_load_observations": (C.c_int, [_P, C.c_int32, _D]),
     "slam_dist_run": (C.c_int, [_P, C.c_int32, C.c_int32, _D, C.POINTER(PFResult)]),

@@ -117,6 +117,7 @@ class DistFilter:
             self.close()
             raise
         self.resample_next = False
+        self.collective = False
 
     def export_handle(self) -> bytes:
         """This rank's exchange-region IPC handle (slam_dist_export)."""
@@ -132,6 +133,16 @@ class DistFilter:
         size = len(blobs[0])
         allb = C.create_string_buffer(b"".join(blobs), size * self.world)
         check(self._lib.slam_dist_connect(self._d, allb), "slam_dist_connect")
+
+    def use_collectives(self, comm=None):
+        """Exchange by collectives instead of peer-memory stores
+        (slam_dist_set_collective): RCCL through ``comm`` (one rank per
+        process; no connect needed -- the fallback when a peer's region cannot
+        be mapped), or device copies between the held shards (LOCAL, comm
+        None).  Steps are then host-orchestrated, without hipGraphs."""
+        check(self._lib.slam_dist_set_collective(self._d, comm._h if comm is not None else None),
+              "slam_dist_set_collective")
+        self.collective = True
 
     def close(self):
         if getattr(self, "_d", None):

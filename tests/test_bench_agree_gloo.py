@@ -22,7 +22,7 @@ def _agree(ok):
     return int(t.item()) == 1
 
 
-def _worker(rank, world, port, fail_rank, fail_phase, q):
+def _worker(rank, world, port, fail_rank, fail_phase, q, fallback=False):
     sys.path.insert(0, ROOT)
     import bench
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -43,8 +43,8 @@ def _worker(rank, world, port, fail_rank, fail_phase, q):
         blobs = [None] * world
         dist.all_gather_object(blobs, blob)                 # the handle exchange collective
         ag.checkpoint("handle exchange")
-        ag.attempt(work, "connect")
-        ag.checkpoint("connect")
+        mode, why = bench.connect_exchange(ag, lambda: work("connect"),
+                                           (lambda: work("collectives")) if fallback else None)
         # the real bench.timed_runs over a stand-in filter: a failure in any of
         # its phases must still pair every barrier and reach the agreement
         import numpy as np
@@ -63,7 +63,7 @@ def _worker(rank, world, port, fail_rank, fail_phase, q):
                 return (0.0, 0)
 
         bench.timed_runs(Filt(), np.zeros((6, 2)), 2, 2, dist.barrier, ag)
-        return "sharded"
+        return "sharded" if mode == "peer" else "sharded-rccl"
 
     try:
         mode, phase = sharded(), None
@@ -110,3 +110,55 @@ def test_one_rank_failure_agreed(fail_rank, fail_phase, expect_phase):
     # the failing rank did no work after its failure; the others stopped at the checkpoint
     flog = res[fail_rank][3]
     assert flog[-1] == fail_phase
+
+
+@pytest.mark.parametrize("fail_phase,expect", [("connect", "sharded-rccl"), ("collectives", "replicas")])
+def test_connect_failure_falls_back_to_collectives(fail_phase, expect):
+    """A peer-memory connect failure on one rank sends every rank to the
+    collective exchange together (bench.connect_exchange); only if that fails
+    as well do the ranks fall back to replicas."""
+    import socket
+    world = 2
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker_two, args=(r, world, port, fail_phase, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert {m for _, m, _, _ in res} == {expect}, res
+    if expect == "replicas":
+        for _, _, phase, _ in res:
+            assert phase.startswith("collectives"), phase
+
+
+def _worker_two(rank, world, port, fail_phase, q):
+    """rank 1 fails its connect (and, for fail_phase "collectives", its
+    collective setup too)."""
+    sys.path.insert(0, ROOT)
+    import bench
+    fail = {"connect"} | ({"collectives"} if fail_phase == "collectives" else set())
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    log = []
+
+    def work(phase):
+        log.append(phase)
+        if rank == 1 and phase in fail:
+            raise RuntimeError(f"injected {phase}")
+        return phase
+
+    try:
+        ag = bench.Agreement(_agree, rank)
+        mode, why = bench.connect_exchange(ag, lambda: work("connect"), lambda: work("collectives"))
+        mode, phase = ("sharded" if mode == "peer" else "sharded-rccl"), None
+    except bench.ShardedFailure as e:
+        mode, phase = "replicas", e.args[0]
+    dist.barrier()
+    dist.destroy_process_group()
+    q.put((rank, mode, phase, log))

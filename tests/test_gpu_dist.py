@@ -210,3 +210,70 @@ def test_dist_two_processes_share_one_gpu(world):
         assert [(r["max_idx"], r["weight_sum"], r["resampled"]) for r in ref] == res
     for k in range(4):
         np.testing.assert_array_equal(np.concatenate([out[r][1][k] for r in range(world)]), xs[k])
+
+
+@pytest.mark.parametrize("world,n_global,nl,lik", [(2, 2 * 8192 + 1000, 5, "product"),
+                                                  (4, 4 << 18, 100, "logsum"),
+                                                  (8, 8 << 20, 100, "logsum")])
+def test_dist_collective_local_matches_single(world, n_global, nl, lik):
+    """Collective mode (slam_dist_set_collective) with every shard held: the
+    exchanges as host-orchestrated collectives (device copies between the held
+    regions standing for RCCL's all-gathers and grouped send/recv), step by
+    step and as a run, bit-identical to one handle."""
+    from slamhip.dist import DistFilter
+    from slamhip.pf import DeviceParticleFilter
+    steps = 20
+    lm, zs, p = _world(n_global, nl, steps, 60 + world)
+    ctl = np.tile([p.vel, p.omega], (steps, 1))
+    single = DeviceParticleFilter(n_global, lm, motion="velocity", likelihood=lik, seed=9)
+    dist = DistFilter(n_global, lm, world=world, motion="velocity", likelihood=lik, seed=9)
+    try:
+        dist.use_collectives()
+        assert not dist.set_merged(None)
+        ra, rb = [], []
+        for k in range(6):
+            ra.append(single.step((p.vel, p.omega), zs[k]))
+            rb.append(dist.step((p.vel, p.omega), zs[k]))
+        single.load_observations(zs)
+        dist.load_observations(zs)
+        ra += single.run(6, ctl[6:])
+        rb += dist.run(6, ctl[6:])
+        for k, (a, b) in enumerate(zip(ra, rb)):
+            _same(a, b, k)
+        assert sum(r["resampled"] for r in ra) >= 3
+        for u, v in zip(single.get_state(), dist.get_state()):
+            np.testing.assert_array_equal(u, v)
+    finally:
+        dist.close()
+        single.close()
+
+
+def test_dist_collective_one_rank_rccl_matches_single():
+    """Collective mode through a 1-rank RCCL communicator (the one-process-per-
+    GPU fallback, without any IPC mapping), at the bench size."""
+    from slamhip.dist import Comm, DistFilter
+    from slamhip.pf import DeviceParticleFilter
+    comm = Comm(Comm.unique_id(), 1, 0, 0)
+    n, nl, steps = 1 << 20, 100, 16
+    lm, zs, p = _world(n, nl, steps, 23)
+    ctl = np.tile([p.vel, p.omega], (steps, 1))
+    try:
+        single = DeviceParticleFilter(n, lm, motion="velocity", likelihood="logsum", seed=31)
+        dist = DistFilter(n, lm, world=1, rank=0, connect=False, motion="velocity",
+                          likelihood="logsum", seed=31)
+        try:
+            dist.use_collectives(comm)
+            assert dist.prepare_graphs() < 5.0          # nothing to capture
+            single.load_observations(zs)
+            dist.load_observations(zs)
+            ra, rb = single.run(0, ctl), dist.run(0, ctl)
+            for k, (a, b) in enumerate(zip(ra, rb)):
+                _same(a, b, k)
+            assert sum(r["resampled"] for r in ra) >= 3
+            for u, v in zip(single.get_state(), dist.get_state()):
+                np.testing.assert_array_equal(u, v)
+        finally:
+            dist.close()
+            single.close()
+    finally:
+        comm.close()

@@ -23,11 +23,21 @@ def _bits(a):
 
 @pytest.mark.parametrize("seed,warm,g", [(0, 0, 1), (1, 3, 2), (2, 1, 3), (3, 0, 1000),
                                          (4, 311, 1501), (5, 312, 6000), (6, 7, 100001),
-                                         (7, 0, 3 * (1 << 20) + 200)])
+                                         (7, 0, 3 * (1 << 20) + 200),
+                                         # > 4096 emit blocks: the prefix launch (rng_api.hip)
+                                         (8, 5, 3 * (1 << 22) + 7),
+                                         # odd stream positions: candidates start at every
+                                         # word alignment of the ring's 16-byte loads
+                                         (9, -311, 20001), (10, -3, 3 * (1 << 20) + 1)])
 def test_standard_normal_matches_numpy(seed, warm, g):
+    """warm < 0: the state's position set to -warm (an odd word offset)."""
     from slamhip.rng import DeviceRandomState
     rs = np.random.RandomState(seed)
-    rs.random_sample(warm)
+    if warm >= 0:
+        rs.random_sample(warm)
+    else:
+        st = rs.get_state()
+        rs.set_state((st[0], st[1], -warm, 0, 0.0))
     with DeviceRandomState(rs, device=0) as d:
         out = d.standard_normal(g)
         ref = rs.standard_normal(g)
