@@ -120,7 +120,12 @@ int slam_debug_pair_normals(int device, uint64_t p0, int64_t count, uint32_t rst
                             double* out);
 
 /* Device-resident multi-step run (bench path): observations for n_steps steps
- * are uploaded once; steps are enqueued back to back with no host sync. */
+ * are uploaded once; steps are enqueued back to back with no host sync.  A
+ * run is one setup launch (controls read from pinned host memory, counters,
+ * the first step's closed-form words unless the previous run's last step
+ * formed them for the same control), the steps' graphs (1/2/4/8-step shapes,
+ * binary decomposition of n_steps), and one wait: the last step's finalize
+ * stores the batch's result records into pinned host memory itself. */
 int slam_pf_load_observations(slam_pf* h, int32_t n_steps, const double* z_all);
 int slam_pf_run(slam_pf* h, int32_t first_step, int32_t n_steps, const double* controls,
                 slam_pf_result* results);
@@ -132,7 +137,7 @@ int slam_pf_enable_timing(slam_pf* h, int32_t on);
 int slam_pf_timing(slam_pf* h, int32_t kernel, double* total_ms, int64_t* launches);
 /* slam_pf_run replays one captured hipGraph per step (default on). */
 int slam_pf_set_graphs(slam_pf* h, int32_t on);
-/* Capture every graph slam_pf_run will replay (8-step and 1-step graphs for
+/* Capture every graph slam_pf_run will replay (1-, 2-, 4- and 8-step graphs for
  * both ping-pong parities) without running them, so that no capture lands in
  * a timed run; *capture_ms (may be NULL) = host time spent.  Graphs are
  * dropped (and captured again on demand) by the calls that change a step's
