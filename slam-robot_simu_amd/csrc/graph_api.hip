@@ -57,7 +57,6 @@ struct slam_graph {
     PcgState* pcg_host = nullptr;  // pinned copies of the device states: the polls of the
     CondState* cond_host = nullptr;  // two streams must not block the host (pageable copies do)
     bool cond_warm = false;        // cx holds the previous update's vectors of this edge set
-    bool cond_fused = true;        // the estimate shares the solve's launches (SLAM_GRAPH_FUSED=0: own stream)
     int32_t cond_last_iters = 0;
     double cond_info[7] = {0, 0, 0, 0, 0, 0, 0};
     hipEvent_t ev[5] = {};
@@ -446,9 +445,10 @@ int solve_dense(slam_graph* h, double* stats, bool* solved) {
 // condition-number estimate (graph_kernels.inl: LOBPCG for the extreme
 // eigenvalues) on h->cstream, enqueued in batches of `count` iterations
 // starting at iteration k0 (k0 = 0: the start sequence first).
-int cond_enqueue(slam_graph* h, int32_t k0, int32_t count, hipStream_t s) {
+int cond_enqueue(slam_graph* h, int32_t k0, int32_t count) {
     const int64_t n = 3 * h->nt;
     const unsigned nb = nblk(n, kPcgThreads);
+    hipStream_t s = h->cstream;
     const double tol = h->cfg.cond_tol > 0.0 ? h->cfg.cond_tol : 1e-5;
     const int32_t mx = h->cfg.cond_max_iter > 0 ? h->cfg.cond_max_iter : 3000;
     int32_t k = k0;
@@ -490,15 +490,10 @@ int solve_pcg(slam_graph* h, double* stats, bool* solved, int32_t* iters) {
     const bool est = (h->cfg.cond_mode == SLAM_GRAPH_COND_ESTIMATE);
     hipLaunchKernelGGL(graph_block_inv_kernel, dim3(nblk(h->nt)), dim3(256), 0, h->stream, h->nt,
                        h->dslot, h->val, h->minv);
-    // the estimate beside the solve: in shared launches on the solve's stream
-    // (fused: PCG iteration k with estimate iteration k + 1, while both run),
-    // or on its own stream (SLAM_GRAPH_FUSED=0)
-    const bool fused = est && h->cond_fused;
-    hipStream_t cstr = fused ? h->stream : h->cstream;
     if (est) {
         SLAM_HIP_TRY(hipEventRecord(h->cev[0], h->stream));
-        SLAM_HIP_TRY(hipStreamWaitEvent(cstr, h->cev[0], 0));
-        SLAM_HIP_TRY(hipEventRecord(h->cev[1], cstr));
+        SLAM_HIP_TRY(hipStreamWaitEvent(h->cstream, h->cev[0], 0));
+        SLAM_HIP_TRY(hipEventRecord(h->cev[1], h->cstream));
     }
     hipLaunchKernelGGL(graph_pcg_start_kernel, dim3(nb), dim3(kPcgThreads), 0, h->stream, n,
                        h->minv, h->b, h->delta, h->r, h->z, h->part);
@@ -514,46 +509,7 @@ int solve_pcg(slam_graph* h, double* stats, bool* solved, int32_t* iters) {
     int32_t c_end = std::max<int32_t>(kCondWin + 1, std::min<int32_t>(h->cond_last_iters + 1, 1024));
     bool pcg_done = false, cond_done = !est, abandoned = false;
     int32_t k0 = 0, c0 = 0;
-    const CondArgs ca{h->minv, h->cx, h->chx, h->cw, h->cw2, h->chw, h->cp, h->chp, h->cpart, h->cst};
     while (!pcg_done || !cond_done) {
-        if (fused && !pcg_done && !cond_done) {
-            if (c0 == 0) {                               // the estimate's start (its iteration 0)
-                GTRY(cond_enqueue(h, 0, 1, h->stream));
-                c0 = 1;
-            }
-            // invariant here: c0 == k0 + 1
-            const int32_t ke = std::min(k_end, c_end - 1);
-            const double tol = h->cfg.cond_tol > 0.0 ? h->cfg.cond_tol : 1e-5;
-            const int32_t mx = h->cfg.cond_max_iter > 0 ? h->cfg.cond_max_iter : 3000;
-            for (int32_t k = k0; k < ke; ++k) {
-                hipLaunchKernelGGL(graph_pcg_cond_spmv_kernel, dim3(nb), dim3(kSpmvThreads), 0,
-                                   h->stream, h->nt, k, h->rptr, h->scol, h->val, h->z, h->p, h->q,
-                                   h->part, h->st, h->cfg.pcg_tol, h->cfg.pcg_max_iter, ca);
-                hipLaunchKernelGGL(graph_cond_fold_kernel, dim3(1), dim3(kCondFoldThreads), 0,
-                                   h->stream, (int64_t)nb, h->cpart, h->cst, k + 1, tol, mx,
-                                   h->cfg.cond_max);
-                hipLaunchKernelGGL(graph_pcg_cond_step_kernel, dim3(nb), dim3(kPcgThreads), 0,
-                                   h->stream, n, k, h->minv, h->p, h->q, h->delta, h->r, h->z,
-                                   h->part, h->st, k + 1, ca);
-            }
-            SLAM_HIP_TRY(hipGetLastError());
-            SLAM_HIP_TRY(hipMemcpyAsync(h->pcg_host, h->st, sizeof(PcgState), hipMemcpyDeviceToHost,
-                                        h->stream));
-            SLAM_HIP_TRY(hipMemcpyAsync(h->cond_host, h->cst, sizeof(CondState), hipMemcpyDeviceToHost,
-                                        h->stream));
-            SLAM_HIP_TRY(hipStreamSynchronize(h->stream));
-            pcg_done = s.done;
-            cond_done = cs.done;
-            k0 = ke;
-            c0 = ke + 1;
-            if (!pcg_done && k0 >= k_end) k_end = k0 + 8;
-            if (!cond_done && c0 >= c_end) c_end = c0 + 16;
-            if (cs.done && (cs.status == 2 || cs.status == 4) && !pcg_done) {
-                pcg_done = true;                         // the gate rejects: no solve (:496)
-                abandoned = true;
-            }
-            continue;
-        }
         if (!pcg_done) {
             for (int32_t k = k0; k < k_end; ++k) {
                 hipLaunchKernelGGL(graph_pcg_dir_spmv_kernel, dim3(nb), dim3(kSpmvThreads), 0,
@@ -567,9 +523,9 @@ int solve_pcg(slam_graph* h, double* stats, bool* solved, int32_t* iters) {
                                         h->stream));
         }
         if (!cond_done) {
-            GTRY(cond_enqueue(h, c0, c_end - c0, cstr));
+            GTRY(cond_enqueue(h, c0, c_end - c0));
             SLAM_HIP_TRY(hipMemcpyAsync(h->cond_host, h->cst, sizeof(CondState), hipMemcpyDeviceToHost,
-                                        cstr));
+                                        h->cstream));
         }
         if (!pcg_done) {
             SLAM_HIP_TRY(hipStreamSynchronize(h->stream));
@@ -578,7 +534,7 @@ int solve_pcg(slam_graph* h, double* stats, bool* solved, int32_t* iters) {
             k_end += 8;
         }
         if (!cond_done) {
-            SLAM_HIP_TRY(hipStreamSynchronize(cstr));
+            SLAM_HIP_TRY(hipStreamSynchronize(h->cstream));
             cond_done = cs.done;
             c0 = c_end;
             c_end += 16;
@@ -598,7 +554,7 @@ int solve_pcg(slam_graph* h, double* stats, bool* solved, int32_t* iters) {
     bool gate = true;
     for (double& v : h->cond_info) v = 0.0;
     if (est) {
-        SLAM_HIP_TRY(hipEventRecord(h->cev[2], cstr));
+        SLAM_HIP_TRY(hipEventRecord(h->cev[2], h->cstream));
         SLAM_HIP_TRY(hipEventSynchronize(h->cev[2]));
         float ms = 0.f;
         SLAM_HIP_TRY(hipEventElapsedTime(&ms, h->cev[1], h->cev[2]));
@@ -685,10 +641,6 @@ int slam_graph_create(const slam_graph_config* cfg, int device, slam_graph** out
     if (h->cfg.cond_max_iter <= 0) h->cfg.cond_max_iter = 3000;
     if (!(h->cfg.pcg_tol > 0.0)) h->cfg.pcg_tol = 1e-10;
     h->device = device;
-    {
-        const char* ev = std::getenv("SLAM_GRAPH_FUSED");
-        h->cond_fused = !(ev && ev[0] == '0');
-    }
     if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&h->cstream, hipStreamNonBlocking) != hipSuccess) {
         slam_graph_destroy(h);

@@ -723,7 +723,7 @@ __device__ __forceinline__ void pcg_block_dot(const int64_t s, const int64_t* __
     a2 = fma(b[8], z2, a2);
 }
 
-__device__ __forceinline__ void pcg_dir_spmv_body(
+__global__ __launch_bounds__(kSpmvThreads) void graph_pcg_dir_spmv_kernel(
     const int64_t nt, const int32_t k, const int64_t* __restrict__ rptr,
     const int64_t* __restrict__ col, const double* __restrict__ val,
     const double* __restrict__ z, double* __restrict__ p, double* __restrict__ q,
@@ -780,18 +780,9 @@ __device__ __forceinline__ void pcg_dir_spmv_body(
     if (threadIdx.x == 0) part[blockIdx.x] = pq;
 }
 
-__global__ __launch_bounds__(kSpmvThreads) void graph_pcg_dir_spmv_kernel(
-    const int64_t nt, const int32_t k, const int64_t* __restrict__ rptr,
-    const int64_t* __restrict__ col, const double* __restrict__ val,
-    const double* __restrict__ z, double* __restrict__ p, double* __restrict__ q,
-    double* __restrict__ part, PcgState* __restrict__ st, const double tol,
-    const int32_t max_iter) {
-    pcg_dir_spmv_body(nt, k, rptr, col, val, z, p, q, part, st, tol, max_iter);
-}
-
 // iteration k, second launch: alpha = rho_k / p.q (curvature gate), x += alpha p,
 // r -= alpha q, z = M^-1 r ; partials r.z, r.r
-__device__ __forceinline__ void pcg_step_body(
+__global__ __launch_bounds__(kPcgThreads) void graph_pcg_step_kernel(
     const int64_t n, const int32_t k, const double* __restrict__ minv,
     const double* __restrict__ p, const double* __restrict__ q, double* __restrict__ x,
     double* __restrict__ r, double* __restrict__ z, double* __restrict__ part,
@@ -845,14 +836,6 @@ __device__ __forceinline__ void pcg_step_body(
         part[nb + blockIdx.x] = rz;
         part[2 * nb + blockIdx.x] = rr;
     }
-}
-
-__global__ __launch_bounds__(kPcgThreads) void graph_pcg_step_kernel(
-    const int64_t n, const int32_t k, const double* __restrict__ minv,
-    const double* __restrict__ p, const double* __restrict__ q, double* __restrict__ x,
-    double* __restrict__ r, double* __restrict__ z, double* __restrict__ part,
-    PcgState* __restrict__ st) {
-    pcg_step_body(n, k, minv, p, q, x, r, z, part, st);
 }
 
 // ------------------------------------------- condition number (PCG path)
@@ -1104,7 +1087,7 @@ __device__ __forceinline__ void cond_block_dot2(const int64_t s, const int64_t* 
 // (three per wave: lanes take three rows each, then the xor butterfly).
 constexpr int kCondRows = kSpmvThreads / kSpmvGroup * 3;   // 192 rows per workgroup
 template <bool START>
-__device__ __forceinline__ void cond_spmv_body(
+__global__ __launch_bounds__(kSpmvThreads) void graph_cond_spmv_kernel(
     const int64_t nt, const int64_t* __restrict__ rptr, const int64_t* __restrict__ col,
     const double* __restrict__ val, const double* __restrict__ x, double* __restrict__ hx,
     const double* __restrict__ w, double* __restrict__ w2, double* __restrict__ hw,
@@ -1198,16 +1181,6 @@ __device__ __forceinline__ void cond_spmv_body(
 }
 static_assert(kSpmvThreads / 64 * 3 == 2 * kCondGram, "three Gram quantities per wave");
 
-template <bool START>
-__global__ __launch_bounds__(kSpmvThreads) void graph_cond_spmv_kernel(
-    const int64_t nt, const int64_t* __restrict__ rptr, const int64_t* __restrict__ col,
-    const double* __restrict__ val, const double* __restrict__ x, double* __restrict__ hx,
-    const double* __restrict__ w, double* __restrict__ w2, double* __restrict__ hw,
-    const double* __restrict__ p, const double* __restrict__ hp, double* __restrict__ part,
-    const CondState* __restrict__ st) {
-    cond_spmv_body<START>(nt, rptr, col, val, x, hx, w, w2, hw, p, hp, part, st);
-}
-
 // One workgroup per iteration: the 24 Gram partial rows folded in a fixed
 // order (one wave per row, lanes strided, then the xor butterfly), then the
 // two small problems (one lane each, on different waves), the stopping tests
@@ -1297,7 +1270,7 @@ __global__ __launch_bounds__(kCondFoldThreads) void graph_cond_fold_kernel(
 // side it updated); unless the estimate is done, r = Hx - theta x, w = T r
 // (side 0: the block-Jacobi inverse of the pose, the three rows of a pose in
 // one workgroup; side 1: w = r) and the x.w partials.
-__device__ __forceinline__ void cond_update_body(
+__global__ __launch_bounds__(kPcgThreads) void graph_cond_update_kernel(
     const int64_t n, const int32_t k, const double* __restrict__ minv, double* __restrict__ x,
     double* __restrict__ hx, const double* __restrict__ w2, const double* __restrict__ hw,
     double* __restrict__ p, double* __restrict__ hp, double* __restrict__ w,
@@ -1360,47 +1333,6 @@ __device__ __forceinline__ void cond_update_body(
         part[2 * kCondGram * nb + blockIdx.x] = xw0;
         part[(2 * kCondGram + 1) * nb + blockIdx.x] = xw1;
     }
-}
-
-__global__ __launch_bounds__(kPcgThreads) void graph_cond_update_kernel(
-    const int64_t n, const int32_t k, const double* __restrict__ minv, double* __restrict__ x,
-    double* __restrict__ hx, const double* __restrict__ w2, const double* __restrict__ hw,
-    double* __restrict__ p, double* __restrict__ hp, double* __restrict__ w,
-    double* __restrict__ part, const CondState* __restrict__ st) {
-    cond_update_body(n, k, minv, x, hx, w2, hw, p, hp, w, part, st);
-}
-
-// The solve and the estimate in shared launches (round 4):
-// while both run, PCG iteration k and estimate iteration k + 1 go through the
-// same two grid launches (the estimate's one-workgroup fold between them), one
-// after the other inside each workgroup -- the two SpMVs read the workgroup's
-// block rows of H back to back, the second from L2 -- instead of five
-// launches on two streams that contend for the device.  Each body keeps its
-// own early exit, so either may have finished.
-struct CondArgs {
-    const double* minv;
-    double *x, *hx, *w, *w2, *hw, *p, *hp, *part;
-    CondState* st;
-};
-
-__global__ __launch_bounds__(kSpmvThreads) void graph_pcg_cond_spmv_kernel(
-    const int64_t nt, const int32_t k, const int64_t* __restrict__ rptr,
-    const int64_t* __restrict__ col, const double* __restrict__ val,
-    const double* __restrict__ z, double* __restrict__ p, double* __restrict__ q,
-    double* __restrict__ part, PcgState* __restrict__ st, const double tol,
-    const int32_t max_iter, const CondArgs ca) {
-    pcg_dir_spmv_body(nt, k, rptr, col, val, z, p, q, part, st, tol, max_iter);
-    cond_spmv_body<false>(nt, rptr, col, val, ca.x, ca.hx, ca.w, ca.w2, ca.hw, ca.p, ca.hp, ca.part,
-                          ca.st);
-}
-
-__global__ __launch_bounds__(kPcgThreads) void graph_pcg_cond_step_kernel(
-    const int64_t n, const int32_t k, const double* __restrict__ minv,
-    const double* __restrict__ p, const double* __restrict__ q, double* __restrict__ x,
-    double* __restrict__ r, double* __restrict__ z, double* __restrict__ part,
-    PcgState* __restrict__ st, const int32_t kc, const CondArgs ca) {
-    pcg_step_body(n, k, minv, p, q, x, r, z, part, st);
-    cond_update_body(n, kc, ca.minv, ca.x, ca.hx, ca.w2, ca.hw, ca.p, ca.hp, ca.w, ca.part, ca.st);
 }
 
 // block-Jacobi preconditioner: inverses of the diagonal 3x3 blocks

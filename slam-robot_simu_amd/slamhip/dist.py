@@ -18,7 +18,7 @@ import numpy as np
 
 from . import _lib
 from ._lib import PFResult, check, dptr
-from .pf import DeviceParticleFilter, _f64, make_config
+from .pf import DeviceParticleFilter, RunResults, _f64, make_config
 
 
 class Comm:
@@ -189,7 +189,7 @@ class DistFilter:
         res = (PFResult * k)()
         check(self._lib.slam_dist_run(self._d, int(first_step), k, dptr(controls), res), "slam_dist_run")
         self.resample_next = bool(res[k - 1].resample_next)
-        return [DeviceParticleFilter._res(r) for r in res] if want_results else None
+        return RunResults(res) if want_results else None
 
     def set_merged(self, on=None):
         """Resample exchange in one launch (True) or five (False); None only

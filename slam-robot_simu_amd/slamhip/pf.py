@@ -6,6 +6,7 @@ observations and (in NumPy-stream mode) noise across the boundary.
 from __future__ import annotations
 
 import ctypes as C
+from collections.abc import Sequence
 
 import numpy as np
 
@@ -47,6 +48,39 @@ def make_config(n_global, *, dt=0.1, q=None, r=None, x0=(10.0, 0.0, np.pi / 2), 
     cfg.motion = _lib.MOTION[motion]
     cfg.likelihood = _lib.LIKELIHOOD[likelihood]
     return cfg
+
+
+class RunResults(Sequence):
+    """The records of a device-resident batch (slam_pf_run / slam_dist_run):
+    the C-ABI's slam_pf_result array as returned, each record read into the
+    dict of DeviceParticleFilter._res when it is accessed (a batch's Python
+    dicts cost ~6 us per step; building them lazily keeps that out of the
+    batch's own call).  ``records`` is the same memory as a NumPy structured
+    array."""
+
+    def __init__(self, res):
+        self._r = res
+
+    @property
+    def records(self):
+        return np.ctypeslib.as_array(self._r)
+
+    def __len__(self):
+        return len(self._r)
+
+    def __getitem__(self, i):
+        if isinstance(i, slice):
+            return [self[j] for j in range(*i.indices(len(self)))]
+        return DeviceParticleFilter._res(self._r[i])
+
+    def __add__(self, other):
+        return list(self) + list(other)
+
+    def __radd__(self, other):
+        return list(other) + list(self)
+
+    def __repr__(self):
+        return f"RunResults({list(self)!r})"
 
 
 class DeviceParticleFilter:
@@ -247,7 +281,7 @@ class DeviceParticleFilter:
         check(self._lib.slam_pf_run(self._h, int(first_step), k, dptr(controls), res),
               "slam_pf_run")
         self.resample_next = bool(res[k - 1].resample_next)
-        return [self._res(r) for r in res] if want_results else None
+        return RunResults(res) if want_results else None
 
     def set_ess_band(self, band):
         """Relative band of result['ess_near'] (and of the drop-in's host
