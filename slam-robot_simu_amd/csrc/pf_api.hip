@@ -131,7 +131,6 @@ struct slam_pf {
     // that can change the observations, landmarks or controls clears it.
     int32_t prep_step = -1;
     double prep_ctl[2] = {0.0, 0.0};
-    bool spin_wait = true;                // batch_wait: poll before blocking (SLAM_SPIN_WAIT=0: block)
 };
 
 namespace {
@@ -648,28 +647,6 @@ int launch_step(slam_pf* h, bool host_noise) {
     return launch_reduce(h, -1);
 }
 
-// A batch's end on the host: poll the stream (hipStreamQuery) for up to
-// kSpinUs, then block in hipStreamSynchronize.  A blocking wait's wake-up
-// costs tens of microseconds per call, which a device-resident batch of a few
-// 50 us steps would pay in full; SLAM_SPIN_WAIT=0 always blocks.
-constexpr double kSpinUs = 2000.0;
-
-int batch_wait(slam_pf* h) {
-    if (h->spin_wait) {
-        const auto t0 = std::chrono::steady_clock::now();
-        for (;;) {
-            const hipError_t e = hipStreamQuery(h->stream);
-            if (e == hipSuccess) return SLAM_OK;
-            if (e != hipErrorNotReady) break;          // the error surfaces below
-            if (std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count() >
-                kSpinUs)
-                break;
-        }
-    }
-    SLAM_HIP_TRY(hipStreamSynchronize(h->stream));
-    return SLAM_OK;
-}
-
 // The records of steps [first, first + count) from the coherent host buffer:
 // stored there by the batch's last step end (exported: slam_pf_run on a
 // deferred handle) or by one export launch here.
@@ -682,9 +659,9 @@ int sync_results(slam_pf* h, int32_t first, int32_t count, slam_pf_result* out, 
             reinterpret_cast<uint64_t*>(h->res_host_dev + first));
         SLAM_HIP_TRY(hipGetLastError());
     }
-    int rc = batch_wait(h);
-    if (rc) return rc;
+    SLAM_HIP_TRY(hipStreamSynchronize(h->stream));
     const slam_pf_result* r = h->res_host + first;
+    int rc = SLAM_OK;
     for (int i = 0; i < count; ++i) {
         if (out) out[i] = r[i];
         if (r[i].status & 8)
@@ -746,10 +723,6 @@ int create_impl(const slam_pf_config* cfg, int64_t n_local, int64_t n_global, in
                 hipSuccess)
             h->scan_merged_ok = deferred && (int64_t)h->nb_scan <= (int64_t)per_cu * cus / 2;
         h->scan_merged = h->scan_merged_ok;
-    }
-    {
-        const char* ev = std::getenv("SLAM_SPIN_WAIT");
-        h->spin_wait = !(ev && ev[0] == '0');
     }
     hipError_t e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking);
     if (e != hipSuccess) {
@@ -1210,9 +1183,13 @@ int slam_pf_run(slam_pf* h, int32_t first_step, int32_t n_steps, const double* c
     SLAM_HIP_TRY(hipSetDevice(h->device));
     int rc;
     int32_t prep_next = -1;
+    // a batch continuing the previous one with nothing changed in between
+    // (prep_step, cleared by every call that could): the previous step end
+    // left the block-total prefix for a resampling first step already
+    const bool continues = (h->prep_step == first_step);
     if ((rc = launch_run_setup(h, first_step, n_steps, controls, h->resample_next, &prep_next)))
         return rc;
-    if (h->resample_next && (rc = launch_bsum(h))) return rc;   // prefix for the first step's scan
+    if (h->resample_next && !continues && (rc = launch_bsum(h))) return rc;   // the first step's scan prefix
     const bool graphs = h->use_graph && !h->timing;
     int32_t k = 0;
     while (k < n_steps) {
@@ -1359,6 +1336,7 @@ int slam_pf_set_resample_next(slam_pf* h, int32_t on) {
     SLAM_ARG_CHECK(h, "slam_pf_set_resample_next: NULL handle");
     SLAM_ARG_CHECK(h->n == h->n_global, "slam_pf_set_resample_next: sharded handle");
     SLAM_HIP_TRY(hipSetDevice(h->device));
+    h->prep_step = -1;                       // the next run forms its scan prefix itself
     h->resample_next = on ? 1 : 0;
     int rc = set_flag(h, kFlagResample, h->resample_next);
     if (rc) return rc;

@@ -38,7 +38,10 @@ constexpr int kMtCountThreads = 256;
 constexpr int kMtCandPerBlock = kMtCountThreads * kMtCandPerThread;
 // emit blocks sum their predecessors' counts themselves up to this many blocks
 // (O(nb^2) reads in all); beyond, one prefix launch
-constexpr int kMtEmitSumMax = 4096;
+#ifndef SLAM_MT_EMIT_SUM_MAX
+#define SLAM_MT_EMIT_SUM_MAX 4096
+#endif
+constexpr int kMtEmitSumMax = SLAM_MT_EMIT_SUM_MAX;
 // requests one parallel round feeds: the jump (~160 us, LDS-bound) is paid
 // once per round, the sequential generation grows with it; 4 -> 16 took the
 // device stream from 0.229 to 0.201 ms per 2^20-particle step, 16 -> 32 from
