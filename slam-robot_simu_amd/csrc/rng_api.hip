@@ -45,9 +45,11 @@ constexpr int kMtEmitSumMax = SLAM_MT_EMIT_SUM_MAX;
 // requests one parallel round feeds: the jump (~160 us, LDS-bound) is paid
 // once per round, the sequential generation grows with it; 4 -> 16 took the
 // device stream from 0.229 to 0.201 ms per 2^20-particle step, 16 -> 32 from
-// 0.150 to 0.145 (the ring is ~4 GB at that request size, the one-time
-// priming ~150 ms)
-constexpr int64_t kMtRoundsAhead = 32;
+// 0.150 to 0.145, 32 -> 64 (round 4) from 0.121 to 0.118 (the ring is ~8 GB
+// at that request size, the one-time priming ~300 ms).  Larger requests feed
+// fewer (at least 4) so that the ring stays within kMtRingWordsMax.
+constexpr int64_t kMtRoundsAhead = 64;
+constexpr int64_t kMtRingWordsMax = int64_t(1) << 31;     // 8 GB of words
 
 // ------------------------------------------------------------------ kernels
 
@@ -690,18 +692,27 @@ int mt_reserve(MtBuffers& b, int64_t g_cap, int64_t pre_cap, int device) {
     if (b.R < 1) b.R = 1;
     // R > 1: a round covers kMtRoundsAhead requests, so the jump (a fixed
     // cost per round) is paid once per that many requests
+    // segment length and live words ([p - 624, g1) with g1 - p < need + R S,
+    // plus the round being written) for a given number of requests per round
+    auto seg_len = [&](int64_t ahead) {
+        const int64_t span = b.R > 1 ? ahead * b.need : b.need;
+        int64_t S = (span + (int64_t)b.R * kMtN - 1) / ((int64_t)b.R * kMtN) * kMtN;
+        if (b.R > 1 && S < kMtMinSeg) S = kMtMinSeg;
+        return std::max<int64_t>(S, kMtN);
+    };
+    auto live_words = [&](int64_t S) {
+        const int64_t RS = (int64_t)b.R * S;
+        return std::max<int64_t>(b.need + 2 * RS + 4 * kMtN, RS + 3 * kMtN);
+    };
     int64_t ahead = kMtRoundsAhead;
+    while (ahead > 4 && live_words(seg_len(ahead)) > kMtRingWordsMax) ahead >>= 1;
     if (const char* e = std::getenv("SLAM_MT_ROUNDS_AHEAD")) {   // diagnostic A/B
         const long v = std::atol(e);
         if (v >= 1 && v <= 64) ahead = v;
     }
-    const int64_t span = b.R > 1 ? ahead * b.need : b.need;
-    b.S = (span + (int64_t)b.R * kMtN - 1) / ((int64_t)b.R * kMtN) * kMtN;
-    if (b.R > 1 && b.S < kMtMinSeg) b.S = kMtMinSeg;
-    if (b.S < kMtN) b.S = kMtN;
+    b.S = seg_len(ahead);
     const int64_t RS = (int64_t)b.R * b.S;
-    // live words: [p - 624, g1) with g1 - p < need + R S, plus the round being written
-    const int64_t live = std::max<int64_t>(b.need + 2 * RS + 4 * kMtN, RS + 3 * kMtN);
+    const int64_t live = live_words(b.S);
     b.cap = 1;
     while (b.cap < live) b.cap <<= 1;                    // a power of two: index & (cap - 1)
     SLAM_HIP_TRY(hipMalloc(&b.st, sizeof(MtDeviceState)));

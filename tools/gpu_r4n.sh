@@ -8,6 +8,6 @@ mkdir -p $out
 for r in 1 2 3; do
   for a in 32 64; do
     SLAM_MT_ROUNDS_AHEAD=$a timeout -k 10 200 python tools/ns_ab.py > $out/ab_$a.txt 2>&1 || { tail -3 $out/ab_$a.txt; exit 1; }
-    echo "ahead=$a $(tail -1 $out/ab_$a.txt)"
+    echo "ahead=$a $(tail -1 $out/ab_$a.txt)" | tee -a $out/ab.txt
   done
 done
