@@ -257,6 +257,33 @@ __device__ __forceinline__ double exp_tab(const double x, const double2* __restr
     return (x < -746.0) ? 0.0 : (x > 710.0 ? __builtin_inf() : e);
 }
 
+// exp(-y/2) with exactly the bits of exp_tab(-y/2) -- the product
+// likelihood's exp(-q/2) without forming q/2 (one fp64 multiply less per
+// factor).  Every quantity is held at a power-of-two multiple of exp_tab's:
+// the reduction yields 2r, the polynomial's coefficients are scaled so that it
+// yields 2p, and the table htab holds (t.x/2, t.y).  Scaling by a power of two
+// commutes with rounding in the normal range; where y/2 would be subnormal the
+// result is 1 either way (tests/test_exp_tab.py checks the bits on the host).
+template <bool NONPOS = false>
+__device__ __forceinline__ double exp_nhalf(const double y, const double2* __restrict__ htab) {
+    constexpr double kInvLn2N = 0x1.71547652b82fep+6;       // exp_tab's constants
+    constexpr double kNegLn2HiN = -0x1.62e42ff000000p-7;
+    constexpr double kNegLn2LoN = 0x1.718432a1b0e26p-41;
+    const double kdm = fma(y, -0.5 * kInvLn2N, 0x1.8p52);   // = fma(-y/2, 64/ln2, shift)
+    const double kd = kdm - 0x1.8p52;
+    const double r = fma(kd, 2.0 * kNegLn2LoN, fma(kd, 2.0 * kNegLn2HiN, -y));   // 2 r
+    const int ki = (int)(uint32_t)__double_as_longlong(kdm);
+    const double2 t = htab[ki & 63];                         // (t.x / 2, t.y)
+    const double r2 = r * r;                                 // 4 r^2
+    const double c45 = fma_kk(r, (1.0 / 120.0) / 16.0, (1.0 / 24.0) / 8.0);       // c45 / 8
+    const double c23 = fma_kk(r, (1.0 / 6.0) / 4.0, 0.25);                        // c23 / 2
+    const double p = fma(r2, fma(r2, c45, c23), r);          // 2 p
+    const double v = fma(t.x, 2.0, fma(t.x, p, t.y));        // t.x + fma(t.x, p, t.y)
+    const double e = ldexp(v, ki >> 6);
+    if (NONPOS) return (y > 1492.0) ? 0.0 : e;
+    return (y > 1492.0) ? 0.0 : (y < -1420.0 ? __builtin_inf() : e);
+}
+
 // ---- sqrt of a non-negative, non-subnormal argument ----------------------
 // v_rsq_f64 seed and the Goldschmidt/Newton refinement of the device library's
 // sqrt (without its subnormal scaling); sqrt(0) = 0.

@@ -708,22 +708,22 @@ __device__ __forceinline__ double ref_q(const double xn, const double yn, const 
                                         const double cp, const double lx, const double ly,
                                         const double zx, const double zy, const LikConst& lc);
 
-// TAB: exp from the LDS table etab (product mode; exp_tab) instead of
-// exp_lean.  Without rho, q >= 0 (a sum of two rounded non-negative
-// quotients), so the argument is never positive.
+// TAB: exp from the LDS table htab (product mode; exp_nhalf: the bits of
+// exp_tab(-y/2), the table's values halved) instead of exp_lean.  Without
+// rho, q >= 0 (a sum of two rounded non-negative quotients), so the argument
+// is never positive.
 template <bool TAB = false>
 __device__ __forceinline__ double ref_factor(const double xn, const double yn, const double sp,
                                              const double cp, const double lx, const double ly,
                                              const double zx, const double zy, const LikConst& lc,
-                                             const double2* etab = nullptr) {
+                                             const double2* htab = nullptr) {
     const double q = ref_q(xn, yn, sp, cp, lx, ly, zx, zy, lc);
     double e;
     if (lc.has_rho) {
         const double a = (-q) / lc.d2;
-        e = TAB ? exp_tab<false>(a, etab) : exp_lean(a);
+        e = TAB ? exp_nhalf<false>(-2.0 * a, htab) : exp_lean(a);   // -2a exact: a's bits
     } else {
-        const double a = (-q) * 0.5;                            // d2 == 2 exactly
-        e = TAB ? exp_tab<true>(a, etab) : exp_lean(a);
+        e = TAB ? exp_nhalf<true>(q, htab) : exp_lean((-q) * 0.5);   // d2 == 2 exactly
     }
     return div_refined(e, lc.den, lc.rden);
 }
@@ -850,9 +850,13 @@ __device__ __forceinline__ int likelihood_lanes(const double* xn, const double* 
                                                  double* bn, const int wave_s) {
     const int nl = lc.nl;
     if (LIK == SLAM_LIK_PRODUCT) {
-        // the exp table in LDS (every lane of the block reaches this barrier)
+        // the exp table in LDS, t.x halved for exp_nhalf (every lane of the
+        // block reaches this barrier)
         __shared__ double2 s_etab[64];
-        if (threadIdx.x < 64) s_etab[threadIdx.x] = kExpTab64[threadIdx.x];
+        if (threadIdx.x < 64) {
+            const double2 t = kExpTab64[threadIdx.x];
+            s_etab[threadIdx.x] = make_double2(t.x * 0.5, t.y);
+        }
         __syncthreads();
         double acc[P];
 #pragma unroll
