@@ -275,8 +275,13 @@ __device__ __forceinline__ double exp_nhalf(const double y, const double2* __res
     const int ki = (int)(uint32_t)__double_as_longlong(kdm);
     const double2 t = htab[ki & 63];                         // (t.x / 2, t.y)
     const double r2 = r * r;                                 // 4 r^2
-    const double c45 = fma_kk(r, (1.0 / 120.0) / 16.0, (1.0 / 24.0) / 8.0);       // c45 / 8
-    const double c23 = fma_kk(r, (1.0 / 6.0) / 4.0, 0.25);                        // c23 / 2
+    // c45's addend from a VGPR (the asm hides the constant: hoisted out of the
+    // loop, one v_fma instead of v_mov_b64 + v_fmac); c23's is an inline constant
+    double k24 = (1.0 / 24.0) / 8.0;
+    asm("" : "+v"(k24));
+    double c45;                                                                   // c45 / 8
+    asm("v_fma_f64 %0, %1, %2, %3" : "=v"(c45) : "v"(r), "s"((1.0 / 120.0) / 16.0), "v"(k24));
+    const double c23 = fma(r, (1.0 / 6.0) / 4.0, 0.25);                           // c23 / 2
     const double p = fma(r2, fma(r2, c45, c23), r);          // 2 p
     const double v = fma(t.x, 2.0, fma(t.x, p, t.y));        // t.x + fma(t.x, p, t.y)
     const double e = ldexp(v, ki >> 6);

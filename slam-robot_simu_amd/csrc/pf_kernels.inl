@@ -704,6 +704,7 @@ __device__ void closed_prep_block(const double* __restrict__ lm, const double* _
 
 // One landmark factor in the reference's rounding order
 // (particle_filter.py:187-191: mylib/transform.py:31-35 then mlab.bivariate_normal).
+template <int RHO = -1>
 __device__ __forceinline__ double ref_q(const double xn, const double yn, const double sp,
                                         const double cp, const double lx, const double ly,
                                         const double zx, const double zy, const LikConst& lc);
@@ -712,14 +713,16 @@ __device__ __forceinline__ double ref_q(const double xn, const double yn, const 
 // exp_tab(-y/2), the table's values halved) instead of exp_lean.  Without
 // rho, q >= 0 (a sum of two rounded non-negative quotients), so the argument
 // is never positive.
-template <bool TAB = false>
+// RHO: 1 / 0 when the caller has hoisted the lc.has_rho test out of its loop.
+template <bool TAB = false, int RHO = -1>
 __device__ __forceinline__ double ref_factor(const double xn, const double yn, const double sp,
                                              const double cp, const double lx, const double ly,
                                              const double zx, const double zy, const LikConst& lc,
                                              const double2* htab = nullptr) {
-    const double q = ref_q(xn, yn, sp, cp, lx, ly, zx, zy, lc);
+    const bool rho = RHO < 0 ? lc.has_rho : RHO > 0;
+    const double q = ref_q<RHO>(xn, yn, sp, cp, lx, ly, zx, zy, lc);
     double e;
-    if (lc.has_rho) {
+    if (rho) {
         const double a = (-q) / lc.d2;
         e = TAB ? exp_nhalf<false>(-2.0 * a, htab) : exp_lean(a);   // -2a exact: a's bits
     } else {
@@ -740,6 +743,7 @@ __device__ __forceinline__ double ref_factor(const double xn, const double yn, c
 // ~1e-13 of the reference's normal-range partial product even for particles
 // metres off every landmark (|s| ~ 700, where a plain fp64 chain of 100 sums
 // is off by ~5e-12).
+template <int RHO>
 __device__ __forceinline__ double ref_q(const double xn, const double yn, const double sp,
                                         const double cp, const double lx, const double ly,
                                         const double zx, const double zy, const LikConst& lc) {
@@ -750,7 +754,7 @@ __device__ __forceinline__ double ref_q(const double xn, const double yn, const 
     const double dx = rx - zx;
     const double dy = ry - zy;
     double q = div_refined(dx * dx, lc.sx2, lc.rsx2) + div_refined(dy * dy, lc.sy2, lc.rsy2);
-    if (lc.has_rho) q = q - ((lc.rho2 * dx) * dy) / lc.sxsy;
+    if (RHO < 0 ? lc.has_rho : RHO > 0) q = q - ((lc.rho2 * dx) * dy) / lc.sxsy;
     return q;
 }
 
@@ -861,12 +865,18 @@ __device__ __forceinline__ int likelihood_lanes(const double* xn, const double* 
         double acc[P];
 #pragma unroll
         for (int k = 0; k < P; ++k) acc[k] = 1.0;
-        for (int j = 0; j < nl; ++j) {
-            const double lx = lm[2 * j], ly = lm[2 * j + 1], zx = z[2 * j], zy = z[2 * j + 1];
+        // the rho test hoisted: the P particles' chains interleave in one block
+        auto walk = [&](auto rho) {
+            for (int j = 0; j < nl; ++j) {
+                const double lx = lm[2 * j], ly = lm[2 * j + 1], zx = z[2 * j], zy = z[2 * j + 1];
 #pragma unroll
-            for (int k = 0; k < P; ++k)
-                acc[k] = acc[k] * ref_factor<true>(xn[k], yn[k], sp[k], cp[k], lx, ly, zx, zy, lc, s_etab);
-        }
+                for (int k = 0; k < P; ++k)
+                    acc[k] = acc[k] * ref_factor<true, decltype(rho)::value>(xn[k], yn[k], sp[k], cp[k], lx,
+                                                                            ly, zx, zy, lc, s_etab);
+            }
+        };
+        if (lc.has_rho) walk(std::integral_constant<int, 1>{});
+        else walk(std::integral_constant<int, 0>{});
 #pragma unroll
         for (int k = 0; k < P; ++k) bn[k] = acc[k];
         return 0;

@@ -8,4 +8,4 @@ mkdir -p $out
 timeout -k 10 400 python -u -m pytest tests/test_gpu_pf.py tests/test_gpu_c2.py tests/test_gpu_closed_form.py -m gpu -x -q --timeout 300 --timeout-method thread -k "product or exp" > $out/pytest.log 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -3 $out/pytest.log; [ $rc -eq 0 ] || exit $rc
 export VB_LIK=product
-bash tools/ab.sh ${1:-r4p} 3 libslam_hip.so libslam_prodold.so
+bash tools/ab.sh ${1:-r4p} 3 libslam_hip.so libslam_prodnh.so
