@@ -452,6 +452,36 @@ int cond_enqueue(slam_graph* h, int32_t k0, int32_t count) {
     const double tol = h->cfg.cond_tol > 0.0 ? h->cfg.cond_tol : 1e-5;
     const int32_t mx = h->cfg.cond_max_iter > 0 ? h->cfg.cond_max_iter : 3000;
     int32_t k = k0;
+    // merged (default): the SpMV launch's last workgroup folds and decides
+    // the iteration (two launches per iteration); SLAM_GRAPH_COND_MERGED=0
+    // keeps the separate one-workgroup fold launch (same totals, A/B)
+    static const bool merged = [] {
+        const char* e = std::getenv("SLAM_GRAPH_COND_MERGED");
+        return !(e && e[0] == '0');
+    }();
+    if (merged) {
+        if (k0 == 0) {
+            hipLaunchKernelGGL(graph_cond_init_kernel, dim3(nblk(2 * n)), dim3(256), 0, s, n,
+                               h->cond_warm ? 0 : 1, h->cx, h->cp, h->chp, h->cst);
+            hipLaunchKernelGGL((graph_cond_spmv_kernel<true, true>), dim3(nb), dim3(kSpmvThreads), 0, s,
+                               h->nt, h->rptr, h->scol, h->val, h->cx, h->chx, h->cw, h->cw2, h->chw,
+                               h->cp, h->chp, h->cpart, h->cst, 0, tol, mx, h->cfg.cond_max);
+            hipLaunchKernelGGL(graph_cond_update_kernel, dim3(nb), dim3(kPcgThreads), 0, s, n, 0,
+                               h->minv, h->cx, h->chx, h->cw2, h->chw, h->cp, h->chp, h->cw,
+                               h->cpart, h->cst);
+            k = 1;
+        }
+        for (; k < k0 + count; ++k) {
+            hipLaunchKernelGGL((graph_cond_spmv_kernel<false, true>), dim3(nb), dim3(kSpmvThreads), 0,
+                               s, h->nt, h->rptr, h->scol, h->val, h->cx, h->chx, h->cw, h->cw2,
+                               h->chw, h->cp, h->chp, h->cpart, h->cst, k, tol, mx, h->cfg.cond_max);
+            hipLaunchKernelGGL(graph_cond_update_kernel, dim3(nb), dim3(kPcgThreads), 0, s, n, k,
+                               h->minv, h->cx, h->chx, h->cw2, h->chw, h->cp, h->chp, h->cw,
+                               h->cpart, h->cst);
+        }
+        SLAM_HIP_TRY(hipGetLastError());
+        return SLAM_OK;
+    }
     if (k0 == 0) {
         hipLaunchKernelGGL(graph_cond_init_kernel, dim3(nblk(2 * n)), dim3(256), 0, s, n,
                            h->cond_warm ? 0 : 1, h->cx, h->cp, h->chp, h->cst);
@@ -510,23 +540,32 @@ int solve_pcg(slam_graph* h, double* stats, bool* solved, int32_t* iters) {
     bool pcg_done = false, cond_done = !est, abandoned = false;
     int32_t k0 = 0, c0 = 0;
     while (!pcg_done || !cond_done) {
-        if (!pcg_done) {
-            for (int32_t k = k0; k < k_end; ++k) {
+        // the two streams' launches interleaved in proportion to their batch
+        // lengths, so the estimate starts with the solve instead of after the
+        // host has enqueued the whole PCG batch (~1 ms of launch calls)
+        const int32_t np = pcg_done ? 0 : k_end - k0;
+        const int32_t nc = cond_done ? 0 : c_end - c0;
+        for (int32_t ip = 0, ic = 0; ip < np || ic < nc;) {
+            if (ic < nc && (ip >= np || (int64_t)ic * np <= (int64_t)ip * nc)) {
+                GTRY(cond_enqueue(h, c0 + ic, 1));
+                ++ic;
+            } else {
+                const int32_t k = k0 + ip;
                 hipLaunchKernelGGL(graph_pcg_dir_spmv_kernel, dim3(nb), dim3(kSpmvThreads), 0,
                                    h->stream, h->nt, k, h->rptr, h->scol, h->val, h->z, h->p, h->q,
                                    h->part, h->st, h->cfg.pcg_tol, h->cfg.pcg_max_iter);
                 hipLaunchKernelGGL(graph_pcg_step_kernel, dim3(nb), dim3(kPcgThreads), 0, h->stream,
                                    n, k, h->minv, h->p, h->q, h->delta, h->r, h->z, h->part, h->st);
+                ++ip;
             }
-            SLAM_HIP_TRY(hipGetLastError());
+        }
+        SLAM_HIP_TRY(hipGetLastError());
+        if (!pcg_done)
             SLAM_HIP_TRY(hipMemcpyAsync(h->pcg_host, h->st, sizeof(PcgState), hipMemcpyDeviceToHost,
                                         h->stream));
-        }
-        if (!cond_done) {
-            GTRY(cond_enqueue(h, c0, c_end - c0));
+        if (!cond_done)
             SLAM_HIP_TRY(hipMemcpyAsync(h->cond_host, h->cst, sizeof(CondState), hipMemcpyDeviceToHost,
                                         h->cstream));
-        }
         if (!pcg_done) {
             SLAM_HIP_TRY(hipStreamSynchronize(h->stream));
             pcg_done = s.done;

@@ -873,7 +873,33 @@ struct CondState {
     double lam[2];                // the latest Ritz values (min side, max side)
     double coef[2][4];            // this iteration's update of each side: c0, c1, c2, 1 / |p'|
     int32_t iter, done, status, iters_side[2], conv[2], upd[2], pad;
+    // merged mode: the SpMV launch's arrival tickets -- one 128-byte line per
+    // residue class blockIdx % 8 (one XCD under round-robin dispatch), the
+    // classes' last arrivers on line 0; each word re-zeroed by its last arriver
+    alignas(128) uint32_t tk[9 * 32];
 };
+
+// last-arriver election over write-through partials (the particle filter's
+// arrive_last_n): the storing waves drain, one lane takes an agent-scope
+// ticket; no fence (an agent-scope fence writes back the XCD's L2)
+__device__ __forceinline__ bool cond_arrive_n(uint32_t* counter, const uint32_t expected) {
+    __shared__ int last;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const uint32_t t = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        last = (t == expected - 1) ? 1 : 0;
+        if (last) __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    return last != 0;
+}
+__device__ __forceinline__ bool cond_arrive_last(uint32_t* tk) {
+    const int G = gridDim.x < 8 ? (int)gridDim.x : 8, g = blockIdx.x % G;
+    const uint32_t ng = (gridDim.x - g + G - 1) / G;
+    if (!cond_arrive_n(tk + (1 + g) * 32, ng)) return false;
+    return cond_arrive_n(tk, (uint32_t)G);
+}
 
 __device__ __forceinline__ uint64_t cond_mix64(uint64_t z) {
     z += 0x9E3779B97F4A7C15ULL;
@@ -1051,6 +1077,7 @@ __global__ __launch_bounds__(256) void graph_cond_init_kernel(const int64_t n, c
         st->conv[0] = st->conv[1] = 0;
         st->iters_side[0] = st->iters_side[1] = 0;
     }
+    for (int64_t t = i; t < 9 * 32; t += (int64_t)gridDim.x * 256) st->tk[t] = 0;
     if (i >= 2 * n) return;
     if (cold) x[i] = (double)(int64_t)(cond_mix64((uint64_t)i) >> 11) * 0x1.0p-52 - 1.0;
     p[i] = 0.0;
@@ -1085,14 +1112,24 @@ __device__ __forceinline__ void cond_block_dot2(const int64_t s, const int64_t* 
 // partials.  part: [24][nb] Gram, then [2][nb] x.w.  The 24 products of each
 // of the workgroup's 192 rows go through LDS and are summed in a fixed order
 // (three per wave: lanes take three rows each, then the xor butterfly).
+template <int NT, bool WT>
+__device__ __forceinline__ void cond_fold_body(const int64_t nb, const double* __restrict__ part,
+                                               CondState* __restrict__ st, const int32_t k,
+                                               const double tol, const int32_t max_iter,
+                                               const double cond_max);
+
+// FOLD (merged mode): the workgroup arriving last at the state's ticket also
+// folds the launch's partials and decides iteration k (cond_fold_body), so an
+// iteration is two launches instead of three.
 constexpr int kCondRows = kSpmvThreads / kSpmvGroup * 3;   // 192 rows per workgroup
-template <bool START>
+template <bool START, bool FOLD = false>
 __global__ __launch_bounds__(kSpmvThreads) void graph_cond_spmv_kernel(
     const int64_t nt, const int64_t* __restrict__ rptr, const int64_t* __restrict__ col,
     const double* __restrict__ val, const double* __restrict__ x, double* __restrict__ hx,
     const double* __restrict__ w, double* __restrict__ w2, double* __restrict__ hw,
     const double* __restrict__ p, const double* __restrict__ hp, double* __restrict__ part,
-    const CondState* __restrict__ st) {
+    CondState* __restrict__ st, const int32_t k = 0, const double tol = 0.0,
+    const int32_t max_iter = 0, const double cond_max = 0.0) {
     __shared__ double s_prod[2 * kCondGram][kCondRows];
     __shared__ double sh[2 * kSpmvThreads / 64];
     if (!START && st->done) return;
@@ -1176,7 +1213,18 @@ __global__ __launch_bounds__(kSpmvThreads) void graph_cond_spmv_kernel(
         v += s_prod[j][lane + 128];
 #pragma unroll
         for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
-        if (lane == 0) part[j * nb + blockIdx.x] = v;
+        if (lane == 0) {
+            if constexpr (FOLD)                  // write-through: read by the last arriver
+                __hip_atomic_store((uint64_t*)(part + j * nb + blockIdx.x),
+                                   (uint64_t)__double_as_longlong(v), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+            else
+                part[j * nb + blockIdx.x] = v;
+        }
+    }
+    if constexpr (FOLD) {
+        if (!cond_arrive_last(st->tk)) return;
+        cond_fold_body<kSpmvThreads, true>(nb, part, st, k, tol, max_iter, cond_max);
     }
 }
 static_assert(kSpmvThreads / 64 * 3 == 2 * kCondGram, "three Gram quantities per wave");
@@ -1186,32 +1234,58 @@ static_assert(kSpmvThreads / 64 * 3 == 2 * kCondGram, "three Gram quantities per
 // two small problems (one lane each, on different waves), the stopping tests
 // and this iteration's update coefficients into the state; the update launch
 // only applies them.  k = 0: x normalised, theta its Rayleigh quotient.
-constexpr int kCondFoldThreads = 1024;
-__global__ __launch_bounds__(kCondFoldThreads) void graph_cond_fold_kernel(
-    const int64_t nb, const double* __restrict__ part, CondState* __restrict__ st, const int32_t k,
-    const double tol, const int32_t max_iter, const double cond_max) {
+// The fold itself, by a workgroup of NT threads: row j by wave j % (NT / 64),
+// each lane summing its strided entries four at a time (missing terms add
+// +0.0: the order of the plain loop), the rows of a wave loaded together,
+// then the xor butterfly -- the same totals whichever workgroup size folds.
+// WT: the partials were stored by other workgroups of the same launch (the
+// merged mode's last arriving workgroup): read them with agent-scope loads.
+template <int NT, bool WT>
+__device__ __forceinline__ void cond_fold_body(const int64_t nb, const double* __restrict__ part,
+                                               CondState* __restrict__ st, const int32_t k,
+                                               const double tol, const int32_t max_iter,
+                                               const double cond_max) {
+    constexpr int NW = NT / 64, RPW = (2 * kCondGram + NW - 1) / NW;
     __shared__ double s_tot[2 * kCondGram];
     __shared__ int s_conv[2];
-    if (st->done) return;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    for (int j = wave; j < 2 * kCondGram; j += kCondFoldThreads / 64) {
-        // lane-strided sequential sums, four loads in flight (missing terms
-        // add +0.0: the order of the plain loop)
-        double v = 0.0;
-        const double* pj = part + j * nb;
-        for (int64_t q = lane; q < nb; q += 4 * 64) {
-            const double v0 = pj[q];
-            const double v1 = (q + 64 < nb) ? pj[q + 64] : 0.0;
-            const double v2 = (q + 128 < nb) ? pj[q + 128] : 0.0;
-            const double v3 = (q + 192 < nb) ? pj[q + 192] : 0.0;
-            v += v0;
-            v += v1;
-            v += v2;
-            v += v3;
+    auto ld = [&](const double* a) {
+        if constexpr (WT)
+            return __longlong_as_double((long long)__hip_atomic_load(
+                (const uint64_t*)a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        else
+            return *a;
+    };
+    double v[RPW];
+#pragma unroll
+    for (int r = 0; r < RPW; ++r) v[r] = 0.0;
+    for (int64_t q = lane; q < nb; q += 4 * 64) {
+        double a[RPW][4];
+#pragma unroll
+        for (int r = 0; r < RPW; ++r) {
+            const int j = wave + r * NW;
+            const double* pj = part + (j < 2 * kCondGram ? j : 0) * nb;
+            const bool ok = j < 2 * kCondGram;
+            a[r][0] = ok ? ld(pj + q) : 0.0;
+            a[r][1] = (ok && q + 64 < nb) ? ld(pj + q + 64) : 0.0;
+            a[r][2] = (ok && q + 128 < nb) ? ld(pj + q + 128) : 0.0;
+            a[r][3] = (ok && q + 192 < nb) ? ld(pj + q + 192) : 0.0;
         }
 #pragma unroll
-        for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
-        if (lane == 0) s_tot[j] = v;
+        for (int r = 0; r < RPW; ++r) {
+            v[r] += a[r][0];
+            v[r] += a[r][1];
+            v[r] += a[r][2];
+            v[r] += a[r][3];
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < RPW; ++r) {
+        const int j = wave + r * NW;
+        double t = v[r];
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) t += __shfl_xor(t, d, 64);
+        if (lane == 0 && j < 2 * kCondGram) s_tot[j] = t;
     }
     __syncthreads();
     if (lane == 0 && wave < 2) {
@@ -1264,6 +1338,14 @@ __global__ __launch_bounds__(kCondFoldThreads) void graph_cond_fold_kernel(
         st->status = status;
         st->done = status != 0;
     }
+}
+
+constexpr int kCondFoldThreads = 1024;
+__global__ __launch_bounds__(kCondFoldThreads) void graph_cond_fold_kernel(
+    const int64_t nb, const double* __restrict__ part, CondState* __restrict__ st, const int32_t k,
+    const double tol, const int32_t max_iter, const double cond_max) {
+    if (st->done) return;
+    cond_fold_body<kCondFoldThreads, false>(nb, part, st, k, tol, max_iter, cond_max);
 }
 
 // Applies the fold launch's coefficients to the own rows (x, Hx, p, Hp of each
