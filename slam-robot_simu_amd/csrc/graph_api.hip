@@ -442,6 +442,16 @@ int solve_dense(slam_graph* h, double* stats, bool* solved) {
     return SLAM_OK;
 }
 
+// the estimate's stall window (kCondWin; SLAM_GRAPH_COND_WIN 2..32 for A/B)
+static int cond_win() {
+    static const int w = [] {
+        const char* e = std::getenv("SLAM_GRAPH_COND_WIN");
+        const int v = e ? std::atoi(e) : 0;
+        return (v >= 2 && v <= 32) ? v : kCondWin;
+    }();
+    return w;
+}
+
 // condition-number estimate (graph_kernels.inl: LOBPCG for the extreme
 // eigenvalues) on h->cstream, enqueued in batches of `count` iterations
 // starting at iteration k0 (k0 = 0: the start sequence first).
@@ -462,7 +472,7 @@ int cond_enqueue(slam_graph* h, int32_t k0, int32_t count) {
     if (merged) {
         if (k0 == 0) {
             hipLaunchKernelGGL(graph_cond_init_kernel, dim3(nblk(2 * n)), dim3(256), 0, s, n,
-                               h->cond_warm ? 0 : 1, h->cx, h->cp, h->chp, h->cst);
+                               h->cond_warm ? 0 : 1, cond_win(), h->cx, h->cp, h->chp, h->cst);
             hipLaunchKernelGGL((graph_cond_spmv_kernel<true, true>), dim3(nb), dim3(kSpmvThreads), 0, s,
                                h->nt, h->rptr, h->scol, h->val, h->cx, h->chx, h->cw, h->cw2, h->chw,
                                h->cp, h->chp, h->cpart, h->cst, 0, tol, mx, h->cfg.cond_max);
@@ -484,7 +494,7 @@ int cond_enqueue(slam_graph* h, int32_t k0, int32_t count) {
     }
     if (k0 == 0) {
         hipLaunchKernelGGL(graph_cond_init_kernel, dim3(nblk(2 * n)), dim3(256), 0, s, n,
-                           h->cond_warm ? 0 : 1, h->cx, h->cp, h->chp, h->cst);
+                           h->cond_warm ? 0 : 1, cond_win(), h->cx, h->cp, h->chp, h->cst);
         hipLaunchKernelGGL(graph_cond_spmv_kernel<true>, dim3(nb), dim3(kSpmvThreads), 0, s, h->nt,
                            h->rptr, h->scol, h->val, h->cx, h->chx, h->cw, h->cw2, h->chw, h->cp,
                            h->chp, h->cpart, h->cst);
@@ -536,7 +546,7 @@ int solve_pcg(slam_graph* h, double* stats, bool* solved, int32_t* iters) {
     // Gauss-Newton steps of one edge set converge in similar counts), so a
     // repeated solve usually needs a single host poll; then batches of 8.
     int32_t k_end = std::max<int32_t>(16, std::min<int32_t>(h->pcg_last_iters + 1, 1024));
-    int32_t c_end = std::max<int32_t>(kCondWin + 1, std::min<int32_t>(h->cond_last_iters + 1, 1024));
+    int32_t c_end = std::max<int32_t>(cond_win() + 1, std::min<int32_t>(h->cond_last_iters + 1, 1024));
     bool pcg_done = false, cond_done = !est, abandoned = false;
     int32_t k0 = 0, c0 = 0;
     while (!pcg_done || !cond_done) {

@@ -872,7 +872,7 @@ struct CondState {
     double tot[2 * kCondGram];    // the fold launch's totals
     double lam[2];                // the latest Ritz values (min side, max side)
     double coef[2][4];            // this iteration's update of each side: c0, c1, c2, 1 / |p'|
-    int32_t iter, done, status, iters_side[2], conv[2], upd[2], pad;
+    int32_t iter, done, status, iters_side[2], conv[2], upd[2], win;   // win: the stall window
     // merged mode: the SpMV launch's arrival tickets -- one 128-byte line per
     // residue class blockIdx % 8 (one XCD under round-robin dispatch), the
     // classes' last arrivers on line 0; each word re-zeroed by its last arriver
@@ -1065,6 +1065,7 @@ __device__ __forceinline__ bool cond_small(const double* g, const double* a, con
 
 // random start (cold) or the previous update's vectors (warm); p = Hp = 0
 __global__ __launch_bounds__(256) void graph_cond_init_kernel(const int64_t n, const int cold,
+                                                              const int win,
                                                               double* __restrict__ x,
                                                               double* __restrict__ p,
                                                               double* __restrict__ hp,
@@ -1076,6 +1077,7 @@ __global__ __launch_bounds__(256) void graph_cond_init_kernel(const int64_t n, c
         st->status = 0;
         st->conv[0] = st->conv[1] = 0;
         st->iters_side[0] = st->iters_side[1] = 0;
+        st->win = win;
     }
     for (int64_t t = i; t < 9 * 32; t += (int64_t)gridDim.x * 256) st->tk[t] = 0;
     if (i >= 2 * n) return;
@@ -1311,8 +1313,9 @@ __device__ __forceinline__ void cond_fold_body(const int64_t nb, const double* _
                 c2 = c[2];
                 pinv = (pn > 0.0) ? 1.0 / pn : 0.0;
                 upd = 1;
-                const double old = st->theta[sd][(k - kCondWin) & (kCondHist - 1)];
-                if (k >= kCondWin && fabs(old - theta) <= tol * fabs(theta)) conv = 1;
+                const int win = st->win;
+                const double old = st->theta[sd][(k - win) & (kCondHist - 1)];
+                if (k >= win && fabs(old - theta) <= tol * fabs(theta)) conv = 1;
                 st->iters_side[sd] = k;
             }
         }
