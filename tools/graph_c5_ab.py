@@ -1,6 +1,6 @@
 """Graph C5 Gauss-Newton iteration with the gate's cond estimate (development
-probe): bench.bench_graph's numbers, one line per run (SLAM_GRAPH_FUSED picks
-the estimate's shared launches or its own stream)."""
+probe): bench.bench_graph's numbers, one line per run (round 4: the label's
+SLAM_GRAPH_FUSED selected a fused-launch variant that was measured and not kept)."""
 import os
 import sys
 
