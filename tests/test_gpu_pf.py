@@ -68,6 +68,26 @@ def test_likelihood_stage(slamhip_pf, tag, lik):
     assert out["max_idx"] == int(np.argmax(ref))
 
 
+@pytest.mark.parametrize("lik", ["product", "logsum"])
+def test_likelihood_stage_correlated_r(slamhip_pf, lik):
+    """particle_filter.py:179-191 with a non-zero R01: sigmaxy = sqrt(R01) reaches
+    mlab.bivariate_normal's rho term (the device's has_rho path, exp(-q / d2)).
+    Stage "a" inputs; oracle pf_oracle.likelihood (gauss2d, the published
+    formula); identical zero sets and <= 1e-12 relative (A6's bar)."""
+    g = golden("pf_stages")
+    px, pw = g["lik_a_px"], g["lik_a_pw"]
+    lm, z = g["lik_a_lm"], g["lik_a_z"]
+    r = np.array([[0.09, 0.0025], [0.0025, 0.09]])            # rho = 0.05 / 0.09
+    ref, _ = po.likelihood(px[0], px[1], px[2], pw, lm, z, r)
+    with slamhip_pf.DeviceParticleFilter(pw.size, lm, r=r, likelihood=lik) as d:
+        d.set_state(px[0], px[1], px[2], pw)
+        out = d.update(z)
+        _, _, _, w = d.get_state()
+    worst = weights_match(w, ref, rtol=1e-12)
+    print(f"correlated R {lik}: max relative weight error {worst:.3g}")
+    assert out["max_idx"] == int(np.argmax(ref))
+
+
 @pytest.mark.parametrize("tag", ["a", "b", "c"])
 def test_predict_linear_stage(slamhip_pf, tag):
     g = golden("pf_stages")

@@ -10,7 +10,7 @@ from slamhip.graph import DeviceGraph, circle_graph  # noqa: E402
 init, truth, edges = circle_graph(50000, n_landmarks=64, seed=0, odom_noise=0.002)
 dev = DeviceGraph(solver="pcg", pcg_tol=1e-10)
 dev.set_poses(init)
-for k in range(6):
+for k in range(int(os.environ.get("PROBE_CALLS", "6"))):
     t0 = time.perf_counter()
     dev.set_edges(edges)
     print(f"set_edges {k}: {(time.perf_counter() - t0) * 1e3:.3f} ms", flush=True)
