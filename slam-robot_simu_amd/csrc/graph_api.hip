@@ -54,6 +54,8 @@ struct slam_graph {
     double *cx = nullptr, *chx = nullptr, *cp = nullptr, *chp = nullptr;
     double *cw = nullptr, *cw2 = nullptr, *chw = nullptr, *cpart = nullptr;
     CondState* cst = nullptr;
+    int64_t* cnt_host = nullptr;   // pinned: the structure build's two counts, then its times
+    int64_t cnt_cap = 0;           // (a pageable read-back stalled the host ~7 ms now and then)
     PcgState* pcg_host = nullptr;  // pinned copies of the device states: the polls of the
     CondState* cond_host = nullptr;  // two streams must not block the host (pageable copies do)
     bool cond_warm = false;        // cx holds the previous update's vectors of this edge set
@@ -286,14 +288,23 @@ int build_structure_device(slam_graph* h, int64_t E, const slam_graph_edge* ed) 
         hipLaunchKernelGGL(gb_offsets_kernel, dim3(nblk(nt_ub + 1)), dim3(256), 0, s, bs.bkey_s, 2 * E,
                            bs.cnt, nt_ub + 1, h->bptr);
         SLAM_HIP_TRY(hipGetLastError());
-        int64_t cnt[2];
-        SLAM_HIP_TRY(hipMemcpyAsync(cnt, bs.cnt, sizeof(cnt), hipMemcpyDeviceToHost, s));
+        // read back through pinned memory: the counts, then the distinct times
+        const int64_t need = std::max<int64_t>(2, nt_ub);
+        if (h->cnt_cap < need) {
+            if (h->cnt_host) SLAM_HIP_TRY(hipHostFree(h->cnt_host));
+            h->cnt_host = nullptr;
+            h->cnt_cap = 0;
+            SLAM_HIP_TRY(hipHostMalloc(&h->cnt_host, (size_t)need * sizeof(int64_t)));
+            h->cnt_cap = need;
+        }
+        SLAM_HIP_TRY(hipMemcpyAsync(h->cnt_host, bs.cnt, 2 * sizeof(int64_t), hipMemcpyDeviceToHost, s));
         SLAM_HIP_TRY(hipStreamSynchronize(s));
-        h->times_h.resize(cnt[0]);
-        SLAM_HIP_TRY(hipMemcpyAsync(h->times_h.data(), h->times, cnt[0] * sizeof(int64_t),
+        const int64_t cnt[2] = {h->cnt_host[0], h->cnt_host[1]};
+        SLAM_HIP_TRY(hipMemcpyAsync(h->cnt_host, h->times, cnt[0] * sizeof(int64_t),
                                     hipMemcpyDeviceToHost, s));
         GTRY(finish_structure(h, E, cnt[0], cnt[1]));
         SLAM_HIP_TRY(hipStreamSynchronize(s));
+        h->times_h.assign(h->cnt_host, h->cnt_host + cnt[0]);
         return SLAM_OK;
     }
 rfail:
@@ -725,6 +736,7 @@ int slam_graph_destroy(slam_graph* h) {
     for (auto& e : h->cev)
         if (e) (void)hipEventDestroy(e);
     if (h->pcg_host) (void)hipHostFree(h->pcg_host);
+    if (h->cnt_host) (void)hipHostFree(h->cnt_host);
     if (h->cond_host) (void)hipHostFree(h->cond_host);
     if (h->cstream) (void)hipStreamDestroy(h->cstream);
     if (h->stream) (void)hipStreamDestroy(h->stream);
