@@ -114,6 +114,7 @@ struct slam_pf {
     bool deferred = false;
     bool scan_merged = false;   // exact cumsum in one launch (co-resident grid)
     bool scan_merged_ok = false;  // the merged launch is allowed for this handle
+    bool fused4 = true;         // one-round fused kernel (four particles per lane, pf_fused4.inl)
     double* s_cur = nullptr;
     DeferParts dp{};
     int32_t nb_part = 0;
@@ -261,12 +262,17 @@ int launch_step(slam_pf* h, bool host_noise);
 // (the even ones bring the parity back).
 int capture_steps(slam_pf* h, hipGraphExec_t& ge, int steps) {
     const int cur0 = h->cur;
+    // no timing events inside a graph: launch_step's tic / toc
+    // would record events that never run on the stream
+    const bool timing0 = h->timing;
+    h->timing = false;
     hipGraph_t g;
     SLAM_HIP_TRY(hipStreamBeginCapture(h->stream, hipStreamCaptureModeThreadLocal));
     int rc = SLAM_OK;
     for (int k = 0; k < steps && rc == SLAM_OK; ++k) rc = launch_step(h, false);
     const hipError_t e = hipStreamEndCapture(h->stream, &g);
     h->cur = cur0;
+    h->timing = timing0;
     if (rc) return rc;
     if (e != hipSuccess) return fail(SLAM_ERR_HIP, "hipStreamEndCapture failed");
     SLAM_HIP_TRY(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
@@ -321,6 +327,9 @@ int ensure_steps(slam_pf* h, int32_t steps) {
 int set_ctr(slam_pf* h, int32_t step) {
     SLAM_HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)h->ctr, step, 1, h->stream));
     SLAM_HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)(h->ctr + 1), (int)h->stepno, 1, h->stream));
+    // no batch bounds: the step end's export of a batch's records (ctr[2..3],
+    // written by slam_pf_run's setup) must not fire for this step
+    SLAM_HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)(h->ctr + 2), -1, 2, h->stream));
     return SLAM_OK;
 }
 
@@ -408,7 +417,16 @@ int launch_fused(slam_pf* h, int motion, bool host_noise) {
                                                    h->w_un, h->c, h->flags, nsrc, h->lm, io,     \
                                                    h->pc, h->lc, h->cfg.seed, h->s_cur, h->refp, \
                                                    h->dp)
-#define SLAM_FUSED(M, L, HN) SLAM_FUSED_D(M, L, HN, true)     /* every handle is deferred */
+#define SLAM_FUSED4(M, L, HN)                                                                   \
+    pf_fused4_kernel<M, L, HN><<<(unsigned)((h->nb_part + 1) / 2), 256, 0, s>>>(                   \
+        n, h->x[src], h->y[src], h->th[src], h->x[dst], h->y[dst], h->th[dst], h->w_un, h->c,    \
+        h->flags, nsrc, h->lm, io, h->pc, h->lc, h->cfg.seed, h->s_cur, h->refp, h->dp,          \
+        h->nb_part)
+#define SLAM_FUSED(M, L, HN)                                                                    \
+    do {                                                                                        \
+        if (h->fused4) SLAM_FUSED4(M, L, HN);                                                   \
+        else SLAM_FUSED_D(M, L, HN, true);     /* every handle is deferred */                   \
+    } while (0)
     if (motion == kMotionNone) {
         if (lik == SLAM_LIK_PRODUCT) SLAM_FUSED(2, 0, false); else SLAM_FUSED(2, 1, false);
     } else if (motion == SLAM_MOTION_LINEAR) {
@@ -425,6 +443,7 @@ int launch_fused(slam_pf* h, int motion, bool host_noise) {
         }
     }
 #undef SLAM_FUSED
+#undef SLAM_FUSED4
 #undef SLAM_FUSED_D
     toc(h, 0);
     h->cur = dst;
@@ -736,7 +755,8 @@ int create_impl(const slam_pf_config* cfg, int64_t n_local, int64_t n_global, in
     }
     // deferred handles: particle and weight arrays padded to whole fused blocks
     // (the fused kernel moves particle pairs with 16-byte loads and stores)
-    const int64_t npad = deferred ? (int64_t)h->nb_part * kPartPer : n;
+    // (to whole 1,024-particle blocks of the one-round kernel, pf_fused4.inl)
+    const int64_t npad = deferred ? ((int64_t)h->nb_part + 1) / 2 * kF4Block : n;
     for (int k = 0; k < 2; ++k) {
         A(h->x[k], npad);
         A(h->y[k], npad);
@@ -825,7 +845,8 @@ int create_impl(const slam_pf_config* cfg, int64_t n_local, int64_t n_global, in
     }
     SLAM_HIP_TRY(hipMemset(h->flags, 0, kFlagWords * sizeof(int32_t)));
     SLAM_HIP_TRY(hipMemset(h->tk, 0, 4 * kTicketWords * sizeof(unsigned)));
-    SLAM_HIP_TRY(hipMemset(h->ctr, 0, 4 * sizeof(int32_t)));
+    SLAM_HIP_TRY(hipMemset(h->ctr, 0, 2 * sizeof(int32_t)));
+    SLAM_HIP_TRY(hipMemsetD32((hipDeviceptr_t)(h->ctr + 2), -1, 2));   // no batch bounds yet
     if (n_landmarks > 0)
         SLAM_HIP_TRY(hipMemcpy(h->lm, landmarks, 2 * n_landmarks * sizeof(double), hipMemcpyHostToDevice));
     *out = h;
@@ -1328,6 +1349,13 @@ int slam_pf_set_scan_merged(slam_pf* h, int32_t on) {
                    "slam_pf_set_scan_merged: the merged launch needs a single-GPU handle whose "
                    "scan grid is co-resident");
     h->scan_merged = on != 0;
+    drop_graphs(h);
+    return SLAM_OK;
+}
+
+int slam_pf_set_fused_one_round(slam_pf* h, int32_t on) {
+    SLAM_ARG_CHECK(h, "slam_pf_set_fused_one_round: NULL handle");
+    h->fused4 = on != 0;
     drop_graphs(h);
     return SLAM_OK;
 }

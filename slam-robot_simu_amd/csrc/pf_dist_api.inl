@@ -331,12 +331,20 @@ int dist_capture(slam_dist* d, hipGraphExec_t& ge, int steps) {
     hipStream_t s = d->sh[0]->stream;
     std::vector<int> cur0;
     for (auto* h : d->sh) cur0.push_back(h->cur);
+    std::vector<char> timing0;                        // no timing events inside a graph
+    for (auto* h : d->sh) {
+        timing0.push_back(h->timing ? 1 : 0);
+        h->timing = false;
+    }
     hipGraph_t g;
     SLAM_HIP_TRY(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
     int rc = SLAM_OK;
     for (int k = 0; k < steps && rc == SLAM_OK; ++k) rc = dist_enqueue_step(d);
     const hipError_t e = hipStreamEndCapture(s, &g);
-    for (int i = 0; i < d->nloc; ++i) d->sh[i]->cur = cur0[i];
+    for (int i = 0; i < d->nloc; ++i) {
+        d->sh[i]->cur = cur0[i];
+        d->sh[i]->timing = timing0[i] != 0;
+    }
     if (rc) return rc;
     if (e != hipSuccess) return fail(SLAM_ERR_HIP, "slam_dist_run: hipStreamEndCapture failed");
     SLAM_HIP_TRY(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));

@@ -1357,6 +1357,8 @@ __global__ __launch_bounds__(256) SLAM_FUSED_ATTR void pf_fused_kernel(
     }
 }
 
+#include "pf_fused4.inl"
+
 // ====================================================================
 // numpy-order chunk sums (np.sum: 8192-element buffers, pairwise inside)
 // ====================================================================

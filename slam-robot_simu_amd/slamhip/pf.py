@@ -58,19 +58,30 @@ class RunResults(Sequence):
     batch's own call).  ``records`` is the same memory as a NumPy structured
     array."""
 
-    def __init__(self, res):
+    def __init__(self, res, dicts=None):
         self._r = res
+        self._d = dicts
+
+    @classmethod
+    def from_dicts(cls, dicts):
+        """Records already formed as dicts (the confirm_ess path, whose dicts
+        carry the host's ESS confirmation fields)."""
+        return cls(None, list(dicts))
 
     @property
     def records(self):
+        if self._r is None:
+            raise AttributeError("records: this batch was returned as dicts (confirm_ess)")
         return np.ctypeslib.as_array(self._r)
 
     def __len__(self):
-        return len(self._r)
+        return len(self._d) if self._d is not None else len(self._r)
 
     def __getitem__(self, i):
         if isinstance(i, slice):
             return [self[j] for j in range(*i.indices(len(self)))]
+        if self._d is not None:
+            return self._d[i]
         return DeviceParticleFilter._res(self._r[i])
 
     def __add__(self, other):
@@ -78,6 +89,27 @@ class RunResults(Sequence):
 
     def __radd__(self, other):
         return list(other) + list(self)
+
+    def __eq__(self, other):
+        """Element-wise against any sequence of records: two runs
+        compare by their records, not by identity."""
+        if not isinstance(other, Sequence) or isinstance(other, (str, bytes)):
+            return NotImplemented
+        if len(self) != len(other):
+            return False
+        for a, b in zip(self, other):
+            if a.keys() != b.keys():
+                return False
+            for k in a:
+                if not np.array_equal(a[k], b[k]):
+                    return False
+        return True
+
+    __hash__ = None
+
+    def to_list(self):
+        """The records as plain dicts (JSON-serialisable after .tolist() of the arrays)."""
+        return list(self)
 
     def __repr__(self):
         return f"RunResults({list(self)!r})"
@@ -243,9 +275,9 @@ class DeviceParticleFilter:
         self._z_steps = z_all.shape[0]
 
     def prepare_graphs(self):
-        """Capture every step graph ``run`` replays (both parities, 8-step and
-        1-step) now, so that no capture lands in a timed run; returns the
-        capture time in ms."""
+        """Capture every step graph ``run`` replays (both parities; 1-, 2-, 4-
+        and 8-step graphs) now, so that no capture lands in a timed run;
+        returns the capture time in ms."""
         ms = C.c_double(0.0)
         check(self._lib.slam_pf_prepare_graphs(self._h, C.byref(ms)), "slam_pf_prepare_graphs")
         return ms.value
@@ -276,7 +308,7 @@ class DeviceParticleFilter:
                 else:
                     out["ess_confirmed"] = False
                 outs.append(out)
-            return outs if want_results else None
+            return RunResults.from_dicts(outs) if want_results else None
         res = (PFResult * k)()
         check(self._lib.slam_pf_run(self._h, int(first_step), k, dptr(controls), res),
               "slam_pf_run")
@@ -347,6 +379,12 @@ class DeviceParticleFilter:
         """Exact cumsum of a resample step in one launch (default where the
         grid is co-resident) or two; the results are bit-identical."""
         check(self._lib.slam_pf_set_scan_merged(self._h, int(bool(on))), "slam_pf_set_scan_merged")
+
+    def set_fused_one_round(self, on=True):
+        """The fused kernel in one round of blocks (four particles per lane, the
+        default) or two particles per lane; bit-identical results."""
+        check(self._lib.slam_pf_set_fused_one_round(self._h, int(bool(on))),
+              "slam_pf_set_fused_one_round")
 
     def enable_timing(self, on=True):
         check(self._lib.slam_pf_enable_timing(self._h, int(bool(on))), "slam_pf_enable_timing")
