@@ -106,18 +106,19 @@ def _pinned_init(core):
     os.sched_setaffinity(0, {core})
 
 
-def _cpu_faithful_sample(seconds_target):
+def _cpu_faithful_sample(n_steps, n=NP_PER_GPU):
     """The oracle's faithful port (per-particle loop of particle_filter.py:185-192,
-    velocity motion model) over a bounded sample; runs in a child pinned to one core."""
+    velocity motion model) at the C2 size itself -- 1,048,576 particles x 100
+    landmarks, BASELINE.md's "time a few CPU steps" -- for n_steps whole steps
+    (~12-20 s each); runs in a child pinned to one core."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import pf_oracle as po
-    n = 1 << 15
-    lm, zs, (vel, omega, dt) = simulate_world(40, seed=2)
+    lm, zs, (vel, omega, dt) = simulate_world(max(n_steps, 1), seed=2)
     p = po.PFParams(period_ms=100, n_particles=n, landmarks=lm, motion="velocity")
     pf = po.PFOracle(p)
     rs = np.random.RandomState(0)
     steps, t_used = 0, 0.0
-    while t_used < seconds_target and steps < len(zs):
+    while steps < n_steps:
         g = rs.standard_normal(3 * n).reshape(n, 3)
         t0 = time.perf_counter()
         if pf.needs_resample():
@@ -133,17 +134,18 @@ def _cpu_faithful_sample(seconds_target):
     return n, steps, t_used, sorted(os.sched_getaffinity(0))
 
 
-def cpu_baseline(seconds_target=12.0):
+def cpu_baseline(n_steps=2):
     """The oracle's faithful port on ONE host core (the reference is
-    single-threaded Python): a spawned child pinned with sched_setaffinity
-    (taskset) to the first core this process may use, BLAS threads 1."""
+    single-threaded Python) at the C2 size: a spawned child pinned with
+    sched_setaffinity (taskset) to the first core this process may use, BLAS
+    threads 1."""
     import multiprocessing as mp
     core = min(os.sched_getaffinity(0))
     saved = {k: os.environ.get(k) for k in ("OPENBLAS_NUM_THREADS", "OMP_NUM_THREADS")}
     os.environ.update(OPENBLAS_NUM_THREADS="1", OMP_NUM_THREADS="1")
     try:
         with mp.get_context("spawn").Pool(1, initializer=_pinned_init, initargs=(core,)) as pool:
-            n, steps, t_used, cpus = pool.apply(_cpu_faithful_sample, (seconds_target,))
+            n, steps, t_used, cpus = pool.apply(_cpu_faithful_sample, (n_steps,))
     finally:
         for k, v in saved.items():
             if v is None:

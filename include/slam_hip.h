@@ -146,11 +146,6 @@ int slam_pf_prepare_graphs(slam_pf* h, double* capture_ms);
 /* Exact cumsum of a resample step in one launch (on = default where the grid
  * is co-resident; SLAM_ERR_ARG elsewhere) or in two; bit-identical results. */
 int slam_pf_set_scan_merged(slam_pf* h, int32_t on);
-/* The fused predict + likelihood kernel (particle_filter.py:156-198): on = the
- * one-round form (four particles per lane, 1,024 per block: every block
- * resident at once up to 2^20 particles; the default), off = two particles per
- * lane; bit-identical particles, weights and step records. */
-int slam_pf_set_fused_one_round(slam_pf* h, int32_t on);
 /* Overrides the resample decision of the next step (particle_filter.py:210-211,
  * `ess < ESS_TH`): the caller re-forms ESS as the reference does, `1 / (pw @ pw.T)`
  * on the host's BLAS, when the device's ESS lies within rounding of the

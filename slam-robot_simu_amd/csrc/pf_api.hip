@@ -114,7 +114,6 @@ struct slam_pf {
     bool deferred = false;
     bool scan_merged = false;   // exact cumsum in one launch (co-resident grid)
     bool scan_merged_ok = false;  // the merged launch is allowed for this handle
-    bool fused4 = true;         // one-round fused kernel (four particles per lane, pf_fused4.inl)
     double* s_cur = nullptr;
     DeferParts dp{};
     int32_t nb_part = 0;
@@ -417,16 +416,7 @@ int launch_fused(slam_pf* h, int motion, bool host_noise) {
                                                    h->w_un, h->c, h->flags, nsrc, h->lm, io,     \
                                                    h->pc, h->lc, h->cfg.seed, h->s_cur, h->refp, \
                                                    h->dp)
-#define SLAM_FUSED4(M, L, HN)                                                                   \
-    pf_fused4_kernel<M, L, HN><<<(unsigned)((h->nb_part + 1) / 2), 256, 0, s>>>(                   \
-        n, h->x[src], h->y[src], h->th[src], h->x[dst], h->y[dst], h->th[dst], h->w_un, h->c,    \
-        h->flags, nsrc, h->lm, io, h->pc, h->lc, h->cfg.seed, h->s_cur, h->refp, h->dp,          \
-        h->nb_part)
-#define SLAM_FUSED(M, L, HN)                                                                    \
-    do {                                                                                        \
-        if (h->fused4) SLAM_FUSED4(M, L, HN);                                                   \
-        else SLAM_FUSED_D(M, L, HN, true);     /* every handle is deferred */                   \
-    } while (0)
+#define SLAM_FUSED(M, L, HN) SLAM_FUSED_D(M, L, HN, true)     /* every handle is deferred */
     if (motion == kMotionNone) {
         if (lik == SLAM_LIK_PRODUCT) SLAM_FUSED(2, 0, false); else SLAM_FUSED(2, 1, false);
     } else if (motion == SLAM_MOTION_LINEAR) {
@@ -443,7 +433,6 @@ int launch_fused(slam_pf* h, int motion, bool host_noise) {
         }
     }
 #undef SLAM_FUSED
-#undef SLAM_FUSED4
 #undef SLAM_FUSED_D
     toc(h, 0);
     h->cur = dst;
@@ -755,8 +744,7 @@ int create_impl(const slam_pf_config* cfg, int64_t n_local, int64_t n_global, in
     }
     // deferred handles: particle and weight arrays padded to whole fused blocks
     // (the fused kernel moves particle pairs with 16-byte loads and stores)
-    // (to whole 1,024-particle blocks of the one-round kernel, pf_fused4.inl)
-    const int64_t npad = deferred ? ((int64_t)h->nb_part + 1) / 2 * kF4Block : n;
+    const int64_t npad = deferred ? (int64_t)h->nb_part * kPartPer : n;
     for (int k = 0; k < 2; ++k) {
         A(h->x[k], npad);
         A(h->y[k], npad);
@@ -1349,13 +1337,6 @@ int slam_pf_set_scan_merged(slam_pf* h, int32_t on) {
                    "slam_pf_set_scan_merged: the merged launch needs a single-GPU handle whose "
                    "scan grid is co-resident");
     h->scan_merged = on != 0;
-    drop_graphs(h);
-    return SLAM_OK;
-}
-
-int slam_pf_set_fused_one_round(slam_pf* h, int32_t on) {
-    SLAM_ARG_CHECK(h, "slam_pf_set_fused_one_round: NULL handle");
-    h->fused4 = on != 0;
     drop_graphs(h);
     return SLAM_OK;
 }

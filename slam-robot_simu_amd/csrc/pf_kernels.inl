@@ -356,7 +356,7 @@ __device__ __forceinline__ int64_t wave_min_i64(int64_t v) {
 __device__ void defer_epilogue(const int64_t base, const int64_t n, const double* wv,
                                const double* xv, const double* yv, const double* tv,
                                const double* __restrict__ refp, const DeferParts& dp,
-                               const int wave_s) {
+                               const int wave_s, const int blk) {
     constexpr int kQ = 11;
     constexpr int kLeaves = kPartPer / 128;
     __shared__ double s_w[kPartPer];
@@ -368,7 +368,6 @@ __device__ void defer_epilogue(const int64_t base, const int64_t n, const double
     // the thread index from the wave's SGPR index and the lane id (both
     // rematerialised: threadIdx.x itself would be held across the kernel)
     const int lane = (int)__lane_id(), wave = wave_s, t = (wave << 6) | lane;
-    const int blk = blockIdx.x;
     // lane max and its first particle, then the wave max
     double m = -1.0;
     int64_t mi = INT64_MAX;
@@ -1080,32 +1079,22 @@ __device__ __forceinline__ int likelihood_lanes(const double* xn, const double* 
 #else
 #define SLAM_FUSED_ATTR
 #endif
+// One fused block's tile (blk: 256 lanes x P particles): the body of
+// pf_fused_kernel (a persistent grid walking tiles measured slower: DESIGN 4.4).
 template <int MOTION, int LIK, bool HOSTNOISE, bool DEFER>
-__global__ __launch_bounds__(256) SLAM_FUSED_ATTR void pf_fused_kernel(
+__device__ __forceinline__ void pf_fused_tile(
+    const int64_t blk, const int32_t st, const uint32_t rstep, const int32_t rflag,
+    const double* __restrict__ zs, const int wave_s, const RngTabs& rtab,
     const int64_t n, const double* __restrict__ xs, const double* __restrict__ ys,
     const double* __restrict__ ts, double* __restrict__ xo, double* __restrict__ yo,
     double* __restrict__ to, const double* __restrict__ w_in, double* __restrict__ w_un,
     const double* __restrict__ c, int32_t* __restrict__ flags, const double* __restrict__ noise,
-    const double* __restrict__ lm, StepIO io, PredictConst pc, LikConst lc, uint64_t seed,
-    const double* __restrict__ s_in, const double* __restrict__ refp, DeferParts dp) {
-    static_assert(!DEFER || kDeferPPT % 2 == 0, "the deferred path moves particle pairs");
-    const int32_t st = io.ctr[0];
-    const uint32_t rstep = (uint32_t)io.ctr[1];
-    const int32_t rflag = flags[kFlagResample];
-    const double* __restrict__ zs = io.z + (size_t)st * 2 * (size_t)(lc.nl > 0 ? lc.nl : 1);
+    const double* __restrict__ lm, const StepIO& io, const PredictConst& pc, const LikConst& lc,
+    const uint64_t seed, const double* __restrict__ s_in, const double* __restrict__ refp,
+    const DeferParts& dp) {
     constexpr int P = DEFER ? kDeferPPT : 1;
-    const int64_t base = (int64_t)blockIdx.x * (256 * P);
+    const int64_t base = blk * (256 * P);
     const int64_t i0 = base + P * (int64_t)threadIdx.x;
-    const int wave_s = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
-    FPROBE(0, st);
-    // the device RNG's tables in LDS (every lane reaches the barrier)
-    __shared__ RngTabsLds s_rng;
-    RngTabs rtab{};
-    if constexpr (MOTION != kMotionNone && !HOSTNOISE) {
-        rtab = rng_tabs_stage(&s_rng, (int)threadIdx.x, 256);
-        __syncthreads();
-    }
-    FPROBE(1, st);
     bool valid[P];
     int64_t idx[P];
 #pragma unroll
@@ -1187,7 +1176,7 @@ __global__ __launch_bounds__(256) SLAM_FUSED_ATTR void pf_fused_kernel(
         const int32_t v = wave_max_scan_i32(r[P - 1], before);
         if (lane == 63) s_wmax[wave] = v;
         __syncthreads();
-        int32_t run = dp.carry[blockIdx.x];
+        int32_t run = dp.carry[blk];
         for (int w = 0; w < wave; ++w) run = s_wmax[w] > run ? s_wmax[w] : run;
         run = before > run ? before : run;
 #pragma unroll
@@ -1332,32 +1321,72 @@ __global__ __launch_bounds__(256) SLAM_FUSED_ATTR void pf_fused_kernel(
         for (int h = 0; h < P; h += 2)
             *reinterpret_cast<double2*>(w_un + i0 + h) = double2{wv[h], wv[h + 1]};
 #ifndef SLAM_NO_EPILOGUE
-        defer_epilogue(base, n, wv, xv, yv, tv, refp, dp, wave_s);
+        defer_epilogue(base, n, wv, xv, yv, tv, refp, dp, wave_s, (int)blk);
 #endif
         FPROBE(5, wv[0]);
-        // block 0, after its own particles: the NEXT step's closed-form words
-        // (StepIO.zc) -- its eight sums (two per wave) and its
-        // expansion about this step's refp (the estimate two steps before it)
-        // moved twice.  Off the step's critical path: the next launch reads
-        // them; a step staged by the host is prepared again by its prestep.
-        if (MOTION != kMotionNone && lc.closed && blockIdx.x == 0 && st + 1 < io.cap) {
-            __shared__ double s_prep[16];
-            const int32_t sn = st + 1;
-            closed_prep_sums(lm, io.z + (size_t)sn * 2 * lc.nl, lc.nl, wave_s, 4, s_prep);
-            __syncthreads();
-            if (threadIdx.x == 0) {
-                double px, py, pth;
-                closed_prep_reference(refp, 2, io.ctl[2 * sn], io.ctl[2 * sn + 1], pc.dt, io.motion,
-                                      px, py, pth);
-                closed_prep_constants(s_prep, lc.nl, px, py, pth, io.zc + (size_t)sn * kZcWords);
-            }
-        }
     } else if (valid[0]) {
         w_un[i0] = wv[0];
     }
 }
 
-#include "pf_fused4.inl"
+// The step's first fused block, after its own particles: the NEXT step's
+// closed-form words (StepIO.zc) -- its eight sums (two per wave)
+// and its expansion about this step's refp (the estimate two steps before it)
+// moved twice.  Off the step's critical path: the next launch reads them; a
+// step staged by the host is prepared again by its prestep.
+template <int MOTION>
+__device__ __forceinline__ void pf_fused_prep_next(const int32_t st, const int wave_s,
+                                                   const double* __restrict__ lm,
+                                                   const StepIO& io, const PredictConst& pc,
+                                                   const LikConst& lc,
+                                                   const double* __restrict__ refp) {
+    if (MOTION != kMotionNone && lc.closed && blockIdx.x == 0 && st + 1 < io.cap) {
+        __shared__ double s_prep[16];
+        const int32_t sn = st + 1;
+        closed_prep_sums(lm, io.z + (size_t)sn * 2 * lc.nl, lc.nl, wave_s, 4, s_prep);
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            double px, py, pth;
+            closed_prep_reference(refp, 2, io.ctl[2 * sn], io.ctl[2 * sn + 1], pc.dt, io.motion,
+                                  px, py, pth);
+            closed_prep_constants(s_prep, lc.nl, px, py, pth, io.zc + (size_t)sn * kZcWords);
+        }
+    }
+}
+
+#define SLAM_FUSED_PARAMS                                                                          \
+    const int64_t n, const double* __restrict__ xs, const double* __restrict__ ys,                  \
+        const double* __restrict__ ts, double* __restrict__ xo, double* __restrict__ yo,            \
+        double* __restrict__ to, const double* __restrict__ w_in, double* __restrict__ w_un,        \
+        const double* __restrict__ c, int32_t* __restrict__ flags,                                  \
+        const double* __restrict__ noise, const double* __restrict__ lm, StepIO io,                 \
+        PredictConst pc, LikConst lc, uint64_t seed, const double* __restrict__ s_in,               \
+        const double* __restrict__ refp, DeferParts dp
+#define SLAM_FUSED_ARGS n, xs, ys, ts, xo, yo, to, w_in, w_un, c, flags, noise, lm, io, pc, lc, \
+                        seed, s_in, refp, dp
+
+// The step's uniform inputs and the RNG tables (every lane reaches the barrier)
+#define SLAM_FUSED_PROLOGUE                                                                      \
+    const int32_t st = io.ctr[0];                                                                \
+    const uint32_t rstep = (uint32_t)io.ctr[1];                                                  \
+    const int32_t rflag = flags[kFlagResample];                                                  \
+    const double* __restrict__ zs = io.z + (size_t)st * 2 * (size_t)(lc.nl > 0 ? lc.nl : 1);     \
+    const int wave_s = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);                    \
+    __shared__ RngTabsLds s_rng;                                                                 \
+    RngTabs rtab{};                                                                              \
+    if constexpr (MOTION != kMotionNone && !HOSTNOISE) {                                         \
+        rtab = rng_tabs_stage(&s_rng, (int)threadIdx.x, 256);                                    \
+        __syncthreads();                                                                         \
+    }
+
+template <int MOTION, int LIK, bool HOSTNOISE, bool DEFER>
+__global__ __launch_bounds__(256) SLAM_FUSED_ATTR void pf_fused_kernel(SLAM_FUSED_PARAMS) {
+    static_assert(!DEFER || kDeferPPT % 2 == 0, "the deferred path moves particle pairs");
+    SLAM_FUSED_PROLOGUE
+    pf_fused_tile<MOTION, LIK, HOSTNOISE, DEFER>(blockIdx.x, st, rstep, rflag, zs, wave_s, rtab,
+                                                 SLAM_FUSED_ARGS);
+    if constexpr (DEFER) pf_fused_prep_next<MOTION>(st, wave_s, lm, io, pc, lc, refp);
+}
 
 // ====================================================================
 // numpy-order chunk sums (np.sum: 8192-element buffers, pairwise inside)

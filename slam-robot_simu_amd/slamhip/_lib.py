@@ -98,7 +98,6 @@ SIGNATURES = {
     "slam_pf_set_graphs": (C.c_int, [_P, C.c_int32]),
     "slam_pf_prepare_graphs": (C.c_int, [_P, _D]),
     "slam_pf_set_scan_merged": (C.c_int, [_P, C.c_int32]),
-    "slam_pf_set_fused_one_round": (C.c_int, [_P, C.c_int32]),
     "slam_pf_set_ess_band": (C.c_int, [_P, C.c_double]),
     "slam_pf_set_resample_next": (C.c_int, [_P, C.c_int32]),
     "slam_pf_set_stream": (C.c_int, [_P, _P, C.c_int32]),

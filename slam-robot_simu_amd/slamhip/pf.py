@@ -380,12 +380,6 @@ class DeviceParticleFilter:
         grid is co-resident) or two; the results are bit-identical."""
         check(self._lib.slam_pf_set_scan_merged(self._h, int(bool(on))), "slam_pf_set_scan_merged")
 
-    def set_fused_one_round(self, on=True):
-        """The fused kernel in one round of blocks (four particles per lane, the
-        default) or two particles per lane; bit-identical results."""
-        check(self._lib.slam_pf_set_fused_one_round(self._h, int(bool(on))),
-              "slam_pf_set_fused_one_round")
-
     def enable_timing(self, on=True):
         check(self._lib.slam_pf_enable_timing(self._h, int(bool(on))), "slam_pf_enable_timing")
 
