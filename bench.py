@@ -388,19 +388,27 @@ def bench_graph(n_poses=50000, iters=3, device=0):
         st = dev.update()
         per.append(time.perf_counter() - t0)
         brk.append(dev.timing())
-        conds.append(dict(dev.cond_info(), cond=st[3]))
+        conds.append(dict(dev.cond_info(), cond=st[3], det=st[2]))
+    gate = dev.gate_info()
     dev.close()
-    # the same iterations without the gate's cond estimate (cond_mode off)
-    dev = DeviceGraph(solver="pcg", pcg_tol=1e-10, cond="off", device=device)
-    dev.set_poses(init)
-    dev.set_edges(edges)
-    dev.update()
-    per_off = []
-    for _ in range(iters):
-        t0 = time.perf_counter()
-        dev.update()
-        per_off.append(time.perf_counter() - t0)
-    dev.close()
+
+    def per_iteration(cond):
+        # the same iterations with another gate mode: "off" (no gate), "estimate"
+        # (the LOBPCG estimate to its tight convergence, round 4's gate)
+        g = DeviceGraph(solver="pcg", pcg_tol=1e-10, cond=cond, device=device)
+        g.set_poses(init)
+        g.set_edges(edges)
+        g.update()
+        out = []
+        for _ in range(iters):
+            t0 = time.perf_counter()
+            g.update()
+            out.append(time.perf_counter() - t0)
+        g.close()
+        return out
+
+    per_off = per_iteration("off")
+    per_est = per_iteration("estimate")
     lin = float(np.mean([b["linearize_ms"] for b in brk])) / 1e3
     return {"workload": f"graph SLAM C5: {n_poses} poses, {len(edges)} edges, block-Jacobi PCG",
             "value": 1.0 / float(np.mean(per)), "unit": "Gauss-Newton iterations/s",
@@ -411,7 +419,11 @@ def bench_graph(n_poses=50000, iters=3, device=0):
             "breakdown_ms": brk[-1], "is_calc": bool(st[0]),
             "cond": conds[-1]["cond"], "cond_estimate": conds[-1],
             "cond_estimate_first_update": cond_first,
+            "gate": "certify (graph_based_slam.py:494-496: log-det interval + cond estimate "
+                    "with an early decision at a factor-100 margin)",
+            "gate_info": gate,
             "ms_per_iteration_without_cond": float(np.mean(per_off)) * 1e3,
+            "ms_per_iteration_estimate_gate": float(np.mean(per_est)) * 1e3,
             "linearize_edges_per_s": len(edges) / lin,
             "roofline": {"bound": "hbm", "kernel": "graph_linearize_kernel",
                          "achieved": (80 + 48 + 336) * len(edges) / lin / 1e9, "peak": HBM_PEAK_GBS,

@@ -379,11 +379,18 @@ typedef struct {
     int32_t cond_mode;    /* SLAM_GRAPH_COND_* */
 } slam_graph_config;
 
-/* The PCG path's cond (:495): SLAM_GRAPH_COND_ESTIMATE (default) estimates the
- * extreme eigenvalues of H by LOBPCG on a second stream beside the solve and
- * applies the reference's `cond < cond_max`; SLAM_GRAPH_COND_OFF skips it (cond
- * NaN, the gate is the solve's convergence alone). */
-enum { SLAM_GRAPH_COND_ESTIMATE = 0, SLAM_GRAPH_COND_OFF = 1 };
+/* The PCG path's gate (:494-496).  SLAM_GRAPH_COND_ESTIMATE: cond = the extreme
+ * eigenvalues of H by LOBPCG on a second stream beside the solve, the
+ * reference's `cond < cond_max` from a converged estimate, det not formed
+ * (NaN).  SLAM_GRAPH_COND_CERTIFY (the Python default): the same estimate
+ * stops as soon as it clears cond_max by a factor 100 (or converges with a
+ * factor 10), and the det half is decided from a log-det interval (M the
+ * block diagonal of H, P = M^-1/2 H M^-1/2: [log det M + c(a)(tr P^2 - n),
+ * log det M]); a half neither decides takes the dense path's value when n <=
+ * 2048, else the update is not solved and flagged undecided
+ * (slam_graph_gate_info).  SLAM_GRAPH_COND_OFF: no gate (cond NaN,
+ * the solve's convergence alone). */
+enum { SLAM_GRAPH_COND_ESTIMATE = 0, SLAM_GRAPH_COND_OFF = 1, SLAM_GRAPH_COND_CERTIFY = 2 };
 
 int slam_graph_create(const slam_graph_config* cfg, int device, slam_graph** out);
 int slam_graph_destroy(slam_graph* h);
@@ -425,6 +432,16 @@ int slam_graph_timing(slam_graph* h, double* out);
  * reached, 4 not positive definite), lambda_min, lambda_max, iterations of the
  * min side, of the max side, device time (ms)}.  Zeros after a dense update. */
 int slam_graph_cond_info(slam_graph* h, double* out);
+/* The last PCG-path update's certificate (SLAM_GRAPH_COND_CERTIFY): out[12] =
+ * {decided by (1 the bounds and the estimate, 2 a half by the dense path), det
+ * decision (1 passed / 0 rejected by the log-det interval, 3 / 2 by the dense
+ * LU det, -1 undecided: not solved), cond decision (1 passed / 0 rejected by
+ * the estimate, 3 / 2 by the dense Lanczos cond, -1 undecided), log det H
+ * lower bound, upper bound, cond (the value the decision used), lambda_min(H),
+ * lambda_max(H) (the estimate's Ritz values), tr(P^2), n, estimate iterations,
+ * host ms}.  Zeros after a dense update, in the other modes, and when the
+ * estimate rejected H for certain (cond_info status 2 / 4). */
+int slam_graph_gate_info(slam_graph* h, double* out);
 /* HalfEdge (graph_based_slam.py:259-300) with its Observation (:20-75). */
 typedef struct {
     int64_t time, pose, landmark;

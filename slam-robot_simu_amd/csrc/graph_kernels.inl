@@ -873,6 +873,11 @@ struct CondState {
     double lam[2];                // the latest Ritz values (min side, max side)
     double coef[2][4];            // this iteration's update of each side: c0, c1, c2, 1 / |p'|
     int32_t iter, done, status, iters_side[2], conv[2], upd[2], win;   // win: the stall window
+    // the gate's early decision (SLAM_GRAPH_COND_CERTIFY; etol 0: off): both
+    // sides moved less than etol (relative) over ewin iterations and
+    // theta_max / theta_min * emargin < cond_max -> status 5
+    double etol, emargin;
+    int32_t ewin, econv[2];
     // merged mode: the SpMV launch's arrival tickets -- one 128-byte line per
     // residue class blockIdx % 8 (one XCD under round-robin dispatch), the
     // classes' last arrivers on line 0; each word re-zeroed by its last arriver
@@ -1069,15 +1074,22 @@ __global__ __launch_bounds__(256) void graph_cond_init_kernel(const int64_t n, c
                                                               double* __restrict__ x,
                                                               double* __restrict__ p,
                                                               double* __restrict__ hp,
-                                                              CondState* __restrict__ st) {
+                                                              CondState* __restrict__ st,
+                                                              const double etol = 0.0,
+                                                              const int ewin = 0,
+                                                              const double emargin = 0.0) {
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (i == 0) {
         st->iter = 0;
         st->done = 0;
         st->status = 0;
         st->conv[0] = st->conv[1] = 0;
+        st->econv[0] = st->econv[1] = 0;
         st->iters_side[0] = st->iters_side[1] = 0;
         st->win = win;
+        st->etol = etol;
+        st->ewin = ewin;
+        st->emargin = emargin;
     }
     for (int64_t t = i; t < 9 * 32; t += (int64_t)gridDim.x * 256) st->tk[t] = 0;
     if (i >= 2 * n) return;
@@ -1316,6 +1328,10 @@ __device__ __forceinline__ void cond_fold_body(const int64_t nb, const double* _
                 const int win = st->win;
                 const double old = st->theta[sd][(k - win) & (kCondHist - 1)];
                 if (k >= win && fabs(old - theta) <= tol * fabs(theta)) conv = 1;
+                const int ew = st->ewin;
+                st->econv[sd] = st->etol > 0.0 && k >= ew &&
+                                fabs(st->theta[sd][(k - ew) & (kCondHist - 1)] - theta) <=
+                                    st->etol * fabs(theta);
                 st->iters_side[sd] = k;
             }
         }
@@ -1336,6 +1352,9 @@ __device__ __forceinline__ void cond_fold_body(const int64_t nb, const double* _
         if (!(t0 > 0.0)) status = 4;                                   // not positive definite
         else if (t1 >= cond_max * t0) status = 2;                      // cond >= cond_max for certain
         else if (s_conv[0] && s_conv[1]) status = 1;
+        else if (st->etol > 0.0 && (s_conv[0] || st->econv[0]) && (s_conv[1] || st->econv[1]) &&
+                 t1 * st->emargin < cond_max * t0)
+            status = 5;                                                // decided with a margin
         else if (k >= max_iter) status = 3;
         st->iter = k;
         st->status = status;
@@ -1463,6 +1482,131 @@ __global__ __launch_bounds__(1024) void graph_dsum_kernel(const int64_t nparts,
     for (int64_t k = threadIdx.x; k < nparts; k += 1024) s += part[k];
     s = block_sum_fixed<1024>(s, sh);
     if (threadIdx.x == 0) *dsum = s;
+}
+
+// ------------------------------------- the gate's certificate (PCG path)
+// updateEstPose :494-496 solves only if 0.1 < det(H) and cond(H) < 1e15.  At
+// config-5 size neither is formed; with M the block diagonal of H (the PCG's
+// block-Jacobi preconditioner, M_i its 3x3 blocks) and P = M^-1/2 H M^-1/2
+// (unit diagonal blocks, so tr P = n):
+//   cond(H) <= cond(P) cond(M),   cond(M) <= max_i tr(M_i) * max_i tr(M_i^-1);
+//   log det H = log det M + log det P,   log det P <= 0 (AM-GM with tr P = n),
+//   log det P >= c(a) (tr(P^2) - n)  for any a <= lambda_min(P),
+//                c(a) = (ln a - a + 1) / (a - 1)^2   (ln x >= (x - 1) + c(a)(x - 1)^2 on x >= a).
+// These kernels form the four sums the bounds need -- sum_i log det M_i,
+// tr(P^2) = sum over block slots (r, c) of tr(M_r^-1 H_rc M_c^-1 H_rc^T),
+// max tr(M_i), max tr(M_i^-1) -- one lane per pose, one lane per block slot,
+// per-workgroup partials folded by one workgroup in a fixed order.  With the
+// LOBPCG estimate of lambda_min(H) (lambda_min(P) >= lambda_min(H) / max tr M_i)
+// graph_api.hip turns them into the det decision.
+struct CertState {
+    double logdet_m, trp2, trm_max, trminv_max;
+    int32_t bad, pad;              // diagonal blocks that are not positive definite
+};
+constexpr int kCertThreads = 256;
+
+template <int NT>
+__device__ __forceinline__ double block_max_fixed(double v, double* sh) {
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) v = fmax(v, __shfl_xor(v, d, 64));
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = v;
+    __syncthreads();
+    double r = sh[0];
+    for (int w = 1; w < NT / 64; ++w) r = fmax(r, sh[w]);
+    __syncthreads();
+    return r;
+}
+
+// per pose i: log det of the symmetric part of M_i by its 3x3 Cholesky
+// pivots (log d0 + log d1 + log d2), tr(M_i), tr(M_i^-1) (the block-Jacobi
+// inverse).  part: [0, nb) log det, [nb, 2nb) bad, [2nb, 3nb) max tr M,
+// [3nb, 4nb) max tr M^-1.
+__global__ __launch_bounds__(kCertThreads) void graph_cert_pose_kernel(
+    const int64_t nt, const int64_t* __restrict__ dslot, const double* __restrict__ val,
+    const double* __restrict__ minv, double* __restrict__ part) {
+    __shared__ double sh[2 * kCertThreads / 64];
+    const int64_t nb = gridDim.x;
+    const int64_t i = (int64_t)blockIdx.x * kCertThreads + threadIdx.x;
+    double ld = 0.0, bad = 0.0, trm = 0.0, tri = 0.0;
+    if (i < nt) {
+        const double* a = val + dslot[i] * 9;
+        const double s00 = a[0], s11 = a[4], s22 = a[8];
+        const double s10 = 0.5 * (a[1] + a[3]), s20 = 0.5 * (a[2] + a[6]), s21 = 0.5 * (a[5] + a[7]);
+        const double l10 = s10 / s00, l20 = s20 / s00;
+        const double d1 = s11 - l10 * s10;
+        const double l21 = (s21 - l20 * s10) / d1;
+        const double d2 = (s22 - l20 * s20) - l21 * (s21 - l20 * s10);
+        if (s00 > 0.0 && d1 > 0.0 && d2 > 0.0) ld = log(s00) + log(d1) + log(d2);
+        else bad = 1.0;
+        trm = s00 + s11 + s22;
+        const double* m = minv + i * 9;
+        tri = m[0] + m[4] + m[8];
+    }
+    block_sum2_fixed<kCertThreads>(ld, bad, sh);
+    trm = block_max_fixed<kCertThreads>(trm, sh);
+    tri = block_max_fixed<kCertThreads>(tri, sh);
+    if (threadIdx.x == 0) {
+        part[blockIdx.x] = ld;
+        part[nb + blockIdx.x] = bad;
+        part[2 * nb + blockIdx.x] = trm;
+        part[3 * nb + blockIdx.x] = tri;
+    }
+}
+
+// per block slot s = (r, c): tr(M_r^-1 H_rc M_c^-1 H_rc^T) = ||L_r^-1 H_rc L_c^-T||_F^2
+// (the slot's share of tr(P^2)); part: one partial per workgroup
+__global__ __launch_bounds__(kCertThreads) void graph_cert_slot_kernel(
+    const int64_t n_slots, const int64_t* __restrict__ srow, const int64_t* __restrict__ scol,
+    const double* __restrict__ val, const double* __restrict__ minv, double* __restrict__ part) {
+    __shared__ double sh[kCertThreads / 64];
+    const int64_t s = (int64_t)blockIdx.x * kCertThreads + threadIdx.x;
+    double t = 0.0;
+    if (s < n_slots) {
+        const double* A = minv + srow[s] * 9;
+        const double* B = val + s * 9;
+        const double* C = minv + scol[s] * 9;
+        double X[9], Y[9];
+#pragma unroll
+        for (int r = 0; r < 3; ++r)
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+                X[3 * r + c] = fma(A[3 * r + 2], B[6 + c], fma(A[3 * r + 1], B[3 + c], A[3 * r] * B[c]));
+                Y[3 * r + c] = fma(C[3 * r + 2], B[3 * c + 2], fma(C[3 * r + 1], B[3 * c + 1], C[3 * r] * B[3 * c]));
+            }
+#pragma unroll
+        for (int r = 0; r < 3; ++r)
+#pragma unroll
+            for (int c = 0; c < 3; ++c) t = fma(X[3 * r + c], Y[3 * c + r], t);
+    }
+    t = block_sum_fixed<kCertThreads>(t, sh);
+    if (threadIdx.x == 0) part[blockIdx.x] = t;
+}
+
+// one workgroup: the partials of both kernels, fixed order -> CertState
+__global__ __launch_bounds__(kCertThreads) void graph_cert_fold_kernel(
+    const int64_t nb_pose, const double* __restrict__ ppart, const int64_t nb_slot,
+    const double* __restrict__ spart, CertState* __restrict__ out) {
+    __shared__ double sh[2 * kCertThreads / 64];
+    double ld = 0.0, bad = 0.0, trm = 0.0, tri = 0.0, t2 = 0.0;
+    for (int64_t k = threadIdx.x; k < nb_pose; k += kCertThreads) {
+        ld += ppart[k];
+        bad += ppart[nb_pose + k];
+        trm = fmax(trm, ppart[2 * nb_pose + k]);
+        tri = fmax(tri, ppart[3 * nb_pose + k]);
+    }
+    for (int64_t k = threadIdx.x; k < nb_slot; k += kCertThreads) t2 += spart[k];
+    block_sum2_fixed<kCertThreads>(ld, bad, sh);
+    t2 = block_sum_fixed<kCertThreads>(t2, sh);
+    trm = block_max_fixed<kCertThreads>(trm, sh);
+    tri = block_max_fixed<kCertThreads>(tri, sh);
+    if (threadIdx.x == 0) {
+        out->logdet_m = ld;
+        out->trp2 = t2;
+        out->trm_max = trm;
+        out->trminv_max = tri;
+        out->bad = (int32_t)bad;
+    }
 }
 
 }  // namespace slam

@@ -65,7 +65,7 @@ class GraphConfig(C.Structure):
 
 
 GRAPH_SOLVER = {"auto": 0, "dense": 1, "pcg": 2}
-GRAPH_COND = {"estimate": 0, "off": 1}
+GRAPH_COND = {"estimate": 0, "off": 1, "certify": 2}
 
 _P = C.c_void_p
 _D = C.POINTER(C.c_double)
@@ -172,6 +172,7 @@ SIGNATURES = {
     "slam_graph_get_delta": (C.c_int, [_P, _D]),
     "slam_graph_timing": (C.c_int, [_P, _D]),
     "slam_graph_cond_info": (C.c_int, [_P, _D]),
+    "slam_graph_gate_info": (C.c_int, [_P, _D]),
     "slam_graph_linearize_solve": (C.c_int, [C.POINTER(GraphConfig), _P, C.c_int64, _D, C.c_int64,
                                              _D, C.c_int]),
     "slam_graph_pair_halves": (C.c_int, [C.c_int64, _P, C.c_int64, C.c_int, _I64, _P]),

@@ -65,7 +65,7 @@ class DeviceGraph:
 
     def __init__(self, *, r_dist=0.05, r_dir=np.deg2rad(2.0), r_orient=np.deg2rad(2.0),
                  anchor=1e4, det_min=0.1, cond_max=1e15, solver="auto", pcg_tol=1e-10,
-                 pcg_max_iter=20000, cond="estimate", cond_tol=1e-5, cond_max_iter=3000, device=0):
+                 pcg_max_iter=20000, cond="certify", cond_tol=1e-5, cond_max_iter=3000, device=0):
         cfg = GraphConfig()
         cfg.r_dist, cfg.r_dir, cfg.r_orient = float(r_dist), float(r_dir), float(r_orient)
         cfg.anchor, cfg.det_min, cfg.cond_max = float(anchor), float(det_min), float(cond_max)
@@ -165,6 +165,22 @@ class DeviceGraph:
         return dict(iterations=int(out[0]), status=int(out[1]), lambda_min=out[2],
                     lambda_max=out[3], iterations_min=int(out[4]), iterations_max=int(out[5]),
                     ms=out[6])
+
+    def gate_info(self):
+        """The last PCG-path update's gate certificate (cond="certify";
+        slam_graph_gate_info): the log-det interval, the cond(H) bound, the
+        Ritz values of the preconditioned operator and each half's decision."""
+        out = np.zeros(12)
+        check(self._lib.slam_graph_gate_info(self._h, dptr(out)), "slam_graph_gate_info")
+        return dict(decided_by="bounds" if out[0] == 1 else "dense" if out[0] == 2 else "none",
+                    det_decision=int(out[1]), det=GATE_DET.get(int(out[1]), "none"),
+                    cond_decision=int(out[2]), logdet_lo=out[3], logdet_hi=out[4],
+                    cond=out[5], lambda_min=out[6], lambda_max=out[7], trp2=out[8],
+                    n=int(out[9]), estimate_iterations=int(out[10]), ms=out[11])
+
+
+GATE_DET = {1: "passed (bound)", 0: "rejected (bound)", 3: "passed (dense LU det)",
+            2: "rejected (dense LU det)", -1: "undecided"}
 
 
 def circle_graph(n_poses, n_landmarks=64, loops_per_pose=3, seed=0, odom_noise=0.02):

@@ -146,7 +146,8 @@ def test_c5_graph_full_size_pcg_solves():
         dev.set_edges(edges)
         for _ in range(2):
             is_calc, dsum, det, cond = dev.update()
-            assert is_calc and np.isnan(det) and np.isfinite(cond) and cond < 1e15
+            # the certificate's det is its lower bound exp(lo): inf at this size, as numpy's
+            assert is_calc and det > 0.1 and np.isfinite(cond) and cond < 1e15, (det, cond)
             rows, cols, vals = dev.get_bsr()
             nt = int(rows.max()) + 1
             assert nt == 50000

@@ -1,5 +1,9 @@
 """The reference's gate on the PCG path (graph_based_slam.py:494-498).
 
+Two modes: cond="estimate" (the LOBPCG estimate of cond alone, det not
+formed) and cond="certify" (the default: the estimate with an early decision
+at a factor-100 margin, plus a log-det interval; test_gpu_graph_gate.py).
+
 updateEstPose forms det(H) and cond(H) = numpy's 2-norm condition number and
 solves only if 0.1 < det and cond < 1e15.  At config-5 size the dense route is
 out of reach; the PCG path estimates cond = lambda_max / lambda_min by LOBPCG on
@@ -30,7 +34,7 @@ def _graph(T, seed=0):
 def test_cond_estimate_matches_numpy(T):
     from slamhip.graph import DeviceGraph
     init, _, edges = _graph(T)
-    dev = DeviceGraph(solver="pcg", pcg_tol=1e-10)
+    dev = DeviceGraph(solver="pcg", pcg_tol=1e-10, cond="estimate")
     den = DeviceGraph(solver="dense")
     try:
         for g in (dev, den):
@@ -102,7 +106,7 @@ def test_c5_cond_estimate_matches_scipy():
     import scipy.sparse.linalg as sla
     from slamhip.graph import DeviceGraph
     init, _, edges = _graph(50000)
-    dev = DeviceGraph(solver="pcg", pcg_tol=1e-10)
+    dev = DeviceGraph(solver="pcg", pcg_tol=1e-10, cond="estimate")
     try:
         dev.set_poses(init)
         dev.set_edges(edges)
@@ -167,7 +171,7 @@ def test_gate_rejects_unconverged_estimate():
     the well-conditioned T = 300 graph whose converged estimate passes."""
     from slamhip.graph import DeviceGraph
     init, _, edges = _graph(300)
-    g = DeviceGraph(solver="pcg", cond_max_iter=20)
+    g = DeviceGraph(solver="pcg", cond_max_iter=20, cond="estimate")
     try:
         g.set_poses(init)
         g.set_edges(edges)

@@ -1,0 +1,122 @@
+"""The certificate gate of the PCG path (cond="certify", the default;
+graph_api.hip cert_gate) against the reference's own decision,
+`0.1 < det(H) and cond(H) < 1e15` (graph_based_slam.py:494-496), formed by
+numpy on the same H exported from the device:
+
+  * det: log det H in [log det M + c(a)(tr(P^2) - n), log det M] (M the block
+    diagonal of H, P = M^-1/2 H M^-1/2; Fischer's inequality above, the
+    quadratic bound of ln below) -- the interval must contain numpy's log|det|
+    (T = 300 and T = 5,000 against a sparse LU) and decide as numpy does;
+  * a small-eigenvalue H (the measurement information scaled down 1000x):
+    det < 0.1 < ... -- numpy, the dense path and the PCG certificate all reject;
+  * cond: the estimate's early decision (factor-100 margin) passes the C5-form
+    graphs, whose cond is ~1e6-1e7.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _graph(T, seed=0):
+    from slamhip.graph import circle_graph
+    return circle_graph(T, n_landmarks=64, seed=seed, odom_noise=0.002)
+
+
+def _dense_H(dev):
+    _, H, _, _ = dev.get_system(dense=True)
+    return H
+
+
+def _sparse_H(dev):
+    import scipy.sparse as sp
+    rows, cols, vals = dev.get_bsr()
+    nt = int(rows.max()) + 1
+    return sp.bsr_matrix((vals, cols, np.searchsorted(rows, np.arange(nt + 1))),
+                         shape=(3 * nt, 3 * nt)).tocsc()
+
+
+def test_certificate_decides_like_numpy_t300():
+    from slamhip.graph import DeviceGraph
+    init, _, edges = _graph(300)
+    dev = DeviceGraph(solver="pcg", pcg_tol=1e-10)
+    try:
+        dev.set_poses(init)
+        dev.set_edges(edges)
+        ok, dsum, det, cond = dev.update()
+        gi = dev.gate_info()
+        H = _dense_H(dev)
+    finally:
+        dev.close()
+    sign, ld = np.linalg.slogdet(H)
+    ref = bool((0.1 < np.linalg.det(H)) and (np.linalg.cond(H) < 1e15))
+    assert sign > 0 and gi["logdet_lo"] <= ld <= gi["logdet_hi"], (ld, gi)
+    assert bool(ok) == ref and ref, (ok, det, cond, gi)
+    assert gi["det_decision"] == 1 and gi["cond_decision"] == 1, gi
+
+
+def test_certificate_logdet_interval_t5000():
+    import scipy.sparse.linalg as sla
+    from slamhip.graph import DeviceGraph
+    init, _, edges = _graph(5000)
+    dev = DeviceGraph(solver="pcg", pcg_tol=1e-10)
+    try:
+        dev.set_poses(init)
+        dev.set_edges(edges)
+        ok, dsum, det, cond = dev.update()
+        gi = dev.gate_info()
+        H = _sparse_H(dev)
+    finally:
+        dev.close()
+    lu = sla.splu(H)
+    ld = float(np.sum(np.log(np.abs(lu.U.diagonal()))))
+    print(gi, "numpy-side log|det|", ld)
+    assert gi["logdet_lo"] <= ld <= gi["logdet_hi"], (ld, gi)
+    assert ok and gi["det_decision"] == 1 and gi["cond_decision"] == 1, gi
+    assert gi["decided_by"] == "bounds"
+
+
+@pytest.mark.parametrize("solver", ["pcg", "dense"])
+def test_small_eigenvalue_h_det_rejects(solver):
+    """det < 0.1 < ... : the measurement noise 31.6x larger (information
+    1000x smaller) leaves cond ~1e9 < 1e15 but det ~ e^-1900; the reference
+    rejects on det alone, and so do both paths (the certificate by its upper
+    bound log det M < ln 0.1)."""
+    from slamhip.graph import DeviceGraph
+    init, _, edges = _graph(300)
+    k = np.sqrt(1000.0)
+    g = DeviceGraph(solver=solver, r_dist=0.05 * k, r_dir=np.deg2rad(2.0) * k,
+                    r_orient=np.deg2rad(2.0) * k, pcg_tol=1e-10, pcg_max_iter=20000)
+    try:
+        g.set_poses(init)
+        g.set_edges(edges)
+        ok, dsum, det, cond = g.update()
+        gi = g.gate_info() if solver == "pcg" else None
+        H = _dense_H(g)
+        np.testing.assert_array_equal(g.get_poses(), init)
+    finally:
+        g.close()
+    ndet, ncond = np.linalg.det(H), np.linalg.cond(H)
+    assert ndet < 0.1 and ncond < 1e15, (ndet, ncond)       # the det half alone rejects
+    assert not ok and dsum == 0.0, (solver, ok, det, cond, gi)
+    if solver == "pcg":
+        assert gi["det_decision"] == 0 and gi["logdet_hi"] < np.log(0.1), gi
+
+
+def test_certificate_unconverged_estimate_falls_back_to_dense_cond():
+    """an estimate stopped at cond_max_iter is not a rejection -- the
+    certificate takes the dense path's cond (n <= 2048) and decides as numpy."""
+    from slamhip.graph import DeviceGraph
+    init, _, edges = _graph(300)
+    g = DeviceGraph(solver="pcg", cond_max_iter=3)
+    try:
+        g.set_poses(init)
+        g.set_edges(edges)
+        ok, dsum, det, cond = g.update()
+        gi, info = g.gate_info(), g.cond_info()
+        H = _dense_H(g)
+    finally:
+        g.close()
+    ref = bool((0.1 < np.linalg.det(H)) and (np.linalg.cond(H) < 1e15))
+    assert info["status"] == 3 and gi["cond_decision"] == 3, (info, gi)
+    assert bool(ok) == ref and ref
