@@ -1177,6 +1177,34 @@ __device__ __forceinline__ void rng_sincos2pi_tab(const uint32_t b, const RngTab
     *cp = fma(t.y, cr, -(t.x * sr));
 }
 
+// sin / cos of a wrapped heading |x| <= pi + 0.1 (every particle heading of the
+// velocity model's predict, motion_model.py:50-56) from the same LDS table of
+// (sin, cos)(2 pi j / 256) the device RNG stages: j = rint(x 128 / pi), the
+// remainder r = x - j pi/128 (|r| <= pi/256: the first fma is exact -- j pi1
+// has <= 53 bits and lies within a factor 2 of x -- the second one rounds
+// once), sin r and cos r by their Taylor polynomials to r^7 / r^6 (truncation
+// below 3e-21 relative), then the angle addition: within ~1.5 ulp (the
+// fdlibm-kernel fast_sincos: < 1 ulp) at half its issue cost.  Anything
+// larger goes to fast_sincos.
+__device__ __forceinline__ void heading_sincos_tab(const double x, const RngTabs& T, double* sp,
+                                                   double* cp) {
+    constexpr double k128Pi = 40.74366543152521;              // 128 / pi
+    constexpr double kPi128Hi = 0x1.921fb54442dp-6;           // pi / 128, 45 significant bits
+    constexpr double kPi128Lo = 0x1.8469898cc5170p-54;        // pi / 128 - kPi128Hi
+    if (!(fabs(x) <= 3.2415926535897931)) {
+        fast_sincos(x, sp, cp);
+        return;
+    }
+    const double j = rint(x * k128Pi);
+    const double r = fma(-j, kPi128Lo, fma(-j, kPi128Hi, x));
+    const double2 t = T.sc[(int)j & 255];
+    const double z = r * r;
+    const double sr = fma(r * z, fma_k(z, fma_kk(z, -1.0 / 5040.0, 1.0 / 120.0), -1.0 / 6.0), r);
+    const double cr = fma(z, fma_k(z, fma_kk(z, -1.0 / 720.0, 1.0 / 24.0), -0.5), 1.0);
+    *sp = fma(t.x, cr, t.y * sr);
+    *cp = fma(t.y, cr, -(t.x * sr));
+}
+
 // log((a + 1) 2^-32), a a 32-bit word: m in [sqrt(1/2), sqrt(2)) as in
 // fdlibm, r = m invc - 1 (one rounding, |r| <= 2^-7), log1p(r) by its degree-8
 // Taylor polynomial (truncation < 2e-18 relative), plus e ln2 and -log(invc)

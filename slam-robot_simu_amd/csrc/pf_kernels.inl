@@ -353,6 +353,9 @@ __device__ __forceinline__ int64_t wave_min_i64(int64_t v) {
 // accumulators.  Every sum has a fixed order: per lane over k, lane pairs
 // (2l, 2l+1), 16 pair-strided segments of 8 (conflict-free LDS reads) left to
 // right, then the 16 segments.
+#ifndef SLAM_EPI_FMA
+#define SLAM_EPI_FMA 0
+#endif
 __device__ void defer_epilogue(const int64_t base, const int64_t n, const double* wv,
                                const double* xv, const double* yv, const double* tv,
                                const double* __restrict__ refp, const DeferParts& dp,
@@ -401,16 +404,28 @@ __device__ void defer_epilogue(const int64_t base, const int64_t n, const double
         const double d0 = xv[k] - r0, d1 = yv[k] - r1, d2 = tv[k] - r2;
         const double ud0 = u * d0, ud1 = u * d1, ud2 = u * d2;
         q[0] += u;
-        q[1] += u * u;
         q[2] += ud0;
         q[3] += ud1;
         q[4] += ud2;
+#if SLAM_EPI_FMA
+        // the second moments as fused multiply-adds (one rounding each; the
+        // partials are the filter's own, not the reference's: cov 1e-6)
+        q[1] = fma(u, u, q[1]);
+        q[5] = fma(ud0, d0, q[5]);
+        q[6] = fma(ud0, d1, q[6]);
+        q[7] = fma(ud0, d2, q[7]);
+        q[8] = fma(ud1, d1, q[8]);
+        q[9] = fma(ud1, d2, q[9]);
+        q[10] = fma(ud2, d2, q[10]);
+#else
+        q[1] += u * u;
         q[5] += ud0 * d0;
         q[6] += ud0 * d1;
         q[7] += ud0 * d2;
         q[8] += ud1 * d1;
         q[9] += ud1 * d2;
         q[10] += ud2 * d2;
+#endif
     }
 #pragma unroll
     for (int j = 0; j < kQ; ++j) {
@@ -503,12 +518,18 @@ __device__ __forceinline__ int64_t search_c(const double* __restrict__ c, int64_
 //    from sin/cos(th) and the small turn increments w dt and gamma dt (two
 //    kernel-only sin/cos instead of two range-reduced ones; within 2 ulp of
 //    the direct evaluation).
+// SLAM_TAB_SINCOS (default 1): the velocity model's sin/cos(th) from the LDS
+// table (heading_sincos_tab) instead of fast_sincos.
+#ifndef SLAM_TAB_SINCOS
+#define SLAM_TAB_SINCOS 1
+#endif
 template <int MOTION>
 __device__ __forceinline__ void predict_particle(const double x, const double y, const double th,
                                                  const double v, const double om, const double g0,
                                                  const double g1, const double g2,
                                                  const PredictConst& pc, double& xn, double& yn,
-                                                 double& tn, double& ls, double& lc) {
+                                                 double& tn, double& ls, double& lc,
+                                                 const RngTabs& T) {
     if (MOTION == kMotionNone) {           // likelihood-only entry (particle_filter.py:170)
         xn = x;
         yn = y;
@@ -536,7 +557,12 @@ __device__ __forceinline__ void predict_particle(const double x, const double y,
         const double a = vh / wh;
         const double b = wh * pc.dt;
         double s0, c0, sb, cb, s1, c1, se, ce;
+#if SLAM_TAB_SINCOS
+        heading_sincos_tab(th, T, &s0, &c0);
+#else
+        (void)T;
         fast_sincos(th, &s0, &c0);
+#endif
         small_sincos(b, &sb, &cb);
         rotate_sc(s0, c0, sb, cb, &s1, &c1);                 // (th + w dt)
         xn = (x - (a * s0)) + (a * s1);
@@ -1279,7 +1305,7 @@ __device__ __forceinline__ void pf_fused_tile(
 #pragma unroll
     for (int k = 0; k < P; ++k)
         predict_particle<MOTION>(x[k], y[k], th[k], v, om, g[k][0], g[k][1], g[k][2], pc, xv[k],
-                                 yv[k], tv[k], sp[k], cp[k]);
+                                 yv[k], tv[k], sp[k], cp[k], rtab);
     if (DEFER) {                       // padded arrays: the pair is stored whole
 #pragma unroll
         for (int h = 0; h < P; h += 2) {
@@ -1374,7 +1400,8 @@ __device__ __forceinline__ void pf_fused_prep_next(const int32_t st, const int w
     const int wave_s = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);                    \
     __shared__ RngTabsLds s_rng;                                                                 \
     RngTabs rtab{};                                                                              \
-    if constexpr (MOTION != kMotionNone && !HOSTNOISE) {                                         \
+    if constexpr ((MOTION != kMotionNone && !HOSTNOISE) ||                                      \
+                  (MOTION == SLAM_MOTION_VELOCITY && SLAM_TAB_SINCOS)) {                         \
         rtab = rng_tabs_stage(&s_rng, (int)threadIdx.x, 256);                                    \
         __syncthreads();                                                                         \
     }
