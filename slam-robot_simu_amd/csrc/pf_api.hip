@@ -686,7 +686,7 @@ int sync_results(slam_pf* h, int32_t first, int32_t count, slam_pf_result* out, 
 
 int create_impl(const slam_pf_config* cfg, int64_t n_local, int64_t n_global, int64_t gbase,
                 int32_t n_landmarks, const double* landmarks, int device, slam_pf** out,
-                bool deferred) {
+                bool deferred, bool dist_shard) {
     SLAM_ARG_CHECK(cfg && out, "slam_pf_create: NULL argument");
     SLAM_ARG_CHECK(n_local > 0 && n_global < (int64_t(1) << 31) && gbase >= 0 &&
                        gbase + n_local <= n_global,
@@ -744,22 +744,28 @@ int create_impl(const slam_pf_config* cfg, int64_t n_local, int64_t n_global, in
     }
     // deferred handles: particle and weight arrays padded to whole fused blocks
     // (the fused kernel moves particle pairs with 16-byte loads and stores)
+    // (a sharded handle: npad staging slots on either side of each particle
+    // array for the particles a resample receives from other ranks, DeferParts.goff)
     const int64_t npad = deferred ? (int64_t)h->nb_part * kPartPer : n;
+    const int64_t side = dist_shard ? npad : 0;
     for (int k = 0; k < 2; ++k) {
-        A(h->x[k], npad);
-        A(h->y[k], npad);
-        A(h->th[k], npad);
+        A(h->x[k], npad + 2 * side);
+        A(h->y[k], npad + 2 * side);
+        A(h->th[k], npad + 2 * side);
+        if (npad > n || side) {
+            SLAM_HIP_TRY(hipMemsetAsync(h->x[k], 0, sizeof(double) * (npad + 2 * side), h->stream));
+            SLAM_HIP_TRY(hipMemsetAsync(h->y[k], 0, sizeof(double) * (npad + 2 * side), h->stream));
+            SLAM_HIP_TRY(hipMemsetAsync(h->th[k], 0, sizeof(double) * (npad + 2 * side), h->stream));
+        }
+        h->x[k] += side;
+        h->y[k] += side;
+        h->th[k] += side;
     }
+    h->dp.goff = side;
+    h->dp.glim = dist_shard ? 3 * npad : n;
     A(h->w, n);
     A(h->w_un, npad);
-    if (npad > n) {
-        for (int k = 0; k < 2; ++k) {
-            SLAM_HIP_TRY(hipMemsetAsync(h->x[k], 0, sizeof(double) * npad, h->stream));
-            SLAM_HIP_TRY(hipMemsetAsync(h->y[k], 0, sizeof(double) * npad, h->stream));
-            SLAM_HIP_TRY(hipMemsetAsync(h->th[k], 0, sizeof(double) * npad, h->stream));
-        }
-        SLAM_HIP_TRY(hipMemsetAsync(h->w_un, 0, sizeof(double) * npad, h->stream));
-    }
+    if (npad > n) SLAM_HIP_TRY(hipMemsetAsync(h->w_un, 0, sizeof(double) * npad, h->stream));
     A(h->c, npad);
     A(h->kincl, n);
     A(h->fexcl, n);
@@ -907,7 +913,8 @@ extern "C" {
 
 int slam_pf_create(const slam_pf_config* cfg, int64_t n_particles, int32_t n_landmarks,
                    const double* landmarks, int device, slam_pf** out) {
-    return create_impl(cfg, n_particles, n_particles, 0, n_landmarks, landmarks, device, out, true);
+    return create_impl(cfg, n_particles, n_particles, 0, n_landmarks, landmarks, device, out, true,
+                       false);
 }
 
 int slam_pf_destroy(slam_pf* h) {

@@ -66,6 +66,8 @@ struct DistLayout {
     int64_t spec = 0;           // [world][cap_spec] SpecialIn
     int64_t item_hdr = 0;       // [world] {count, pad}
     int64_t item = 0;           // [world][cap_item] DistItem (own slot unused: self_items)
+    int64_t pitem = 0;          // [cap_item] DistRun at its first local position (merged exchange)
+    int64_t pcarry = 0;         // [cap_item / kPartPer + 1] (epoch << 32) | run start of each fused block
     int64_t total = 0;
     int64_t rec_stride = 0, cap_spec = 0, cap_item = 0;
 };
@@ -74,6 +76,13 @@ struct DistLayout {
 struct alignas(16) DistItem {
     double x, y, th;
     int64_t lo, hi, pad;
+};
+
+// a resampled particle received from a peer, at the first position of its run
+// in this rank's shard (the merged exchange; no count exchange needed)
+struct alignas(16) DistRun {
+    double x, y, th;
+    uint64_t tag;               // (epoch << 32) | run length
 };
 
 struct DistPeers {
@@ -99,9 +108,10 @@ struct DistScratch {
     uint64_t ktot_g;
     double base_off;            // approximate cumsum before local element 0
     double c_left;              // exact cumsum just before local element 0 (-inf on rank 0)
-    int64_t lo0;                // positions <= c_left
+    int64_t lo0;                // positions <= c_left (the first one this rank's sources serve)
+    int64_t hi0;                // positions served by this rank and the lower ones (merged exchange)
     int64_t covered;            // positions covered by the received items (unpack; reset by its last block)
-    int32_t rel[4];             // dist_resample_merged_kernel: release tokens of phases A / B / D
+    int32_t rel[4];             // dist_resample_merged_kernel: release tokens of phases A / D
     int64_t dbase[kDistMaxWorld];   // per destination: selected sources before its range
     int64_t dcnt[kDistMaxWorld];    // per destination: items sent
 };
@@ -529,6 +539,7 @@ __device__ void dist_unpack_items(const int64_t n, double* __restrict__ xs, doub
     const int64_t ntot = s_off[P.world] < n ? s_off[P.world] : n;
     const int64_t gb = P.gb[P.rank];
     const int64_t gen = (int64_t)(uint32_t)flags[kFlagMarkGen] << 32;
+    const int64_t goff = (n + kPartPer - 1) / kPartPer * kPartPer;   // npad
     uint64_t cov = 0;
     for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < ntot;
          k += (int64_t)gridDim.x * blockDim.x) {
@@ -558,8 +569,9 @@ __device__ void dist_unpack_items(const int64_t n, double* __restrict__ xs, doub
         xs[k] = x;
         ys[k] = y;
         ts[k] = th;
-        mark[lo] = gen | k;
-        for (int64_t b = (lo + kPartPer - 1) / kPartPer; b * kPartPer < hi; ++b) carry[b] = (int32_t)k;
+        mark[lo] = gen | (goff + k);                        // gather source goff + k (DeferParts.goff)
+        for (int64_t b = (lo + kPartPer - 1) / kPartPer; b * kPartPer < hi; ++b)
+            carry[b] = (int32_t)(goff + k);
         cov += (uint64_t)(hi - lo);
     }
     cov = wave_sum_u64(cov);
@@ -645,6 +657,137 @@ __device__ __forceinline__ void dist_token_release(int32_t* word, const int32_t 
     if (threadIdx.x == 0) {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         st_wt_i(word, token);
+    }
+}
+
+// Merged exchange, phase B: the runs of this lane's selected sources (global
+// positions [lv, hv), local source j0 + k) that fall in destination d's shard.
+// This rank's own positions get the fused kernel's inverse map directly -- a
+// run mark (mark generation | npad + j) at the run's first position and the
+// carry of every fused block whose first position lies in the run, as the
+// single-GPU expand pass writes them; a peer's get the particle stored at the
+// run's first local position of its region, tagged with the epoch and the
+// run length, and the carries in its region (system-scope stores: complete
+// when the storing block takes its ticket).
+__device__ __forceinline__ void dist_store_run(DistRun* r, const double x, const double y, const double th,
+                                               const uint64_t tag) {
+    uint64_t* q = reinterpret_cast<uint64_t*>(r);
+    __hip_atomic_store(q + 0, (uint64_t)__double_as_longlong(x), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(q + 1, (uint64_t)__double_as_longlong(y), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(q + 2, (uint64_t)__double_as_longlong(th), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(q + 3, tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__device__ __forceinline__ void dist_place_runs(const DistPeers& P, const int d,
+                                                const int64_t (&lv)[kScanPer],
+                                                const int64_t (&hv)[kScanPer], const int64_t j0,
+                                                const int64_t npad, const int64_t gen,
+                                                const uint64_t epoch, const double* __restrict__ xs,
+                                                const double* __restrict__ ys,
+                                                const double* __restrict__ ts,
+                                                int64_t* __restrict__ mark,
+                                                int32_t* __restrict__ carry) {
+    const int lane = threadIdx.x & 63;
+    const int64_t g0 = P.gb[d], g1 = P.gb[d + 1];
+    const bool own = d == P.rank;
+    DistRun* runs = reinterpret_cast<DistRun*>(P.base[d] + P.L.pitem);
+    uint64_t* pcar = reinterpret_cast<uint64_t*>(P.base[d] + P.L.pcarry);
+    const uint64_t etag = epoch << 32;
+#pragma unroll
+    for (int k = 0; k < kScanPer; ++k) {
+        const int64_t lo = lv[k] > g0 ? lv[k] : g0, hi = hv[k] < g1 ? hv[k] : g1;
+        const int64_t p0 = lo - g0, p1 = hi - g0, j = j0 + k;
+        int64_t flo = 0, fhi = 0;
+        if (hv[k] > lv[k] && lo < hi) {
+            if (own) mark[p0] = gen | (npad + j);
+            else dist_store_run(runs + p0, xs[j], ys[j], ts[j], etag | (uint64_t)(p1 - p0));
+            flo = (p0 + kPartPer - 1) / kPartPer;
+            fhi = (p1 + kPartPer - 1) / kPartPer;
+        }
+        // carries, written by the whole wave (a heavy source may own many)
+        uint64_t act = __ballot(fhi > flo);
+        while (act) {
+            const int l = __ffsll((unsigned long long)act) - 1;
+            act &= act - 1;
+            const int64_t L = __shfl(flo, l, 64), H = __shfl(fhi, l, 64);
+            if (own) {
+                const int32_t v = (int32_t)(npad + __shfl(j, l, 64));
+                for (int64_t f = L + lane; f < H; f += 64) carry[f] = v;
+            } else {
+                const uint64_t v = etag | (uint64_t)__shfl(p0, l, 64);
+                for (int64_t f = L + lane; f < H; f += 64)
+                    __hip_atomic_store(pcar + f, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+        }
+    }
+}
+
+// Merged exchange, phase D (after every rank's kXItem): the positions of this
+// shard that other ranks' sources serve -- [0, a) from the lower ranks, [b, n)
+// from the higher ones, a / b from the global fold (lo0, hi0) -- take the
+// runs the peers stored: the particle into the staging slot of gather index v
+// (v = p below a, 2 npad + p from b: x[v - npad]), a run mark at p, and the
+// carry of every fused block starting there.  The run lengths must tile both
+// ranges (status kDistStItems otherwise; the last block checks).
+__device__ void dist_take_runs(const DistPeers& P, const int64_t n, const int64_t npad,
+                               const int64_t lo0, const int64_t hi0, const int64_t gen,
+                               const uint64_t epoch, double* __restrict__ xs,
+                               double* __restrict__ ys, double* __restrict__ ts,
+                               int64_t* __restrict__ mark, int32_t* __restrict__ carry,
+                               unsigned* __restrict__ counter, int32_t* __restrict__ flags,
+                               DistScratch* __restrict__ scr) {
+    __shared__ unsigned long long s_cov;
+    __shared__ int s_bad;
+    if (threadIdx.x == 0) {
+        s_cov = 0;
+        s_bad = 0;
+    }
+    __syncthreads();
+    const int64_t gb = P.gb[P.rank];
+    auto local = [&](int64_t v) {
+        v -= gb;
+        return v < 0 ? (int64_t)0 : (v > n ? n : v);
+    };
+    const int64_t a = local(lo0), b = local(hi0) > a ? local(hi0) : a;
+    const int64_t m = a + (n - b);
+    const DistRun* runs = reinterpret_cast<const DistRun*>(P.base[P.rank] + P.L.pitem);
+    const uint64_t* pcar = reinterpret_cast<const uint64_t*>(P.base[P.rank] + P.L.pcarry);
+    const uint32_t e32 = (uint32_t)epoch;
+    uint64_t cov = 0;
+    bool bad = false;
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < m;
+         t += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t p = t < a ? t : b + (t - a);
+        const uint64_t tag = ld_sys(&runs[p].tag);
+        if ((uint32_t)(tag >> 32) == e32) {
+            const int64_t v = p < a ? p : 2 * npad + p;
+            xs[v - npad] = ld_sys_d(&runs[p].x);
+            ys[v - npad] = ld_sys_d(&runs[p].y);
+            ts[v - npad] = ld_sys_d(&runs[p].th);
+            mark[p] = gen | v;
+            cov += tag & 0xFFFFFFFFu;
+        }
+        if (p % kPartPer == 0) {                            // a fused block starts here
+            const uint64_t c = ld_sys(pcar + p / kPartPer);
+            const int64_t p0 = (int64_t)(uint32_t)c;
+            if ((uint32_t)(c >> 32) == e32 && p0 <= p)
+                carry[p / kPartPer] = (int32_t)(p < a ? p0 : 2 * npad + p0);
+            else
+                bad = true;
+        }
+    }
+    cov = wave_sum_u64(cov);
+    if ((threadIdx.x & 63) == 0 && cov) atomicAdd(&s_cov, (unsigned long long)cov);
+    if (bad) s_bad = 1;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        if (s_cov) atomicAdd((unsigned long long*)&scr->covered, s_cov);
+        if (s_bad) atomicOr(&flags[kFlagStatus], kDistStItems);
+    }
+    if (!arrive_last(counter)) return;
+    if (threadIdx.x == 0) {
+        const unsigned long long c = atomicExch((unsigned long long*)&scr->covered, 0ull);
+        if ((int64_t)c != m) atomicOr(&flags[kFlagStatus], kDistStItems);
     }
 }
 
@@ -734,18 +877,15 @@ __global__ __launch_bounds__(kScanThreads) void dist_resample_merged_kernel(
     uint64_t* __restrict__ boffk, int32_t* __restrict__ bofff, uint64_t* __restrict__ ktot_p,
     int32_t* __restrict__ nspec_p, unsigned* __restrict__ tk, int32_t* __restrict__ flags,
     SpecialOut* __restrict__ spec_go, DistScratch* __restrict__ scr,
-    int32_t* __restrict__ bsel, int32_t* __restrict__ bsel_off, int32_t* __restrict__ bdst,
     double* __restrict__ xs, double* __restrict__ ys, double* __restrict__ ts,
     int64_t* __restrict__ mark, int32_t* __restrict__ carry, const DistPeers P, StepIO io,
     const PredictConst pc, const uint64_t seed, const int ntiles) {
     if (!dist_resampling(flags)) return;
     __shared__ int64_t s_off[kDistMaxWorld + 1];
     __shared__ uint64_t s_koff[kDistMaxWorld + 1];
-    __shared__ int32_t s_cb[kDistMaxWorld], s_cc[kDistMaxWorld];
     const uint64_t epoch = dist_epoch(io);
     const int32_t tokA = ld_wt_i(&scr->rel[0]) + 1;        // read before this block arrives
     const int32_t tokB = ld_wt_i(&scr->rel[1]) + 1;
-    const int32_t tokD = ld_wt_i(&scr->rel[2]) + 1;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int64_t tile = (int64_t)blockIdx.x * kTilesPerBlock + wave;
     const bool active = tile < ntiles;
@@ -839,8 +979,22 @@ __global__ __launch_bounds__(kScanThreads) void dist_resample_merged_kernel(
             scr->k_base = s_koff[P.rank];
             scr->nspec_g = (int32_t)s_off[P.world];
             scr->ktot_g = s_koff[P.world];
+            // the first position the next rank's sources serve: everything
+            // from there on (and before lo0) arrives from the peers
+            int64_t hi0 = n_global;
+            if (P.rank + 1 < P.world) {
+                const int64_t sb1 = s_off[P.rank + 1];
+                double c1 = -INFINITY;
+                if (sb1 > 0) {
+                    const SpecialOut p1 = ld_wt_struct(&spec_go[sb1 - 1]);
+                    c1 = p1.cs + (double)(s_koff[P.rank + 1] - p1.P) * ldexp(1.0, p1.E - 52);
+                }
+                const double ofs = resample_offset(io.ofs[io.ctr[0]], np_recip, seed, (uint32_t)io.ctr[1]);
+                hi0 = positions_upto(c1, n_global, pc.rstep, ofs);
+            }
             scr->c_left = cl;
             scr->lo0 = lo0;
+            scr->hi0 = hi0;
         }
         dist_token_release(&scr->rel[0], tokA);
         PROBE_AT(22);
@@ -849,15 +1003,11 @@ __global__ __launch_bounds__(kScanThreads) void dist_resample_merged_kernel(
     }
     __syncthreads();
     if (ld_wt_i(&flags[kFlagFallback])) return;             // block-uniform
-    // ---- B: expand, positions, selected counts
-    if ((int)threadIdx.x < kDistMaxWorld) {
-        s_cb[threadIdx.x] = 0;
-        s_cc[threadIdx.x] = 0;
-    }
+    // ---- B: expand, positions; every run placed where its positions are
     const double ofs = resample_offset(io.ofs[io.ctr[0]], np_recip, seed, (uint32_t)io.ctr[1]);
     const int32_t sb = ld_wt_i(&scr->spec_base);
-    int64_t hv[kScanPer], lv[kScanPer];
-    int32_t cnt = 0;
+    const int64_t npad = (int64_t)ntiles * kPartPer;        // the gather offset (DeferParts.goff)
+    const int64_t gen = (int64_t)(uint32_t)flags[kFlagMarkGen] << 32;
     if (active) {
         const uint64_t kb = ld_wt(&scr->k_base);
         const int64_t b = blockIdx.x;
@@ -889,6 +1039,7 @@ __global__ __launch_bounds__(kScanThreads) void dist_resample_merged_kernel(
         }
         int64_t sj = positions_upto(cprev, n_global, pc.rstep, ofs);
         const int64_t j0 = tile * kWaveTile + 8 * lane;
+        int64_t lv[kScanPer], hv[kScanPer];
 #pragma unroll
         for (int k = 0; k < kScanPer; ++k) {
             const int64_t j = j0 + k;
@@ -902,115 +1053,31 @@ __global__ __launch_bounds__(kScanThreads) void dist_resample_merged_kernel(
             }
             lv[k] = sj;
             hv[k] = ej;
-            cnt += (ej > sj) ? 1 : 0;
             sj = ej;
         }
-        // per destination: selected sources entirely before its positions / overlapping them
-        for (int d = 0; d < P.world; ++d) {
-            int32_t cb = 0, cc = 0;
-#pragma unroll
-            for (int k = 0; k < kScanPer; ++k) {
-                if (hv[k] > lv[k]) {
-                    if (hv[k] <= P.gb[d]) ++cb;
-                    else if (lv[k] < P.gb[d + 1]) ++cc;
-                }
-            }
-            {   // both counts (<= 512 per wave) in one word
-                const int32_t both = wave_sum_i32((cb << 16) | cc);
-                cb = both >> 16;
-                cc = both & 0xFFFF;
-            }
-            if (lane == 0) {
-                if (cb) atomicAdd(&s_cb[d], cb);
-                if (cc) atomicAdd(&s_cc[d], cc);
-            }
+        // the destinations this wave's runs reach (positions are monotone
+        // over the lanes): usually this rank alone
+        const int64_t wlo = __shfl(lv[0], 0, 64), whi = __shfl(hv[kScanPer - 1], 63, 64);
+        if (whi > wlo) {
+            const int dlo = dist_owner(P, wlo), dhi = dist_owner(P, whi - 1);
+            for (int d = dlo; d <= dhi; ++d)
+                dist_place_runs(P, d, lv, hv, j0, npad, gen, epoch, xs, ys, ts, mark, carry);
         }
     }
-    __shared__ int32_t shs[kScanThreads / 64 + 1];
-    int32_t tot;
-    const int32_t cex = block_excl_scan<int32_t, kScanThreads>(cnt, shs, tot);   // (barriers publish s_cb / s_cc)
-    // the block's counts per destination (bdst[b][2 d + {0, 1}]): no contended atomics
-    if ((int)threadIdx.x < 2 * P.world) {
-        const int d = threadIdx.x >> 1;
-        st_wt_i(&bdst[(int64_t)blockIdx.x * 2 * kDistMaxWorld + threadIdx.x],
-                (threadIdx.x & 1) ? s_cc[d] : s_cb[d]);
-    }
-    if (threadIdx.x == 0) st_wt_i(&bsel[blockIdx.x], tot);
     PROBE_MAX(23);
-    if (arrive_last(tk + kTicketWords)) {
-        __shared__ int32_t shs2[kScanThreads / 64 + 1];
-        block_scan_array<int32_t, kScanThreads>(bsel, bsel_off, gridDim.x, nullptr, shs2, true);
-        // dbase / dcnt: the per-destination counts summed over the blocks (a
-        // wave per destination pair, lanes striding over the blocks)
-        for (int e = wave; e < 2 * P.world; e += kScanThreads / 64) {
-            int64_t a = 0;
-            for (int b0 = lane; b0 < (int)gridDim.x; b0 += 64 * 8) {
-                int32_t v[8];                               // eight loads in flight
-#pragma unroll
-                for (int u = 0; u < 8; ++u) {
-                    const int b = b0 + 64 * u;
-                    v[u] = (b < (int)gridDim.x) ? ld_wt_i(&bdst[(int64_t)b * 2 * kDistMaxWorld + e]) : 0;
-                }
-#pragma unroll
-                for (int u = 0; u < 8; ++u) a += v[u];
-            }
-            a = (int64_t)wave_sum_u64((uint64_t)a);
-            if (lane == 0) st_wt((e & 1) ? (void*)&scr->dcnt[e >> 1] : (void*)&scr->dbase[e >> 1], (uint64_t)a);
-        }
-        dist_token_release(&scr->rel[1], tokB);
-        PROBE_AT(24);
-    } else {
-        dist_token_wait(&scr->rel[1], tokB, flags);
-    }
-    __shared__ int64_t s_dbase[kDistMaxWorld];
-    __shared__ int64_t s_ps0;
-    if ((int)threadIdx.x < P.world) s_dbase[threadIdx.x] = (int64_t)ld_wt(&scr->dbase[threadIdx.x]);
-    if (threadIdx.x == 0) s_ps0 = ld_wt_i(&bsel_off[blockIdx.x]);
-#ifdef SLAM_PROBE
-    if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0)
-        g_probe[15] = (unsigned long long)(ld_wt_i(&bsel_off[blockIdx.x]) + tot);
-#endif
-    __syncthreads();
-    // ---- C: items to every destination
-    if (active) {
-        int64_t ps = s_ps0 + cex;
-        const int64_t j0 = tile * kWaveTile + 8 * lane;
-#pragma unroll
-        for (int k = 0; k < kScanPer; ++k) {
-            if (hv[k] > lv[k]) {
-                const int64_t j = j0 + k, lo = lv[k], h = hv[k];
-                const double x = xs[j], y = ys[j], th = ts[j];
-                for (int d = dist_owner(P, lo); d < P.world && P.gb[d] < h; ++d) {
-                    const int64_t slot = ps - s_dbase[d];
-                    if (slot >= 0 && slot < P.L.cap_item)
-                        dist_store_item(P, d, slot, x, y, th, lo > P.gb[d] ? lo : P.gb[d],
-                                        h < P.gb[d + 1] ? h : P.gb[d + 1]);
-                    else atomicOr(&flags[kFlagStatus], kDistStItems);
-                }
-                ++ps;
-            }
-        }
-    }
-    PROBE_MAX(25);
-    // ---- D: publish, wait for every rank's items, unpack them (dist_unpack_items)
-    if (arrive_last(tk + 2 * kTicketWords)) {              // (drains this block's item stores)
-        if ((int)threadIdx.x < P.world) {
-            int64_t* hdr = reinterpret_cast<int64_t*>(P.base[threadIdx.x] + P.L.item_hdr) + 2 * P.rank;
-            hdr[0] = (int64_t)ld_wt(&scr->dcnt[threadIdx.x]);
-        }
-        __syncthreads();
+    if (P.world == 1) return;                               // every run is this rank's own
+    // ---- D: publish, wait for every rank's runs, take the received ones
+    if (arrive_last(tk + kTicketWords)) {                   // (drains this block's run stores)
         dist_signal(P, kXItem, epoch);
         PROBE_AT(26);
         dist_wait(P, kXItem, epoch, flags);
-        dist_token_release(&scr->rel[2], tokD);
+        dist_token_release(&scr->rel[1], tokB);
     } else {
-        dist_token_wait(&scr->rel[2], tokD, flags);
+        dist_token_wait(&scr->rel[1], tokB, flags);
     }
     __syncthreads();
-    __shared__ int64_t s_ioff[kDistMaxWorld + 1];
-    if (threadIdx.x == 0) dist_item_offsets(P, s_ioff);
-    __syncthreads();
-    dist_unpack_items(n, xs, ys, ts, mark, carry, tk + 3 * kTicketWords, flags, scr, P, s_ioff);
+    dist_take_runs(P, n, npad, (int64_t)ld_wt(&scr->lo0), (int64_t)ld_wt(&scr->hi0), gen, epoch, xs,
+                   ys, ts, mark, carry, tk + 3 * kTicketWords, flags, scr);
 }
 
 // ---------------------------------------------------------------- record

@@ -22,7 +22,6 @@ struct slam_dist {
     std::vector<SpecialOut*> spec_go;
     std::vector<int64_t*> hi;
     std::vector<int32_t*> bsel, bsel_off;
-    std::vector<int32_t*> bdst;               // [nb_scan][2 kDistMaxWorld] per-block destination counts
     std::vector<unsigned*> tk;                // 4 ticket blocks per held shard
     std::vector<void*> dallocs;
     std::vector<void*> opened;                // IPC mappings of peer regions
@@ -68,7 +67,7 @@ int dist_enqueue_step(slam_dist* d) {
         dist_resample_merged_kernel<<<h->nb_scan, kScanThreads, 0, h->stream>>>(
             h->w_un, h->s_cur, h->pc.np_recip, h->n, h->boff, delta, h->stage, h->bk, h->bf,
             h->boffk, h->bofff, h->ktot, h->nspec, d->tk[0], h->flags, d->spec_go[0], d->scr[0],
-            d->bsel[0], d->bsel_off[0], d->bdst[0], h->x[c], h->y[c], h->th[c], h->dp.mark,
+            h->x[c], h->y[c], h->th[c], h->dp.mark,
             h->dp.carry, d->peers[0], step_io(h), h->pc, h->cfg.seed, h->nb_part);
     }
     for (int i = 0; i < m && !d->merged; ++i) {           // exact cumsum: classify
@@ -363,7 +362,7 @@ int slam_pf_create_dist_shard(const slam_pf_config* cfg, int64_t n_local, int64_
                    "slam_pf_create_dist_shard: every shard but the last must hold a multiple of "
                    "8192 particles (np.sum buffer alignment)");
     SLAM_ARG_CHECK(n_local <= (int64_t)2048 * kSumChunk, "slam_pf_create_dist_shard: n_local > 2^24");
-    return create_impl(cfg, n_local, n_global, gbase, n_landmarks, landmarks, device, out, true);
+    return create_impl(cfg, n_local, n_global, gbase, n_landmarks, landmarks, device, out, true, true);
 }
 
 // the standard split of N particles over `world` ranks: rank r holds
@@ -441,6 +440,8 @@ int slam_dist_create(slam_pf** shards, int32_t n_held, int32_t world, int32_t ra
     L.spec = take((int64_t)sizeof(SpecialIn) * L.cap_spec * world);
     L.item_hdr = take(16 * world);
     L.item = take((int64_t)sizeof(DistItem) * L.cap_item * world);
+    L.pitem = take((int64_t)sizeof(DistRun) * L.cap_item);
+    L.pcarry = take(8 * (L.cap_item / kPartPer + 2));
     L.total = off;
     int rc;
     if (d->local) {
@@ -455,7 +456,9 @@ int slam_dist_create(slam_pf** shards, int32_t n_held, int32_t world, int32_t ra
             return bail(fail(SLAM_ERR_HIP, "slam_dist_create: fine-grained exchange region allocation failed"));
         d->xbuf.push_back((char*)xb);
         DIST_TRY(hipMemset(xb, 0, (size_t)L.flags + 3 * kDistMaxWorld * 8));
-        void *p1, *p2, *p3, *p4, *p5, *p6, *p7, *p8, *p9;
+        // run tags (epoch >= 1) of the merged exchange start unmatched
+        DIST_TRY(hipMemset((char*)xb + L.pitem, 0, (size_t)(L.total - L.pitem)));
+        void *p1, *p2, *p3, *p4, *p5, *p6, *p7, *p8;
         const int32_t nbs = h->nb_scan;
         if ((rc = dist_alloc(d, &p1, sizeof(DistScratch))) ||
             (rc = dist_alloc(d, &p2, sizeof(SpecialIn) * (size_t)std::max<int64_t>(N, 1))) ||
@@ -464,8 +467,7 @@ int slam_dist_create(slam_pf** shards, int32_t n_held, int32_t world, int32_t ra
             (rc = dist_alloc(d, &p5, sizeof(int32_t) * (size_t)nbs)) ||
             (rc = dist_alloc(d, &p6, sizeof(int32_t) * (size_t)nbs)) ||
             (rc = dist_alloc(d, &p7, sizeof(unsigned) * 4 * kTicketWords)) ||
-            (rc = dist_alloc(d, &p8, sizeof(DistItem) * (size_t)L.cap_item)) ||
-            (rc = dist_alloc(d, &p9, sizeof(int32_t) * 2 * kDistMaxWorld * (size_t)nbs)))
+            (rc = dist_alloc(d, &p8, sizeof(DistItem) * (size_t)L.cap_item)))
             return bail(rc);
         DIST_TRY(hipMemset(p1, 0, sizeof(DistScratch)));
         DIST_TRY(hipMemset(p7, 0, sizeof(unsigned) * 4 * kTicketWords));
@@ -476,7 +478,6 @@ int slam_dist_create(slam_pf** shards, int32_t n_held, int32_t world, int32_t ra
         d->bsel.push_back((int32_t*)p5);
         d->bsel_off.push_back((int32_t*)p6);
         d->tk.push_back((unsigned*)p7);
-        d->bdst.push_back((int32_t*)p9);
         DistPeers P{};
         P.world = world;
         P.rank = rank0 + i;

@@ -55,6 +55,13 @@ struct DeferParts {
     double* leaf;           // [blocks] the block's np.sum subtree (its kPartPer / 128 leaves, pairwise)
     int64_t* mark;          // [npad] resample-run starts: (RNG step << 32) | source (expand pass)
     int32_t* carry;         // [blocks] source of each fused block's first position
+    // the resample gather reads source v at (x - goff)[v]: 0 on single-GPU
+    // handles; npad on a sharded handle, whose particle arrays carry npad
+    // staging slots on either side (particles received from lower ranks at
+    // v = p, its own at npad + j, from higher ranks at 2 npad + p, so the
+    // running max over a block's marks stays monotone)
+    int64_t goff;
+    int64_t glim;           // sources >= glim: the reference's IndexError (n; 3 npad when sharded)
 };
 
 // particle_filter.py:179-181 + the mlab.bivariate_normal constants

@@ -1205,17 +1205,20 @@ __device__ __forceinline__ void pf_fused_tile(
         int32_t run = dp.carry[blk];
         for (int w = 0; w < wave; ++w) run = s_wmax[w] > run ? s_wmax[w] : run;
         run = before > run ? before : run;
+        const double* gx = xs - dp.goff;                         // the gather base
+        const double* gy = ys - dp.goff;
+        const double* gt = ts - dp.goff;
 #pragma unroll
         for (int k = 0; k < P; ++k) {
             int64_t src = r[k] > run ? r[k] : run;
-            if (src >= n) {
-                src = n - 1;                                     // IndexError in the reference
+            if (src >= dp.glim) {
+                src = dp.goff + n - 1;                           // IndexError in the reference
                 if (valid[k]) atomicOr(&flags[kFlagStatus], 1);
             }
             src = src < 0 ? 0 : src;
-            x[k] = xs[src];
-            y[k] = ys[src];
-            th[k] = ts[src];
+            x[k] = gx[src];
+            y[k] = gy[src];
+            th[k] = gt[src];
         }
     } else if (rflag == 1) {
         // bracket: the sources of the block's first and last positions (two
