@@ -752,7 +752,7 @@ def main():
             t0 = time.perf_counter()
             pf.run(s0 + args.warmup, ctl[s0 + args.warmup:s0 + args.warmup + ns_steps])
             barrier_sync()
-            return time.perf_counter() - t0
+            return time.perf_counter() - t0, pf.rng_ring_info()
         finally:
             pf.close()
 
@@ -834,10 +834,10 @@ def main():
                                          "ms_per_step": e2 * 1e3 / args.steps,
                                          "fused_avg_ms": f2 * 1e3,
                                          "roofline": fused_roofline("product", n_rank, f2)}}
-        e4 = measure_numpy_stream(args.likelihood)
+        e4, ring = measure_numpy_stream(args.likelihood)
         line["alt_modes"]["numpy_stream"] = {
             "value": NP_PER_GPU * NL * ns_steps / e4, "ms_per_step": e4 * 1e3 / ns_steps,
-            "steps": ns_steps,
+            "steps": ns_steps, "ring": ring,
             "note": "the reference's own noise stream (MT19937 + polar normals, bit-identical to "
                     "np.random) drawn on the device with the observations simulated there"}
     if world == 1 and args.mode == "replicas" and not strong:

@@ -519,6 +519,9 @@ int slam_pf_set_rng_mt19937(slam_pf* h, const uint32_t* key, int32_t pos, int32_
                             double gauss, const double* r_factor);
 int slam_pf_get_rng_mt19937(slam_pf* h, uint32_t* key, int32_t* pos, int32_t* has_gauss,
                             double* gauss);
+/* the device stream's word ring: out[4] = ring bytes, segments per refill
+ * round, words per segment, requests one round feeds (at least) */
+int slam_pf_rng_mt19937_info(slam_pf* h, int64_t* out);
 int slam_pf_step_truth(slam_pf* h, const double* control, const double* truth, double* z_out,
                        slam_pf_result* res);
 /* device-resident batch: truth[n_steps][4]; slam_pf_run then simulates the

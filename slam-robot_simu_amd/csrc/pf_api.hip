@@ -1282,6 +1282,17 @@ int slam_pf_get_rng_mt19937(slam_pf* h, uint32_t* key, int32_t* pos, int32_t* ha
     return mt_get_state(h->mtb, key, pos, has_gauss, gauss, h->stream);
 }
 
+int slam_pf_rng_mt19937_info(slam_pf* h, int64_t* out) {
+    SLAM_ARG_CHECK(h && out, "slam_pf_rng_mt19937_info: NULL argument");
+    SLAM_ARG_CHECK(h->mt, "slam_pf_rng_mt19937_info: the device stream is not enabled");
+    const MtBuffers& b = h->mtb;
+    out[0] = b.cap * (int64_t)sizeof(uint32_t);
+    out[1] = b.R;
+    out[2] = b.S;
+    out[3] = b.need > 0 ? (int64_t)b.R * b.S / b.need : 0;
+    return SLAM_OK;
+}
+
 int slam_pf_step_truth(slam_pf* h, const double* control, const double* truth, double* z_out,
                        slam_pf_result* res) {
     SLAM_ARG_CHECK(h && control && truth, "slam_pf_step_truth: NULL argument");

@@ -45,11 +45,11 @@ constexpr int kMtEmitSumMax = SLAM_MT_EMIT_SUM_MAX;
 // requests one parallel round feeds: the jump (~160 us, LDS-bound) is paid
 // once per round, the sequential generation grows with it; 4 -> 16 took the
 // device stream from 0.229 to 0.201 ms per 2^20-particle step, 16 -> 32 from
-// 0.150 to 0.145, 32 -> 64 (round 4) from 0.121 to 0.118 (the ring is ~8 GB
+// 0.150 to 0.145, 32 -> 64 (round 4) from 0.121 to 0.118 (the ring is 2 GB
 // at that request size, the one-time priming ~300 ms).  Larger requests feed
 // fewer (at least 4) so that the ring stays within kMtRingWordsMax.
 constexpr int64_t kMtRoundsAhead = 64;
-constexpr int64_t kMtRingWordsMax = int64_t(1) << 31;     // 8 GB of words
+constexpr int64_t kMtRingWordsMax = int64_t(1) << 29;     // 2 GB of words
 
 // ------------------------------------------------------------------ kernels
 
@@ -692,8 +692,10 @@ int mt_reserve(MtBuffers& b, int64_t g_cap, int64_t pre_cap, int device) {
     if (b.R < 1) b.R = 1;
     // R > 1: a round covers kMtRoundsAhead requests, so the jump (a fixed
     // cost per round) is paid once per that many requests
-    // segment length and live words ([p - 624, g1) with g1 - p < need + R S,
-    // plus the round being written) for a given number of requests per round
+    // segment length and live words for a given number of requests per round:
+    // the ring holds [p - 624, g1 + R S) while a round writes (it runs only
+    // when g1 - p < need) and [p - 624, g1) with g1 - p < need + R S after it,
+    // so need + R S + a few blocks (round 5; the round-4 bound counted R S twice)
     auto seg_len = [&](int64_t ahead) {
         const int64_t span = b.R > 1 ? ahead * b.need : b.need;
         int64_t S = (span + (int64_t)b.R * kMtN - 1) / ((int64_t)b.R * kMtN) * kMtN;
@@ -702,7 +704,7 @@ int mt_reserve(MtBuffers& b, int64_t g_cap, int64_t pre_cap, int device) {
     };
     auto live_words = [&](int64_t S) {
         const int64_t RS = (int64_t)b.R * S;
-        return std::max<int64_t>(b.need + 2 * RS + 4 * kMtN, RS + 3 * kMtN);
+        return std::max<int64_t>(b.need + RS + 4 * kMtN, RS + 3 * kMtN);
     };
     int64_t ahead = kMtRoundsAhead;
     while (ahead > 4 && live_words(seg_len(ahead)) > kMtRingWordsMax) ahead >>= 1;

@@ -116,6 +116,7 @@ SIGNATURES = {
     "slam_glibc_log": (C.c_int, [C.c_int64, _D, _D]),
     "slam_mt_jump_window": (C.c_int, [_U32, C.c_uint64, _U32]),
     "slam_pf_set_rng_mt19937": (C.c_int, [_P, _U32, C.c_int32, C.c_int32, C.c_double, _D]),
+    "slam_pf_rng_mt19937_info": (C.c_int, [_P, C.POINTER(C.c_int64)]),
     "slam_pf_get_rng_mt19937": (C.c_int, [_P, _U32, _I32, _I32, _D]),
     "slam_pf_step_truth": (C.c_int, [_P, _D, _D, _D, C.POINTER(PFResult)]),
     "slam_pf_load_truth": (C.c_int, [_P, C.c_int32, _D]),

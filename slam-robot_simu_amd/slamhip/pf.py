@@ -334,6 +334,13 @@ class DeviceParticleFilter:
                                                 dptr(rf)), "slam_pf_set_rng_mt19937")
         self.mt = True
 
+    def rng_ring_info(self):
+        """The device stream's word ring (slam_pf_rng_mt19937_info): bytes,
+        segments per refill round, words per segment, requests per round."""
+        out = (C.c_int64 * 4)()
+        check(self._lib.slam_pf_rng_mt19937_info(self._h, out), "slam_pf_rng_mt19937_info")
+        return dict(ring_bytes=out[0], segments=out[1], segment_words=out[2], requests_per_round=out[3])
+
     def rng_state(self):
         """The device stream's state as an np.random.get_state() tuple."""
         key = np.empty(624, dtype=np.uint32)

@@ -146,7 +146,7 @@ def test_comm_one_rank_rccl():
         comm.close()
 
 
-def _rank_main(rank, world, n, lm, zs, ctl, q_out, q_in, conn):
+def _rank_main(rank, world, n, lm, zs, ctl, q_out, q_in, conn, kw=None):
     sys.path.insert(0, os.path.join(os.path.dirname(HERE), "slam-robot_simu_amd"))
     from slamhip.dist import DistFilter
 
@@ -156,7 +156,7 @@ def _rank_main(rank, world, n, lm, zs, ctl, q_out, q_in, conn):
 
     try:
         d = DistFilter(n, lm, world=world, rank=rank, all_gather=all_gather, motion="velocity",
-                       likelihood="logsum", seed=8)
+                       likelihood="logsum", seed=8, **(kw or {}))
         d.load_observations(zs)
         merged = d.set_merged(None)
         res = d.run(0, ctl)
@@ -167,19 +167,23 @@ def _rank_main(rank, world, n, lm, zs, ctl, q_out, q_in, conn):
         q_out.put((rank, repr(e), None))
 
 
-@pytest.mark.parametrize("world", [2, 4])
-def test_dist_two_processes_share_one_gpu(world):
+@pytest.mark.parametrize("world,tight", [(2, False), (4, False), (3, True)])
+def test_dist_two_processes_share_one_gpu(world, tight):
     """Two (four) ranks, one process each, one GPU: the IPC path of one process
     per GPU (exchange regions exported / opened, device-side signalling across
-    processes), replayed as hipGraphs; compared with one handle."""
+    processes), replayed as hipGraphs; compared with one handle.  tight: a
+    sharp likelihood (R = 0.1^2 I) and a resample every step, so a few
+    particles carry the weight and their runs span whole shards -- the
+    merged exchange's runs stored into peers' regions, with their carries."""
     from slamhip.pf import DeviceParticleFilter
     n, nl, steps = world * 65536, 50, 16
     lm, zs, p = _world(n, nl, steps, 23)
+    kw = dict(r=np.diag([0.1, 0.1]) ** 2, ess_threshold=float(n)) if tight else {}
     ctl = np.tile([p.vel, p.omega], (steps, 1))
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     pipes = [ctx.Pipe() for _ in range(world)]
-    procs = [ctx.Process(target=_rank_main, args=(r, world, n, lm, zs, ctl, q, None, pipes[r][1]))
+    procs = [ctx.Process(target=_rank_main, args=(r, world, n, lm, zs, ctl, q, None, pipes[r][1], kw))
              for r in range(world)]
     for pr in procs:
         pr.start()
@@ -200,10 +204,14 @@ def test_dist_two_processes_share_one_gpu(world):
             pr.join(timeout=60)
             if pr.is_alive():
                 pr.kill()
-    with DeviceParticleFilter(n, lm, motion="velocity", likelihood="logsum", seed=8) as single:
+    with DeviceParticleFilter(n, lm, motion="velocity", likelihood="logsum", seed=8, **kw) as single:
         single.load_observations(zs)
         ref = single.run(0, ctl)
         xs = single.get_state()
+    if tight:
+        assert all(r["resampled"] for r in ref[1:])
+        print("tight ess", [round(r["ess"], 1) for r in ref])
+        assert min(r["ess"] for r in ref) < n / 1000             # a few particles serve long runs
     for rank in range(world):
         res, st = out[rank]
         assert st[4], "one shard per process: the one-launch resample exchange"

@@ -59,6 +59,32 @@ def test_interleaved_calls_match_numpy():
             _same_state(d.get_state(), rs.get_state())
 
 
+def test_many_requests_cross_refill_rounds():
+    """200 requests of one size: the word ring refills about three times and
+    wraps (it holds one round plus one request, rng_api.hip mt_reserve), every
+    request bit-exact."""
+    from slamhip.rng import DeviceRandomState
+    rs = np.random.RandomState(31)
+    with DeviceRandomState(rs, device=0) as d:
+        for k in range(200):
+            out, ref = d.standard_normal(100001), rs.standard_normal(100001)
+            bad = np.flatnonzero(_bits(out) != _bits(ref))
+            assert bad.size == 0, (k, bad[:5])
+        _same_state(d.get_state(), rs.get_state())
+
+
+def test_bench_size_ring_within_2gb():
+    """The 2^20-particle handle's ring (<= 2 GB) still feeds
+    64 requests per refill round."""
+    from slamhip.pf import DeviceParticleFilter
+    lm = np.random.RandomState(2).uniform(-10, 10, (100, 2))
+    with DeviceParticleFilter(1 << 20, lm, motion="velocity", likelihood="logsum") as d:
+        d.use_numpy_stream(np.random.RandomState(5))
+        info = d.rng_ring_info()
+    assert info["ring_bytes"] <= 2 << 30, info
+    assert info["requests_per_round"] >= 64, info
+
+
 def _expected_state_after(seed, steps, resampled, n, nl):
     """np.random after the reference's draws: [rand() if resampling] ->
     mvn(Q, n) -> mvn(R, nl) per step (standard_normal counts)."""
