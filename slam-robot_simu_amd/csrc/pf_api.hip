@@ -649,7 +649,9 @@ int launch_step(slam_pf* h, bool host_noise) {
         host_noise = true;
     }
     tic(h, 2);
+#ifndef SLAM_NO_SCAN_LAUNCH       // A/B diagnostic only: wrong on resample steps
     if ((rc = launch_scans(h, 0, false))) return rc;
+#endif
     toc(h, 2);
     if ((rc = launch_fused(h, h->cfg.motion, host_noise))) return rc;
     return launch_reduce(h, -1);

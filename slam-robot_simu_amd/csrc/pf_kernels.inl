@@ -876,7 +876,7 @@ __device__ __forceinline__ int likelihood_lanes(const double* xn, const double* 
                                                  const double* __restrict__ lm,
                                                  const double* __restrict__ z,
                                                  const double* __restrict__ zc, const LikConst& lc,
-                                                 double* bn, const int wave_s) {
+                                                 double* bn, const int wave_s, const double* pw) {
     const int nl = lc.nl;
     if (LIK == SLAM_LIK_PRODUCT) {
         // the exp table in LDS, t.x halved for exp_nhalf (every lane of the
@@ -1060,6 +1060,15 @@ __device__ __forceinline__ int likelihood_lanes(const double* xn, const double* 
     for (int k = 0; k < P; ++k) {
         bn[k] = exp_lean(L[k]);
         slow[k] = !(L[k] >= lc.fast_min_l);                 // also NaN
+        // a zero previous weight makes the weight 0 for any finite likelihood,
+        // and below fast_min_l the likelihood is finite (a NaN L still goes
+        // the reference's way): the exact product is not needed
+#ifndef SLAM_NO_ZERO_SKIP                                   // A/B diagnostic
+        if (slow[k] && pw[k] == 0.0 && !isnan(L[k])) {
+            slow[k] = false;
+            bn[k] = 0.0;
+        }
+#endif
 #ifdef SLAM_PROBE_NO_SLOW                                  // timing probe only: not exact
         slow[k] = false;
 #endif
@@ -1323,6 +1332,13 @@ __device__ __forceinline__ void pf_fused_tile(
     }
 
     FPROBE(3, xv[P - 1] + sp[P - 1]);
+    // previous weights: particle_filter.py:222 (a resampled step starts from
+    // 1/NP) / :235-236 (deferred: w_un / s, NaN -> 1/NP)
+    double pw[P];
+    const double s_prev = DEFER ? *s_in : 1.0;
+#pragma unroll
+    for (int k = 0; k < P; ++k)
+        pw[k] = rflag ? pc.np_recip : (DEFER ? norm_w(wprev[k], s_prev, pc.np_recip) : wprev[k]);
     // ---- likelihood and weight (particle_filter.py:170-198)
     double bn[P];
 #ifdef SLAM_PROBE_NO_LIK                                   // timing probe only: not exact
@@ -1331,20 +1347,13 @@ __device__ __forceinline__ void pf_fused_tile(
     const int lane_dd = 0;
 #else
     const int lane_dd = likelihood_lanes<LIK, P>(xv, yv, sp, cp, lm, zs,
-                                                 io.zc + (size_t)st * kZcWords, lc, bn, wave_s);
+                                                 io.zc + (size_t)st * kZcWords, lc, bn, wave_s, pw);
 #endif
     FPROBE(4, bn[P - 1]);
     if (__ballot(lane_dd) != 0 && __lane_id() == 0) atomicAdd(&flags[kFlagDDWaves], 1);
-    // previous weights: particle_filter.py:222 (a resampled step starts from
-    // 1/NP) / :235-236 (deferred: w_un / s, NaN -> 1/NP)
     double wv[P];
-    const double s_prev = DEFER ? *s_in : 1.0;
 #pragma unroll
-    for (int k = 0; k < P; ++k) {
-        const double pw = rflag ? pc.np_recip
-                                : (DEFER ? norm_w(wprev[k], s_prev, pc.np_recip) : wprev[k]);
-        wv[k] = valid[k] ? pw * bn[k] : 0.0;                     // particle_filter.py:194
-    }
+    for (int k = 0; k < P; ++k) wv[k] = valid[k] ? pw[k] * bn[k] : 0.0;   // particle_filter.py:194
     if constexpr (DEFER) {
 #pragma unroll
         for (int h = 0; h < P; h += 2)

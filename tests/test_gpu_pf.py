@@ -173,6 +173,34 @@ def test_step_covariance_vs_oracle(slamhip_pf):
             assert rd["resample_next"] == (ess_after < p.ess_th)
 
 
+def test_never_resampling_filter_degenerate_weights(slamhip_pf):
+    """ESS threshold 0: the filter never resamples, the weights degenerate and
+    most particles reach weight 0 while their likelihood falls below the
+    closed form's range (fast_min_l).  Those skip the exact sequential product
+    (0 x any finite likelihood is 0); the weights, zero set included, and the
+    estimate still follow the reference step by step."""
+    rs = np.random.RandomState(12)
+    n, nl = 4000, 30
+    lm = rs.uniform(-10, 10, (nl, 2))
+    p = po.PFParams(n_particles=n, landmarks=lm)
+    p.ess_th = 0.0
+    orc = po.PFOracle(p)
+    with slamhip_pf.DeviceParticleFilter(n, lm, likelihood="logsum", ess_threshold=0.0) as d:
+        world = po.PFWorld(p)
+        np.random.seed(4)
+        for k in range(30):
+            world.advance()
+            noise = np.random.multivariate_normal([0.0, 0.0, 0.0], p.q, n)
+            z = world.observe()
+            ro = orc.step(z, noise, None)
+            rd = d.step((p.vel, p.omega), z, noise, np.nan)
+            assert not rd["resampled"]
+            assert rd["max_idx"] == ro["max_idx"], k
+            np.testing.assert_allclose(rd["x_est"], ro["x_est"], rtol=1e-6)
+            weights_match(d.get_state()[3], orc.w, rtol=1e-9, floor=1e-290)
+        assert np.count_nonzero(orc.w == 0) > n // 2       # the regime the skip serves
+
+
 @pytest.mark.parametrize("motion", ["linear", "velocity"])
 def test_device_rng_run_tracks_truth(slamhip_pf, motion):
     """Device-resident run (bench path): on-device Philox noise, device-decided
