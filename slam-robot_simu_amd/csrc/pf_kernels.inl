@@ -783,6 +783,13 @@ __device__ __forceinline__ double ref_q(const double xn, const double yn, const 
     return q;
 }
 
+// double from/to lane l (uniform result, SGPR-held)
+__device__ __forceinline__ double readlane_d(const double v, const int l) {
+    const int lo = __builtin_amdgcn_readlane(__double2loint(v), l);
+    const int hi = __builtin_amdgcn_readlane(__double2hiint(v), l);
+    return __hiloint2double(hi, lo);
+}
+
 // double-double a + b (TwoSum of the high parts, low parts added, renormalised)
 __device__ __forceinline__ void dd_add(double& ah, double& al, const double bh, const double bl) {
     const double t = ah + bh;
@@ -846,10 +853,28 @@ __device__ SLAM_SLOW_ATTR double logsum_slow(const double xn, const double yn, c
         ch = __shfl(th, 63, 64);
         cl = __shfl(tl, 63, 64);
     }
+    // the exact tail: the factors of 64 landmarks at a time, one per lane,
+    // then the reference's left-to-right product over them (round 5: the
+    // factors used to be formed inside the serial loop, ~60 issue slots per
+    // landmark for the whole wave -- several us per slow particle)
     double acc = exp_lean(s_prev);           // s_prev = 0 -> exactly 1 (j0 = 0)
+#ifdef SLAM_SLOW_SERIAL_TAIL                                 // A/B diagnostic: the round-4 form
     for (int j = j0; j < nl; ++j) {
         acc = acc * ref_factor(xn, yn, sp, cp, lm[2 * j], lm[2 * j + 1], z[2 * j], z[2 * j + 1], lc);
         if (acc == 0.0) break;
+    }
+    return acc;
+#endif
+    for (int base = j0; base < nl && acc != 0.0; base += 64) {
+        const int j = base + lane;
+        const double f = (j < nl) ? ref_factor(xn, yn, sp, cp, lm[2 * j], lm[2 * j + 1], z[2 * j],
+                                               z[2 * j + 1], lc)
+                                  : 1.0;
+        const int cnt = (nl - base < 64) ? nl - base : 64;
+        for (int l = 0; l < cnt; ++l) {
+            acc = acc * readlane_d(f, l);
+            if (acc == 0.0) break;
+        }
     }
     return acc;
 }
@@ -2370,12 +2395,6 @@ __device__ __forceinline__ void wave_tile_stage(const int64_t tile, const TileSc
     }
 }
 
-// double from/to lane l (uniform result, SGPR-held)
-__device__ __forceinline__ double readlane_d(const double v, const int l) {
-    const int lo = __builtin_amdgcn_readlane(__double2loint(v), l);
-    const int hi = __builtin_amdgcn_readlane(__double2hiint(v), l);
-    return __hiloint2double(hi, lo);
-}
 
 // The lean path's place + fold (last block of pass A): the M specials, in
 // global order, are located in the tiles' staging areas (tile offsets bofff in
