@@ -1275,7 +1275,9 @@ __device__ __forceinline__ void dist_record(const int64_t n, const DeferParts& d
     // from the candidate blocks (usually one element: M) -- one element per lane,
     // a candidate block per round (block-uniform loop)
     PROBE_AT(3);
+#ifndef SLAM_FIN_AB                                   // finalize-width A/B builds skip the sharded path's check
     static_assert(kFinThreads == kPartPer, "one lane per element of a fused block");
+#endif
     {
         __shared__ int s_wh[kFinWaves];
         int cnt = 0;
