@@ -24,7 +24,8 @@ fused block (or per resample run) where it is local:
   marks3    one block also accepts step 3's run marks (a tag test that fails);
   misrun    one run's start mark missed: its positions take the previous
             run's source;
-  noreset   (global) the post-resample weights are not reset to 1/NP.
+  noreset   (global) the post-resample weights are not reset to 1/NP;
+  lost / stale5 again per 128-, 256-, 1024-, 2048-, 4096- and 8192-element unit.
 
 Prints the best fit of each (max relative error over the six distinct entries
 of ACTUAL, which the log printed to 7 digits: a true cause fits to ~1e-6).
@@ -236,7 +237,17 @@ def main():
         S = tuple(m.sum(0) for m in unit_moments(X, Y, T, wp * L))
         print(f"{nm:9s} global fit {err(cov_of(*S)):.3g}")
 
-    # two-unit combinations of the best 64 units of each local hypothesis
+    # the one-unit hypotheses at every granularity a hand-off could
+    # have (a 128-element leaf ... an 8192-element np.sum buffer), lost and stale5
+    Pb6 = np.vstack([X - ref[0], Y - ref[1], T - ref[2]])
+    Pb5 = np.vstack([X5 - ref5[0], Y5 - ref5[1], T5 - ref5[2]])
+    for size in (128, 256, 1024, 2048, 4096, 8192):
+        m = n // size
+        base_s = moments(w_un, Pb6, m)
+        tot_s = tuple(q.sum(0) for q in base_s)
+        zero_s = (np.zeros(m), np.zeros((m, 3)), np.zeros((m, 3, 3)))
+        best_local(f"lost@{size}", tot_s, zero_s, base_s)
+        best_local(f"stale5@{size}", tot_s, moments(w_prev5 * L5, Pb5, m), base_s)
     print("(a true cause fits to ~1e-6, the printing precision of ACTUAL)")
     return results
 
