@@ -419,10 +419,17 @@ int slam_dist_create(slam_pf** shards, int32_t n_held, int32_t world, int32_t ra
             return bail(fail(SLAM_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_))); \
     } while (0)
     DIST_TRY(hipSetDevice(d->device));
-    // the largest shard sets the slot sizes (shards are equal but the last)
+    // the largest shard sets the slot sizes (shards are equal but the last);
+    // every rank must lay its region out the same way, so one shard per
+    // process takes the standard split's full shard (rank 0's: ceil(N / world)
+    // rounded up to whole np.sum buffers), not ceil(N / world) itself
     int64_t nmax = 0;
     for (auto* h : d->sh) nmax = std::max(nmax, h->n);
-    if (!d->local) nmax = std::max<int64_t>(nmax, (N + world - 1) / world);
+    if (!d->local) {
+        int64_t g0 = 0, nfull = 0;
+        slam_dist_shard_range(N, world, 0, &g0, &nfull);
+        nmax = std::max<int64_t>(nmax, nfull);
+    }
     const int64_t nch = (nmax + kSumChunk - 1) / kSumChunk;
     DistLayout& L = d->L;
     L.rec_stride = ((int64_t)sizeof(DistRec) + 8 * nch + 255) / 256 * 256;

@@ -167,16 +167,18 @@ def _rank_main(rank, world, n, lm, zs, ctl, q_out, q_in, conn, kw=None):
         q_out.put((rank, repr(e), None))
 
 
-@pytest.mark.parametrize("world,tight", [(2, False), (4, False), (3, True)])
-def test_dist_two_processes_share_one_gpu(world, tight):
+@pytest.mark.parametrize("world,tight,extra", [(2, False, 0), (4, False, 0), (3, True, 0),
+                                               (2, True, 1000), (2, False, 1000)])
+def test_dist_two_processes_share_one_gpu(world, tight, extra):
     """Two (four) ranks, one process each, one GPU: the IPC path of one process
     per GPU (exchange regions exported / opened, device-side signalling across
     processes), replayed as hipGraphs; compared with one handle.  tight: a
     sharp likelihood (R = 0.1^2 I) and a resample every step, so a few
     particles carry the weight and their runs span whole shards -- the
-    merged exchange's runs stored into peers' regions, with their carries."""
+    merged exchange's runs stored into peers' regions, with their carries.
+    extra: particles beyond whole shards (a ragged last shard: 73,728 + 58,344)."""
     from slamhip.pf import DeviceParticleFilter
-    n, nl, steps = world * 65536, 50, 16
+    n, nl, steps = world * 65536 + extra, 50, 16
     lm, zs, p = _world(n, nl, steps, 23)
     kw = dict(r=np.diag([0.1, 0.1]) ** 2, ess_threshold=float(n)) if tight else {}
     ctl = np.tile([p.vel, p.omega], (steps, 1))
