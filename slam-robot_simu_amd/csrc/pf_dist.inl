@@ -131,9 +131,23 @@ __device__ __forceinline__ int dist_push_hi(const DistPeers& P) { return P.coll 
 // stores the flags.  Data that other blocks stored earlier in the launch was
 // written with system-scope stores (dist_store_item) and had completed before
 // their tickets.
+// One rank (world 1): no peer to publish to -- every wait on the flags is the
+// same block's (or a later launch's, behind the kernel boundary), and every
+// read of the published data is a system-scope load, so the block's drained
+// stores and a barrier are enough (SLAM_DIST_W1_FLAGS keeps the flags, A/B).
+__device__ __forceinline__ bool dist_single_rank(const DistPeers& P) {
+#ifdef SLAM_DIST_W1_FLAGS
+    (void)P;
+    return false;
+#else
+    return P.world == 1;
+#endif
+}
+
 __device__ __forceinline__ void dist_signal(const DistPeers& P, const int kind, const uint64_t epoch) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    if (dist_single_rank(P)) return;
     if (threadIdx.x == 0) {
         __threadfence_system();
         for (int q = dist_push_lo(P); q < dist_push_hi(P); ++q)
@@ -171,7 +185,7 @@ __device__ __forceinline__ void dist_mark_dead(int32_t* flags) {
 // (bounded: ~2^24 polls, ~20 s, then status bit kDistStWait and proceed)
 __device__ __forceinline__ void dist_wait(const DistPeers& P, const int kind, const uint64_t epoch,
                                           int32_t* flags) {
-    if ((int)threadIdx.x < P.world) {
+    if ((int)threadIdx.x < P.world && !dist_single_rank(P)) {
         const uint64_t* f = dist_flags(P, P.rank) + kind * kDistMaxWorld + threadIdx.x;
         if (dist_dead(flags)) {
             atomicOr(&flags[kFlagStatus], kDistStWait);
