@@ -623,22 +623,26 @@ __global__ __launch_bounds__(256) void dist_unpack_kernel(
 // ---------------------------------------------------------------- resample, one launch
 // The whole exchange side of a resample step in ONE launch (one shard per
 // process; the grid must be co-resident -- checked on the host -- because its
-// blocks wait for one another twice):
+// blocks wait for one another):
 //   A  every wave classifies its 512-element tile of w = w_un / s with the
 //      global approximate prefix (the lean exact cumsum's pass A) and stages its
 //      special elements; the last block scans the tile totals, pushes this
 //      rank's specials (global index, rank-local increment prefix) into every
 //      peer's slot, waits for every rank's, folds the global list in rank
-//      order (one wave, 63 specials per round) and releases the grid;
+//      order (one wave, 63 specials per round), derives the first positions
+//      this rank's and the next rank's sources serve (lo0, hi0) and releases
+//      the grid;
 //   B  every wave expands its tile's exact cumsum from the classification it
 //      kept in registers, counts the systematic positions at or below each
-//      c_j (a run [s_j, e_j) per selected source) and the block's selected
-//      sources, per destination rank too; the last block scans the counts and
-//      releases the grid again;
-//   C  every selected source is pushed, clipped to each destination's
-//      positions, into that destination's item slot for this rank; the last
-//      block publishes the counts and signals kXItem.
-// dist_unpack_kernel then hands the received items to the fused kernel.
+//      c_j (a run [s_j, e_j) per selected source) and places every run where
+//      its positions are (dist_place_runs): this rank's part as the fused
+//      kernel's run marks and carries, a peer's part at its first local
+//      position in that peer's region.  World 1 ends here;
+//   D  the last block publishes kXItem, waits for every rank's and releases
+//      the grid; every block takes the positions other ranks serve
+//      ([0, lo0) and [hi0, n) locally) from its region (dist_take_runs).
+// The five-launch form (grids that are not co-resident) packs the items
+// instead and dist_unpack_kernel hands them to the fused kernel.
 constexpr int kDistTokenWait = 1 << 22;
 constexpr int kDistBfLds = 2048;            // block offsets staged in LDS (nb_scan <= 2048: n <= 2^22)
 
