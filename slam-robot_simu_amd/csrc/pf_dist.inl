@@ -522,7 +522,7 @@ __global__ void dist_publish_kernel(const DistPeers P, const int kind, const Ste
 // gather (the single-GPU expand pass's inverse map): item k (ranks in order,
 // each rank's items in position order) is stored at local index k of the
 // particle arrays -- the pre-resample particles were packed already -- with a
-// run mark (mark generation | k) at its first local position and the carry of
+// run mark (mark generation | npad + k: DeferParts.goff) at its first local position and the carry of
 // every fused block whose first position it covers.  Items never outnumber the
 // positions (disjoint, non-empty ranges), so k < n.  The last block checks that
 // the ranges tile the shard (status kDistStItems otherwise).  The resample flag
@@ -603,7 +603,7 @@ __device__ void dist_unpack_items(const int64_t n, double* __restrict__ xs, doub
 // gather (the single-GPU expand pass's inverse map): item k (ranks in order,
 // each rank's items in position order) is stored at local index k of the
 // particle arrays -- the pre-resample particles were packed already -- with a
-// run mark (mark generation | k) at its first local position and the carry of
+// run mark (mark generation | npad + k: DeferParts.goff) at its first local position and the carry of
 // every fused block whose first position it covers.  Items never outnumber the
 // positions (disjoint, non-empty ranges), so k < n.  The last block checks that
 // the ranges tile the shard (status kDistStItems otherwise).  The resample flag
