@@ -37,6 +37,8 @@ constexpr int kFinRegBlocks = 2048 / kFinThreads;   // fused blocks held in regi
 constexpr int kFinLeafLanes = 4;            // lanes per 8192-element buffer (16 leaves each)
 constexpr int kFinBufPerRound = kFinThreads / kFinLeafLanes;   // 128 buffers per round
 constexpr int kFinCand = 8;                 // argmax candidate records staged in LDS
+constexpr int kFinBatch = 8;                // loads in flight per lane beyond the registers (NP > 2^20)
+constexpr int kFinSumBatch = 2;             // blocks (12 loads each) in flight in the sums pass
 
 struct FinRecord {
     double pre, xe[3];
@@ -157,8 +159,20 @@ __global__ __launch_bounds__(kFinThreads) void finalize_deferred_kernel(
     for (int k = 0; k < kFinRegBlocks; ++k)
         if (has[k]) mlane = fmax(mlane, pm[k]);
     // NP > 2^20: blocks beyond the registers (two passes: max, then sums)
+    // (round 5: every loop over the blocks beyond the registers issues a batch
+    // of loads before it uses them -- one memory round trip per iteration made
+    // the 2^23-particle finalize 50-110 us; the adds keep their order)
     const int64_t bx0 = tid + (int64_t)kFinThreads * kFinRegBlocks;
-    for (int64_t b = bx0; b < nb; b += kFinThreads) mlane = fmax(mlane, dp.pmax[b]);
+    for (int64_t b0 = bx0; b0 < nb; b0 += kFinBatch * (int64_t)kFinThreads) {
+        double v[kFinBatch];
+#pragma unroll
+        for (int u = 0; u < kFinBatch; ++u) {
+            const int64_t b = b0 + (int64_t)u * kFinThreads;
+            v[u] = (b < nb) ? dp.pmax[b] : -1.0;
+        }
+#pragma unroll
+        for (int u = 0; u < kFinBatch; ++u) mlane = fmax(mlane, v[u]);
+    }
     double acc[11];
 #pragma unroll
     for (int j = 0; j < 11; ++j) acc[j] = 0.0;
@@ -174,12 +188,26 @@ __global__ __launch_bounds__(kFinThreads) void finalize_deferred_kernel(
                 for (int j = 2; j < 11; ++j) acc[j] += r * q[k][j];
             }
         }
-        for (int64_t b = bx0; b < nb; b += kFinThreads) {
-            const double r = dp.pmax[b] * rm;
-            acc[0] += r * dp.ps[0][b];
-            acc[1] += (r * r) * dp.ps[1][b];
+        for (int64_t b0 = bx0; b0 < nb; b0 += kFinSumBatch * (int64_t)kFinThreads) {
+            double pv[kFinSumBatch], qv[kFinSumBatch][11];
 #pragma unroll
-            for (int j = 2; j < 11; ++j) acc[j] += r * dp.ps[j][b];
+            for (int u = 0; u < kFinSumBatch; ++u) {
+                const int64_t b = b0 + (int64_t)u * kFinThreads;
+                const int64_t bb = (b < nb) ? b : b0;
+                pv[u] = dp.pmax[bb];
+#pragma unroll
+                for (int j = 0; j < 11; ++j) qv[u][j] = dp.ps[j][bb];
+            }
+#pragma unroll
+            for (int u = 0; u < kFinSumBatch; ++u) {
+                if (b0 + (int64_t)u * kFinThreads < nb) {
+                    const double r = pv[u] * rm;
+                    acc[0] += r * qv[u][0];
+                    acc[1] += (r * r) * qv[u][1];
+#pragma unroll
+                    for (int j = 2; j < 11; ++j) acc[j] += r * qv[u][j];
+                }
+            }
         }
     }
     const double mx = wave_max_f64(mlane);
@@ -286,8 +314,19 @@ __global__ __launch_bounds__(kFinThreads) void finalize_deferred_kernel(
         for (int k = kFinRegBlocks - 1; k >= 0; --k)
             if (has[k] && pm[k] >= M * (1.0 - 0x1p-48) && pm[k] / s == mval)
                 cb = (unsigned long long)fin_blk(tid, k);
-        for (int64_t b = tid + (int64_t)kFinThreads * kFinRegBlocks; b < nb; b += kFinThreads)
-            if (cb == ~0ull && dp.pmax[b] / s == mval) cb = (unsigned long long)b;
+        for (int64_t b0 = bx0; b0 < nb && cb == ~0ull; b0 += kFinBatch * (int64_t)kFinThreads) {
+            double v[kFinBatch];
+#pragma unroll
+            for (int u = 0; u < kFinBatch; ++u) {
+                const int64_t b = b0 + (int64_t)u * kFinThreads;
+                v[u] = (b < nb) ? dp.pmax[b] : -1.0;
+            }
+#pragma unroll
+            for (int u = 0; u < kFinBatch; ++u) {
+                const int64_t b = b0 + (int64_t)u * kFinThreads;
+                if (cb == ~0ull && b < nb && v[u] / s == mval) cb = (unsigned long long)b;
+            }
+        }
         if (cb != ~0ull) atomicMin(&s_min, cb);
         __syncthreads();
         const int64_t bc = (int64_t)s_min;
@@ -400,16 +439,34 @@ __global__ __launch_bounds__(kFinThreads) void finalize_deferred_kernel(
         };
         const int per = (int)((nb + kFinThreads - 1) / kFinThreads);
         const int64_t b0 = (int64_t)tid * per;
+        // batches of kFinBatch totals (their loads together), then the adds in order
+        auto btot_batch = [&](const int k0, double (&t)[kFinBatch]) {
+#pragma unroll
+            for (int u = 0; u < kFinBatch; ++u) {
+                const int64_t b = b0 + k0 + u;
+                t[u] = (k0 + u < per && b < nb) ? btot(b) : 0.0;
+            }
+        };
         double loc = 0.0;
-        for (int k = 0; k < per; ++k)
-            if (b0 + k < nb) loc += btot(b0 + k);
+        for (int k0 = 0; k0 < per; k0 += kFinBatch) {
+            double t[kFinBatch];
+            btot_batch(k0, t);
+#pragma unroll
+            for (int u = 0; u < kFinBatch; ++u)
+                if (k0 + u < per && b0 + k0 + u < nb) loc += t[u];
+        }
         double total;
         double ex = block_excl_scan<double, kFinThreads>(loc, s_q[0], total);
-        for (int k = 0; k < per; ++k)
-            if (b0 + k < nb) {
-                boff[b0 + k] = ex;
-                ex = ex + btot(b0 + k);
-            }
+        for (int k0 = 0; k0 < per; k0 += kFinBatch) {
+            double t[kFinBatch];
+            btot_batch(k0, t);
+#pragma unroll
+            for (int u = 0; u < kFinBatch; ++u)
+                if (k0 + u < per && b0 + k0 + u < nb) {
+                    boff[b0 + k0 + u] = ex;
+                    ex = ex + t[u];
+                }
+        }
         if (tid == 0) boff[nb] = total;
     }
     FIN_STAMP(5);

@@ -4,7 +4,8 @@ process per round, measured as bench.py does -- graphs captured, 124 settle
 steps, 5 warm-up, 50 timed steps, then an event pass over 49 more.
 
     python tools/variant_ab.py ROUNDS LIB [LIB ...]      (LIB: file name under slamhip/)
-    VB_LIK=product for the product likelihood; VB_ESS=<threshold> (0: never resample)
+    VB_LIK=product for the product likelihood; VB_ESS=<threshold> (0: never resample);
+    VB_NP=<particles> (default the bench's 2^20)
 """
 import os
 import subprocess
@@ -25,7 +26,8 @@ def child():
     lm, zs, (vel, omega, dt) = bench.simulate_world(total)
     ctl = np.tile([vel, omega], (total, 1))
     kw = {"ess_threshold": float(os.environ["VB_ESS"])} if "VB_ESS" in os.environ else {}
-    pf = DeviceParticleFilter(bench.NP_PER_GPU, lm, dt=dt, motion="velocity",
+    n = int(os.environ.get("VB_NP", bench.NP_PER_GPU))
+    pf = DeviceParticleFilter(n, lm, dt=dt, motion="velocity",
                               likelihood=os.environ.get("VB_LIK", "logsum"), seed=3, **kw)
     pf.load_observations(zs)
     pf.prepare_graphs()
