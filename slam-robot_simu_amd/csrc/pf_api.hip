@@ -116,6 +116,7 @@ struct slam_pf {
     bool scan_merged_ok = false;  // the merged launch is allowed for this handle
     double* s_cur = nullptr;
     DeferParts dp{};
+    FinSlices fsl{};                      // NP > 2^20: the finalize's slice pre-pass (pf_finalize.inl)
     int32_t nb_part = 0;
     // NumPy's RandomState stream on the device (slam_pf_set_rng_mt19937)
     bool mt = false;
@@ -447,10 +448,12 @@ int launch_reduce(slam_pf* h, int32_t resampled_known) {
     const int c = h->cur;
     tic(h, 1);
     if (h->deferred) {
+        if (h->fsl.nsl > 1)
+            finalize_slices_kernel<<<h->fsl.nsl - 1, kFinThreads, 0, s>>>(n, h->dp, h->fsl);
         finalize_deferred_kernel<<<1, kFinThreads, 0, s>>>(
             n, h->dp, h->w_un, h->s_cur, h->tail_leaves, h->tail_ops, h->n_tail_leaves,
             h->n_tail_ops, h->x[c], h->y[c], h->th[c], h->refp, h->flags, h->cfg.ess_threshold,
-            step_io(h), resampled_known, h->pc.np_recip, h->boff);
+            step_io(h), resampled_known, h->pc.np_recip, h->boff, h->fsl);
         toc(h, 1);
         SLAM_HIP_TRY(hipGetLastError());
         return SLAM_OK;
@@ -783,6 +786,13 @@ int create_impl(const slam_pf_config* cfg, int64_t n_local, int64_t n_global, in
     A(h->dp.leaf, (size_t)(kPartPer / 128) * h->nb_part);
     A(h->dp.mark, npad);
     A(h->dp.carry, h->nb_part + 1);
+    if (deferred && h->nb_part > kFinThreads * kFinRegBlocks) {
+        const int32_t per = kFinThreads * kFinRegBlocks;
+        h->fsl.nsl = (h->nb_part + per - 1) / per;
+        A(h->fsl.m, h->fsl.nsl);
+        A(h->fsl.q, 11 * (size_t)h->fsl.nsl);
+        A(h->fsl.buf, std::max<int64_t>(n / kSumChunk, 1));
+    }
     SLAM_HIP_TRY(hipMemsetAsync(h->dp.mark, 0xff, sizeof(int64_t) * npad, h->stream));
     SLAM_HIP_TRY(hipMemsetAsync(h->dp.carry, 0, sizeof(int32_t) * (h->nb_part + 1), h->stream));
     // tile totals: 2048-element tiles (shards) or 512-element wave tiles (deferred)

@@ -90,13 +90,126 @@ __device__ __forceinline__ int64_t fin_blk(const int t, const int k) {
     return 2 * (int64_t)t + (k & 1) + 2 * (int64_t)kFinThreads * (k >> 1);
 }
 
+// NP > 2^20 (round 5): slices of 2048 fused blocks beyond the first, one
+// workgroup each, laid out like the finalize's register blocks: the slice's
+// max M_g, its 11 partial sums scaled to M_g (lane sums over the lane's four
+// blocks, rescaled to M_g, then the finalize's transposed reduction), and the
+// np.sum value of each of its 128 buffers (pairwise over the buffer's 16
+// block subtrees).  The finalize then rescales the slices to the global max
+// and continues np.sum's left-to-right chain over the buffer values, instead
+// of pulling every block through one CU (a 2^23-particle finalize: 1.7 MB).
+struct FinSlices {
+    double* m;          // [nsl] slice max (slice 0: the finalize's own)
+    double* q;          // [nsl][11] slice sums scaled to the slice max
+    double* buf;        // [nfull] np.sum value of each full 8192-element buffer
+    int32_t nsl;        // slices of 2048 fused blocks; <= 1: no pre-pass
+};
+
+__global__ __launch_bounds__(kFinThreads) void finalize_slices_kernel(const int64_t n,
+                                                                      const DeferParts dp,
+                                                                      const FinSlices sl) {
+    __shared__ double s_q[11][kFinThreads];
+    __shared__ double s_wmax[kFinWaves];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int g = 1 + (int)blockIdx.x;
+    const int64_t nb = (n + kPartPer - 1) / kPartPer;
+    const int64_t nfull = n / kSumChunk;
+    const int64_t b_base = (int64_t)g * kFinThreads * kFinRegBlocks;
+    double pm[kFinRegBlocks], q[kFinRegBlocks][11];
+    bool has[kFinRegBlocks];
+#pragma unroll
+    for (int kp = 0; kp < kFinRegBlocks / 2; ++kp) {
+        const int64_t b = b_base + fin_blk(tid, 2 * kp);
+        has[2 * kp] = b < nb;
+        has[2 * kp + 1] = b + 1 < nb;
+        const int64_t bb = has[2 * kp] ? b : 0;
+        const double2 t = *reinterpret_cast<const double2*>(dp.pmax + bb);
+        pm[2 * kp] = t.x;
+        pm[2 * kp + 1] = t.y;
+#pragma unroll
+        for (int j = 0; j < 11; ++j) {
+            const double2 u = *reinterpret_cast<const double2*>(dp.ps[j] + bb);
+            q[2 * kp][j] = u.x;
+            q[2 * kp + 1][j] = u.y;
+        }
+    }
+    // the slice's buffers: 4 lanes per buffer, pairwise
+    {
+        const int part = tid & (kFinLeafLanes - 1);
+        const int64_t c = (int64_t)g * kFinBufPerRound + tid / kFinLeafLanes;
+        double v = 0.0;
+        if (c < nfull) {
+            const double* Lp = dp.leaf + 16 * c + 4 * part;
+            v = (Lp[0] + Lp[1]) + (Lp[2] + Lp[3]);
+        }
+        {
+            const double o = dpp_f64<kDppXor1>(v);
+            v = (part & 1) ? (o + v) : (v + o);
+        }
+        {
+            const double o = dpp_f64<kDppXor2>(v);
+            v = (part & 2) ? (o + v) : (v + o);
+        }
+        if (part == 0 && c < nfull) sl.buf[c] = v;
+    }
+    double mlane = -1.0;
+#pragma unroll
+    for (int k = 0; k < kFinRegBlocks; ++k)
+        if (has[k]) mlane = fmax(mlane, pm[k]);
+    double acc[11];
+#pragma unroll
+    for (int j = 0; j < 11; ++j) acc[j] = 0.0;
+    if (mlane > 0.0) {
+        const double rm = 1.0 / mlane;
+#pragma unroll
+        for (int k = 0; k < kFinRegBlocks; ++k) {
+            if (has[k]) {
+                const double r = pm[k] * rm;
+                acc[0] += r * q[k][0];
+                acc[1] += (r * r) * q[k][1];
+#pragma unroll
+                for (int j = 2; j < 11; ++j) acc[j] += r * q[k][j];
+            }
+        }
+    }
+    const double mx = wave_max_f64(mlane);
+    if (lane == 0) s_wmax[wave] = mx;
+    __syncthreads();
+    double M = s_wmax[0];
+#pragma unroll
+    for (int w = 1; w < kFinWaves; ++w) M = fmax(M, s_wmax[w]);
+    {
+        const double rl = (mlane > 0.0 && M > 0.0) ? mlane / M : 0.0;
+        acc[0] *= rl;
+        acc[1] *= rl * rl;
+#pragma unroll
+        for (int j = 2; j < 11; ++j) acc[j] *= rl;
+#pragma unroll
+        for (int j = 0; j < 11; ++j) s_q[j][tid] = acc[j];
+    }
+    __syncthreads();
+    for (int j = wave; j < 11; j += kFinWaves) {
+        double r = s_q[j][lane];
+#pragma unroll
+        for (int m = 1; m < kFinThreads / 64; ++m) r = r + s_q[j][lane + 64 * m];
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const double o = xor_f64(r, d);
+            r = (lane & d) ? (o + r) : (r + o);
+        }
+        if (lane == 0) sl.q[(int64_t)g * 11 + j] = r;
+    }
+    if (tid == 0) sl.m[g] = M;
+}
+
 __global__ __launch_bounds__(kFinThreads) void finalize_deferred_kernel(
     const int64_t n, const DeferParts dp, const double* __restrict__ w_un,
     double* __restrict__ s_cur, const int32_t* __restrict__ tail_leaves,
     const int32_t* __restrict__ tail_ops, const int32_t n_tail_leaves, const int32_t n_tail_ops,
     const double* __restrict__ xs, const double* __restrict__ ys, const double* __restrict__ ts,
     double* __restrict__ refp, int32_t* __restrict__ flags, const double ess_th, StepIO io,
-    const int32_t resampled_known, const double np_recip, double* __restrict__ boff) {
+    const int32_t resampled_known, const double np_recip, double* __restrict__ boff,
+    const FinSlices sl) {
     __shared__ double sh[2048];                      // buffer sums / tail leaves / block totals
     __shared__ double s_q[11][kFinThreads];
     __shared__ BlockPartial shp[kFinWaves];
@@ -163,7 +276,9 @@ __global__ __launch_bounds__(kFinThreads) void finalize_deferred_kernel(
     // of loads before it uses them -- one memory round trip per iteration made
     // the 2^23-particle finalize 50-110 us; the adds keep their order)
     const int64_t bx0 = tid + (int64_t)kFinThreads * kFinRegBlocks;
-    for (int64_t b0 = bx0; b0 < nb; b0 += kFinBatch * (int64_t)kFinThreads) {
+    const bool sliced = sl.nsl > 1;                  // blocks beyond the registers pre-reduced
+    const int64_t bxs = sliced ? nb : bx0;           // (the loops below then do nothing)
+    for (int64_t b0 = bxs; b0 < nb; b0 += kFinBatch * (int64_t)kFinThreads) {
         double v[kFinBatch];
 #pragma unroll
         for (int u = 0; u < kFinBatch; ++u) {
@@ -188,7 +303,7 @@ __global__ __launch_bounds__(kFinThreads) void finalize_deferred_kernel(
                 for (int j = 2; j < 11; ++j) acc[j] += r * q[k][j];
             }
         }
-        for (int64_t b0 = bx0; b0 < nb; b0 += kFinSumBatch * (int64_t)kFinThreads) {
+        for (int64_t b0 = bxs; b0 < nb; b0 += kFinSumBatch * (int64_t)kFinThreads) {
             double pv[kFinSumBatch], qv[kFinSumBatch][11];
 #pragma unroll
             for (int u = 0; u < kFinSumBatch; ++u) {
@@ -213,8 +328,10 @@ __global__ __launch_bounds__(kFinThreads) void finalize_deferred_kernel(
     const double mx = wave_max_f64(mlane);
     if (lane == 0) s_wmax[wave] = mx;
     // ---- np.sum: 8192-element buffers, 128 per round, pairwise inside
+    // (sliced: only the first slice's round here, the slices' buffer values after)
     double s = 0.0;
-    for (int64_t c0 = 0; c0 < nfull; c0 += kFinBufPerRound) {
+    const int64_t nleaf = sliced ? (nfull < kFinBufPerRound ? nfull : kFinBufPerRound) : nfull;
+    for (int64_t c0 = 0; c0 < nleaf; c0 += kFinBufPerRound) {
         const int64_t cnt = (nfull - c0 < kFinBufPerRound) ? nfull - c0 : kFinBufPerRound;
         const int64_t c = c0 + tid / kFinLeafLanes;
         double v = 0.0;
@@ -243,10 +360,26 @@ __global__ __launch_bounds__(kFinThreads) void finalize_deferred_kernel(
         }
     }
     if (nfull == 0) __syncthreads();                     // s_wmax visible
-    const int64_t last_cnt = nfull - ((nfull - 1) / kFinBufPerRound) * kFinBufPerRound;
+    int64_t last_cnt = nfull - ((nfull - 1) / kFinBufPerRound) * kFinBufPerRound;
+    if (sliced && nfull > kFinBufPerRound) {
+        // the slices' buffer values, staged 2048 at a time behind the chain so far
+        for (int64_t c0 = kFinBufPerRound; c0 < nfull; c0 += 2048) {
+            const int64_t cnt = (nfull - c0 < 2048) ? nfull - c0 : 2048;
+            __syncthreads();                                  // lane 0 is done with sh
+            for (int64_t k = tid; k < cnt; k += kFinThreads) sh[k] = sl.buf[c0 + k];
+            __syncthreads();
+            if (c0 + 2048 < nfull && tid == 0) s = lds_chain_sum(s, sh, (int)cnt);
+            last_cnt = cnt;
+        }
+    }
     double M = s_wmax[0];
 #pragma unroll
     for (int w = 1; w < kFinWaves; ++w) M = fmax(M, s_wmax[w]);
+    if (sliced) {                                        // the slices' maxima (every wave alike)
+        double msl = -1.0;
+        for (int g = 1 + lane; g < sl.nsl; g += 64) msl = fmax(msl, sl.m[g]);
+        M = fmax(M, wave_max_f64(msl));
+    }
     FIN_STAMP(1);
     if (tid == 0) {
         // the last round's buffers left to right (the other waves meanwhile
@@ -306,6 +439,20 @@ __global__ __launch_bounds__(kFinThreads) void finalize_deferred_kernel(
                 r = (lane & d) ? (o + r) : (r + o);
             }
             if (lane == 0) s_tot[j] = r;
+        }
+        if (sliced) {                                    // + the slices, rescaled to M, in order
+            __syncthreads();
+            if (tid < 11) {
+                double r = s_tot[tid];
+                for (int g = 1; g < sl.nsl; ++g) {
+                    const double mg = sl.m[g];
+                    if (mg > 0.0) {
+                        const double f = mg / M;
+                        r = r + sl.q[(int64_t)g * 11 + tid] * (tid == 1 ? f * f : f);
+                    }
+                }
+                s_tot[tid] = r;
+            }
         }
         // ---- argmax: the first block whose max rounds to fl(M / s)
         const double mval = M / s;

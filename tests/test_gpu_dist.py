@@ -47,7 +47,10 @@ def _same(a, b, k):
 
 @pytest.mark.parametrize("world,n_global,nl,lik", [(3, 3 * 65536, 20, "logsum"),
                                                   (2, 2 * 8192 + 1000, 5, "product"),
-                                                  (8, 8 << 20, 100, "logsum")])
+                                                  (8, 8 << 20, 100, "logsum"),
+                                                  # NP > 2^20 with a partial last slice of
+                                                  # the single finalize's pre-pass (round 5)
+                                                  (2, (1 << 21) + 12345, 20, "logsum")])
 def test_dist_local_steps_match_single(world, n_global, nl, lik):
     from slamhip.dist import DistFilter
     from slamhip.pf import DeviceParticleFilter
