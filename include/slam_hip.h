@@ -91,6 +91,13 @@ int slam_pf_set_landmarks(slam_pf* h, const double* landmarks);
 int slam_pf_set_state(slam_pf* h, const double* x, const double* y, const double* th,
                       const double* w);
 int slam_pf_get_state(slam_pf* h, double* x, double* y, double* th, double* w);
+/* The last step's weights before normalisation (w_un = pw * bn, particle_filter.py:194)
+ * and the divisor the device formed for them (np.sum(w_un) in numpy's order,
+ * :234; = slam_pf_result.weight_sum of that step; 1 after set_state / resample).
+ * The current weights are w_un / s (:235, NaN -> 1/NP).  Either pointer may be
+ * NULL.  Lets a caller pin the step-end np.sum and the reductions against
+ * numpy on the device's own w_un.  Single-GPU (deferred) handles. */
+int slam_pf_get_weights_raw(slam_pf* h, double* w_un, double* s);
 
 /* One estimator step of main_pf (particle_filter.py:102-117):
  * resampling (if the previous step's ESS < ESS_TH) -> predict -> likelihood ->

@@ -1027,6 +1027,18 @@ int slam_pf_get_state(slam_pf* h, double* x, double* y, double* th, double* w) {
     return SLAM_OK;
 }
 
+int slam_pf_get_weights_raw(slam_pf* h, double* w_un, double* s) {
+    SLAM_ARG_CHECK(h, "slam_pf_get_weights_raw: NULL handle");
+    SLAM_ARG_CHECK(h->deferred, "slam_pf_get_weights_raw: not a deferred (single-GPU) handle");
+    SLAM_HIP_TRY(hipSetDevice(h->device));
+    if (w_un)
+        SLAM_HIP_TRY(hipMemcpyAsync(w_un, h->w_un, h->n * sizeof(double), hipMemcpyDeviceToHost,
+                                    h->stream));
+    if (s) SLAM_HIP_TRY(hipMemcpyAsync(s, h->s_cur, sizeof(double), hipMemcpyDeviceToHost, h->stream));
+    SLAM_HIP_TRY(hipStreamSynchronize(h->stream));
+    return SLAM_OK;
+}
+
 int slam_pf_step(slam_pf* h, const double* control, const double* z, const double* noise,
                  double u_resample, slam_pf_result* res) {
     SLAM_ARG_CHECK(h && control && (z || h->nl == 0), "slam_pf_step: NULL argument");

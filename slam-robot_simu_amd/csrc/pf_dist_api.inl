@@ -391,6 +391,11 @@ int slam_dist_create(slam_pf** shards, int32_t n_held, int32_t world, int32_t ra
     for (int i = 0; i < n_held; ++i) {
         SLAM_ARG_CHECK(shards[i] && shards[i]->deferred && shards[i]->n_global == N,
                        "slam_dist_create: shards must come from slam_pf_create_dist_shard, same filter");
+        // the resample gathers address the staging slots either side of the
+        // particle arrays (goff = npad), which only a dist shard has
+        SLAM_ARG_CHECK(shards[i]->dp.goff > 0 &&
+                           shards[i]->dp.goff == (int64_t)shards[i]->nb_part * kPartPer,
+                       "slam_dist_create: handle is not a dist shard (slam_pf_create_dist_shard)");
         if (n_held > 1)
             SLAM_ARG_CHECK(shards[i]->device == shards[0]->device &&
                                (i == 0 ? shards[i]->gbase == 0

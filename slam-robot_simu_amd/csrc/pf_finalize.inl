@@ -98,6 +98,10 @@ __device__ __forceinline__ int64_t fin_blk(const int t, const int k) {
 // block subtrees).  The finalize then rescales the slices to the global max
 // and continues np.sum's left-to-right chain over the buffer values, instead
 // of pulling every block through one CU (a 2^23-particle finalize: 1.7 MB).
+// slice g's buffers are g * kFinBufPerRound ...: a slice of 2048 fused blocks
+// must be exactly one round of buffers (16 blocks each), i.e. 512 lanes
+static_assert(kFinThreads * kFinRegBlocks == 16 * kFinBufPerRound,
+              "a finalize slice (2048 fused blocks) must span kFinBufPerRound buffers");
 struct FinSlices {
     double* m;          // [nsl] slice max (slice 0: the finalize's own)
     double* q;          // [nsl][11] slice sums scaled to the slice max

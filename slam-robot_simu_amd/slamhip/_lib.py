@@ -84,6 +84,7 @@ SIGNATURES = {
     "slam_pf_set_landmarks": (C.c_int, [_P, _D]),
     "slam_pf_set_state": (C.c_int, [_P, _D, _D, _D, _D]),
     "slam_pf_get_state": (C.c_int, [_P, _D, _D, _D, _D]),
+    "slam_pf_get_weights_raw": (C.c_int, [_P, _D, _D]),
     "slam_pf_step": (C.c_int, [_P, _D, _D, _D, C.c_double, C.POINTER(PFResult)]),
     "slam_pf_resample": (C.c_int, [_P, C.c_double, C.c_int32, _I32]),
     "slam_pf_predict": (C.c_int, [_P, _D, _D]),

@@ -101,7 +101,10 @@ class RunResults(Sequence):
             if a.keys() != b.keys():
                 return False
             for k in a:
-                if not np.array_equal(a[k], b[k]):
+                x, y = np.asarray(a[k]), np.asarray(b[k])
+                # NaN fields (a degenerate step's cov, det, ESS) compare equal
+                nan_ok = x.dtype.kind in "fc" and y.dtype.kind in "fc"
+                if not np.array_equal(x, y, equal_nan=nan_ok):
                     return False
         return True
 
@@ -202,6 +205,15 @@ class DeviceParticleFilter:
         out = [np.empty(self.n) for _ in range(4)]
         check(self._lib.slam_pf_get_state(self._h, *[dptr(a) for a in out]), "slam_pf_get_state")
         return tuple(out)
+
+    def get_weights_raw(self):
+        """(w_un, s): the last step's weights before normalisation and the
+        np.sum the device divided them by (slam_pf_get_weights_raw)."""
+        w = np.empty(self.n)
+        s = C.c_double(0.0)
+        check(self._lib.slam_pf_get_weights_raw(self._h, dptr(w), C.byref(s)),
+              "slam_pf_get_weights_raw")
+        return w, s.value
 
     def set_landmarks(self, lm):
         lm = _f64(lm).reshape(-1, 2)

@@ -52,6 +52,18 @@ def test_weight_sum_numpy_order(slamhip_pf, n):
     assert s == g["sum_out"][i]
 
 
+@pytest.mark.parametrize("n", [(1 << 21) + 12345, 1 << 23])
+def test_weight_sum_numpy_order_above_2p20(slamhip_pf, n):
+    """np.sum (particle_filter.py:234) beyond the fixture's sizes: numpy itself
+    on the same array is the reference (the step end's np.sum at these sizes,
+    through the finalize's slice pre-pass, is tests/test_gpu_run_oracle.py)."""
+    a = heavy_weights(np.random.RandomState(n % 100003), n)
+    with slamhip_pf.DeviceParticleFilter(n, np.zeros((1, 2))) as d:
+        d.set_state(w=a)
+        s = d.weight_sum()
+    assert s == np.sum(a.reshape(1, n))
+
+
 @pytest.mark.parametrize("lik", ["product", "logsum"])
 @pytest.mark.parametrize("tag", ["a", "b", "c"])
 def test_likelihood_stage(slamhip_pf, tag, lik):

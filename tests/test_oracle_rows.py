@@ -85,3 +85,22 @@ def test_velocity_process_noise_matches_sampled_motion():
     np.testing.assert_allclose(np.diag(emp), np.diag(Qv), rtol=0.02)
     np.testing.assert_allclose(emp[0, 1] / np.sqrt(emp[0, 0] * emp[1, 1]),
                                Qv[0, 1] / np.sqrt(Qv[0, 0] * Qv[1, 1]), atol=0.02)
+
+
+# ------------------------------------------------- the oracle's thread pool
+def test_likelihood_products_threaded_bit_identical():
+    """The large lockstep runs (tests/test_gpu_run_oracle.py) form the
+    reference's per-particle products over a thread pool in particle chunks;
+    every row must be bit-identical to the one-batch form (incl. a ragged last
+    chunk and the underflow tail)."""
+    rs = np.random.RandomState(3)
+    n, nl = 200_003, 37
+    lm = rs.uniform(-10, 10, (nl, 2))
+    x, y = rs.normal(0, 3, n), rs.normal(0, 3, n)
+    th = rs.uniform(-np.pi, np.pi, n)
+    z = po.to_robot_frame(np.array([0.5, -0.2, 1.0]), lm)
+    r = np.diag([0.3, 0.3]) ** 2
+    one = po.landmark_factors(x, y, th, lm, z, r).prod(axis=1)
+    many = po.likelihood_products(x, y, th, lm, z, r, threads=4, chunk=1 << 14)
+    assert np.array_equal(one, many)
+    assert (one == 0).any() and (one > 0).any()

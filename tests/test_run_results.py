@@ -33,3 +33,16 @@ def test_run_results_equality_and_slices():
     d = RunResults.from_dicts(list(b))
     assert len(d) == 3 and d[2]["resampled"] is False
     np.testing.assert_array_equal(d[1]["x_est"], [1.0, 2.0, 3.0])
+
+
+def test_run_results_nan_fields_compare_equal():
+    """A degenerate step's NaN covariance / ESS: two identical runs still
+    compare equal, and a NaN against a number does not."""
+    from slamhip.pf import RunResults
+    a, b = _records(2), _records(2)
+    for r in (a, b):
+        r[1].cov[4] = float("nan")
+        r[1].ess = float("nan")
+    assert RunResults(a) == RunResults(b)
+    b[1].ess = 1.0
+    assert RunResults(a) != RunResults(b)
