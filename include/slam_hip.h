@@ -389,15 +389,20 @@ typedef struct {
 /* The PCG path's gate (:494-496).  SLAM_GRAPH_COND_ESTIMATE: cond = the extreme
  * eigenvalues of H by LOBPCG on a second stream beside the solve, the
  * reference's `cond < cond_max` from a converged estimate, det not formed
- * (NaN).  SLAM_GRAPH_COND_CERTIFY (the Python default): the same estimate
- * stops as soon as it clears cond_max by a factor 100 (or converges with a
- * factor 10), and the det half is decided from a log-det interval (M the
- * block diagonal of H, P = M^-1/2 H M^-1/2: [log det M + c(a)(tr P^2 - n),
- * log det M]); a half neither decides takes the dense path's value when n <=
- * 2048, else the update is not solved and flagged undecided
- * (slam_graph_gate_info).  SLAM_GRAPH_COND_OFF: no gate (cond NaN,
- * the solve's convergence alone). */
-enum { SLAM_GRAPH_COND_ESTIMATE = 0, SLAM_GRAPH_COND_OFF = 1, SLAM_GRAPH_COND_CERTIFY = 2 };
+ * (NaN).  SLAM_GRAPH_COND_MARGIN (the Python default; formerly named
+ * SLAM_GRAPH_COND_CERTIFY): an estimate with margins, NOT a certificate -- the
+ * same estimate stops as soon as its Ritz ratio clears cond_max by a factor 100
+ * (or converges: a factor 10; a converged estimate inside that band decides
+ * by its own value), and the det half is decided from a log-det interval (M
+ * the block diagonal of H, P = M^-1/2 H M^-1/2: [log det M + c(a)(tr P^2 - n),
+ * log det M]) whose upper end is rigorous and whose lower end holds unless the
+ * estimate's lambda_min over-estimates lambda_min(H) by more than 1000x (a =
+ * lambda~min / (1000 max tr M_i)); a half neither decides takes the dense
+ * path's value when n <= 2048, else the update is not solved and flagged
+ * undecided (slam_graph_gate_info).  SLAM_GRAPH_COND_OFF: no gate
+ * (cond NaN, the solve's convergence alone). */
+enum { SLAM_GRAPH_COND_ESTIMATE = 0, SLAM_GRAPH_COND_OFF = 1, SLAM_GRAPH_COND_MARGIN = 2,
+       SLAM_GRAPH_COND_CERTIFY = SLAM_GRAPH_COND_MARGIN /* former name of the same mode */ };
 
 int slam_graph_create(const slam_graph_config* cfg, int device, slam_graph** out);
 int slam_graph_destroy(slam_graph* h);
@@ -439,15 +444,20 @@ int slam_graph_timing(slam_graph* h, double* out);
  * reached, 4 not positive definite), lambda_min, lambda_max, iterations of the
  * min side, of the max side, device time (ms)}.  Zeros after a dense update. */
 int slam_graph_cond_info(slam_graph* h, double* out);
-/* The last PCG-path update's certificate (SLAM_GRAPH_COND_CERTIFY): out[12] =
- * {decided by (1 the bounds and the estimate, 2 a half by the dense path), det
- * decision (1 passed / 0 rejected by the log-det interval, 3 / 2 by the dense
- * LU det, -1 undecided: not solved), cond decision (1 passed / 0 rejected by
- * the estimate, 3 / 2 by the dense Lanczos cond, -1 undecided), log det H
- * lower bound, upper bound, cond (the value the decision used), lambda_min(H),
- * lambda_max(H) (the estimate's Ritz values), tr(P^2), n, estimate iterations,
- * host ms}.  Zeros after a dense update, in the other modes, and when the
- * estimate rejected H for certain (cond_info status 2 / 4). */
+/* The last PCG-path update's gate (SLAM_GRAPH_COND_MARGIN): out[14] =
+ * {decided by (1 the estimate with its margins and the log-det bounds, 2 a
+ * half by the dense path), det decision (1 passed by the interval's lower end
+ * at the 1000x margin / 0 rejected by its (rigorous) upper end, 3 / 2 by the
+ * dense LU det, -1 undecided: not solved), cond decision (1 passed / 0
+ * rejected by the estimate with its margin, 5 passed by a converged estimate
+ * inside the margin band, 3 / 2 by the dense Lanczos cond, -1 undecided), log
+ * det H lower end, upper end, cond (the value the decision used),
+ * lambda_min(H), lambda_max(H) (the estimate's Ritz values), tr(P^2), n,
+ * estimate iterations, host ms, det margin (the largest factor by which the
+ * Ritz lambda_min may over-estimate lambda_min(H) with the lower end still
+ * above ln det_min; 0 if none), cond margin (cond_max / cond)}.  Zeros after a
+ * dense update, in the other modes, and when the estimate rejected H for
+ * certain (cond_info status 2 / 4). */
 int slam_graph_gate_info(slam_graph* h, double* out);
 /* HalfEdge (graph_based_slam.py:259-300) with its Observation (:20-75). */
 typedef struct {

@@ -873,7 +873,7 @@ struct CondState {
     double lam[2];                // the latest Ritz values (min side, max side)
     double coef[2][4];            // this iteration's update of each side: c0, c1, c2, 1 / |p'|
     int32_t iter, done, status, iters_side[2], conv[2], upd[2], win;   // win: the stall window
-    // the gate's early decision (SLAM_GRAPH_COND_CERTIFY; etol 0: off): both
+    // the gate's early decision (SLAM_GRAPH_COND_MARGIN; etol 0: off): both
     // sides moved less than etol (relative) over ewin iterations and
     // theta_max / theta_min * emargin < cond_max -> status 5
     double etol, emargin;

@@ -65,7 +65,7 @@ class GraphConfig(C.Structure):
 
 
 GRAPH_SOLVER = {"auto": 0, "dense": 1, "pcg": 2}
-GRAPH_COND = {"estimate": 0, "off": 1, "certify": 2}
+GRAPH_COND = {"estimate": 0, "off": 1, "margin": 2, "certify": 2}   # "certify": the former name
 
 _P = C.c_void_p
 _D = C.POINTER(C.c_double)

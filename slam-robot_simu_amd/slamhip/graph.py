@@ -65,7 +65,7 @@ class DeviceGraph:
 
     def __init__(self, *, r_dist=0.05, r_dir=np.deg2rad(2.0), r_orient=np.deg2rad(2.0),
                  anchor=1e4, det_min=0.1, cond_max=1e15, solver="auto", pcg_tol=1e-10,
-                 pcg_max_iter=20000, cond="certify", cond_tol=1e-5, cond_max_iter=3000, device=0):
+                 pcg_max_iter=20000, cond="margin", cond_tol=1e-5, cond_max_iter=3000, device=0):
         cfg = GraphConfig()
         cfg.r_dist, cfg.r_dir, cfg.r_orient = float(r_dist), float(r_dir), float(r_orient)
         cfg.anchor, cfg.det_min, cfg.cond_max = float(anchor), float(det_min), float(cond_max)
@@ -167,20 +167,29 @@ class DeviceGraph:
                     ms=out[6])
 
     def gate_info(self):
-        """The last PCG-path update's gate certificate (cond="certify";
-        slam_graph_gate_info): the log-det interval, the cond(H) bound, the
-        Ritz values of the preconditioned operator and each half's decision."""
-        out = np.zeros(12)
+        """The last PCG-path update's gate (cond="margin": an estimate with
+        margins, not a certificate; slam_graph_gate_info): the log-det interval,
+        the cond(H) the decision used, the Ritz values, each half's decision and
+        the margins the decisions held (det_margin: the factor by which the Ritz
+        lambda_min may over-estimate lambda_min(H) before the det lower end
+        drops below ln det_min; cond_margin: cond_max / cond)."""
+        out = np.zeros(14)
         check(self._lib.slam_graph_gate_info(self._h, dptr(out)), "slam_graph_gate_info")
         return dict(decided_by="bounds" if out[0] == 1 else "dense" if out[0] == 2 else "none",
                     det_decision=int(out[1]), det=GATE_DET.get(int(out[1]), "none"),
                     cond_decision=int(out[2]), logdet_lo=out[3], logdet_hi=out[4],
                     cond=out[5], lambda_min=out[6], lambda_max=out[7], trp2=out[8],
-                    n=int(out[9]), estimate_iterations=int(out[10]), ms=out[11])
+                    n=int(out[9]), estimate_iterations=int(out[10]), ms=out[11],
+                    det_margin=out[12], cond_margin=out[13],
+                    cond_decided=GATE_COND.get(int(out[2]), "none"))
 
 
-GATE_DET = {1: "passed (bound)", 0: "rejected (bound)", 3: "passed (dense LU det)",
+GATE_DET = {1: "passed (log-det lower end, estimate with 1000x margin)",
+            0: "rejected (log-det upper end, Fischer bound)", 3: "passed (dense LU det)",
             2: "rejected (dense LU det)", -1: "undecided"}
+GATE_COND = {1: "passed (estimate with margin)", 0: "rejected (estimate: for certain)",
+             5: "passed (converged estimate inside the margin band)",
+             3: "passed (dense Lanczos cond)", 2: "rejected (dense Lanczos cond)", -1: "undecided"}
 
 
 def circle_graph(n_poses, n_landmarks=64, loops_per_pose=3, seed=0, odom_noise=0.02):

@@ -146,7 +146,7 @@ def test_c5_graph_full_size_pcg_solves():
         dev.set_edges(edges)
         for _ in range(2):
             is_calc, dsum, det, cond = dev.update()
-            # the certificate's det is its lower bound exp(lo): inf at this size, as numpy's
+            # the gate's det is its log-det lower end exp(lo): inf at this size, as numpy's
             assert is_calc and det > 0.1 and np.isfinite(cond) and cond < 1e15, (det, cond)
             rows, cols, vals = dev.get_bsr()
             nt = int(rows.max()) + 1

@@ -1,7 +1,7 @@
 """The reference's gate on the PCG path (graph_based_slam.py:494-498).
 
 Two modes: cond="estimate" (the LOBPCG estimate of cond alone, det not
-formed) and cond="certify" (the default: the estimate with an early decision
+formed) and cond="margin" (the default, formerly "certify": the estimate with an early decision
 at a factor-100 margin, plus a log-det interval; test_gpu_graph_gate.py).
 
 updateEstPose forms det(H) and cond(H) = numpy's 2-norm condition number and

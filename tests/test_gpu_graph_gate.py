@@ -1,16 +1,22 @@
-"""The certificate gate of the PCG path (cond="certify", the default;
-graph_api.hip cert_gate) against the reference's own decision,
-`0.1 < det(H) and cond(H) < 1e15` (graph_based_slam.py:494-496), formed by
-numpy on the same H exported from the device:
+"""The PCG path's gate, an estimate with margins (cond="margin", the default,
+formerly "certify"; graph_api.hip cert_gate) against the
+reference's own decision, `0.1 < det(H) and cond(H) < 1e15`
+(graph_based_slam.py:494-496), formed by numpy on the same H exported from the
+device:
 
   * det: log det H in [log det M + c(a)(tr(P^2) - n), log det M] (M the block
     diagonal of H, P = M^-1/2 H M^-1/2; Fischer's inequality above, the
     quadratic bound of ln below) -- the interval must contain numpy's log|det|
     (T = 300 and T = 5,000 against a sparse LU) and decide as numpy does;
   * a small-eigenvalue H (the measurement information scaled down 1000x):
-    det < 0.1 < ... -- numpy, the dense path and the PCG certificate all reject;
+    det < 0.1 < ... -- numpy, the dense path and the PCG gate all reject;
   * cond: the estimate's early decision (factor-100 margin) passes the C5-form
-    graphs, whose cond is ~1e6-1e7.
+    graphs, whose cond is ~1e6-1e7;
+  * a Ritz value that over-estimates lambda_min(H) (SLAM_GRAPH_GATE_RITZ_SCALE:
+    the gate is handed 30x the estimate, as an early stop that missed a
+    near-singular mode would) on an H numpy rejects by det while the rigorous
+    upper end cannot: the gate does not pass it by the estimate -- the det
+    half falls back to the dense LU det and rejects as numpy.
 """
 import numpy as np
 import pytest
@@ -36,7 +42,7 @@ def _sparse_H(dev):
                          shape=(3 * nt, 3 * nt)).tocsc()
 
 
-def test_certificate_decides_like_numpy_t300():
+def test_margin_gate_decides_like_numpy_t300():
     from slamhip.graph import DeviceGraph
     init, _, edges = _graph(300)
     dev = DeviceGraph(solver="pcg", pcg_tol=1e-10)
@@ -55,7 +61,7 @@ def test_certificate_decides_like_numpy_t300():
     assert gi["det_decision"] == 1 and gi["cond_decision"] == 1, gi
 
 
-def test_certificate_logdet_interval_t5000():
+def test_margin_gate_logdet_interval_t5000():
     import scipy.sparse.linalg as sla
     from slamhip.graph import DeviceGraph
     init, _, edges = _graph(5000)
@@ -80,7 +86,7 @@ def test_certificate_logdet_interval_t5000():
 def test_small_eigenvalue_h_det_rejects(solver):
     """det < 0.1 < ... : the measurement noise 31.6x larger (information
     1000x smaller) leaves cond ~1e9 < 1e15 but det ~ e^-1900; the reference
-    rejects on det alone, and so do both paths (the certificate by its upper
+    rejects on det alone, and so do both paths (the gate by its rigorous upper
     bound log det M < ln 0.1)."""
     from slamhip.graph import DeviceGraph
     init, _, edges = _graph(300)
@@ -103,9 +109,9 @@ def test_small_eigenvalue_h_det_rejects(solver):
         assert gi["det_decision"] == 0 and gi["logdet_hi"] < np.log(0.1), gi
 
 
-def test_certificate_unconverged_estimate_falls_back_to_dense_cond():
+def test_margin_gate_unconverged_estimate_falls_back_to_dense_cond():
     """an estimate stopped at cond_max_iter is not a rejection -- the
-    certificate takes the dense path's cond (n <= 2048) and decides as numpy."""
+    gate takes the dense path's cond (n <= 2048) and decides as numpy."""
     from slamhip.graph import DeviceGraph
     init, _, edges = _graph(300)
     g = DeviceGraph(solver="pcg", cond_max_iter=3)
@@ -120,3 +126,40 @@ def test_certificate_unconverged_estimate_falls_back_to_dense_cond():
     ref = bool((0.1 < np.linalg.det(H)) and (np.linalg.cond(H) < 1e15))
     assert info["status"] == 3 and gi["cond_decision"] == 3, (info, gi)
     assert bool(ok) == ref and ref
+
+
+@pytest.mark.parametrize("noise_k,numpy_passes", [(1.0, True), (11.3, False)])
+def test_overestimated_ritz_value_does_not_pass_by_estimate(noise_k, numpy_passes, monkeypatch):
+    """ADVICE / VERDICT r5: the Ritz lambda_min over-estimates lambda_min(H),
+    here by 30x (SLAM_GRAPH_GATE_RITZ_SCALE).  noise_k = 11.3: the measurement
+    information 128x smaller, numpy's det ~ e^-38 < 0.1 while the Fischer upper
+    end log det M stays above ln 0.1: the det half must not pass by the
+    estimate; it takes the dense LU det and rejects, as numpy.  noise_k = 1:
+    the 1000x margin still holds the lower end below numpy's log det, and the
+    update passes as numpy's does."""
+    from slamhip.graph import DeviceGraph
+    monkeypatch.setenv("SLAM_GRAPH_GATE_RITZ_SCALE", "30")
+    init, _, edges = _graph(300)
+    g = DeviceGraph(solver="pcg", r_dist=0.05 * noise_k, r_dir=np.deg2rad(2.0) * noise_k,
+                    r_orient=np.deg2rad(2.0) * noise_k, pcg_tol=1e-10, pcg_max_iter=20000)
+    try:
+        g.set_poses(init)
+        g.set_edges(edges)
+        ok, dsum, det, cond = g.update()
+        gi, info = g.gate_info(), g.cond_info()
+        H = _dense_H(g)
+    finally:
+        g.close()
+    sign, ld = np.linalg.slogdet(H)
+    lam = np.linalg.eigvalsh(H)[0]
+    ref = bool((0.1 < np.linalg.det(H)) and (np.linalg.cond(H) < 1e15))
+    print(gi, info, "numpy log det", ld, "lambda_min", lam)
+    assert ref == numpy_passes and bool(ok) == ref, (ok, ref, gi)
+    assert gi["lambda_min"] > 10 * lam                  # the gate saw an over-estimate > 10x
+    assert gi["logdet_lo"] <= ld <= gi["logdet_hi"], (ld, gi)
+    if numpy_passes:
+        assert gi["det_decision"] == 1 and gi["det_margin"] >= 1000, gi
+    else:
+        assert gi["logdet_hi"] > np.log(0.1), gi        # the upper end cannot reject it
+        assert gi["det_decision"] == 2 and gi["decided_by"] == "dense", gi
+        assert dsum == 0.0
