@@ -25,7 +25,16 @@ fused block (or per resample run) where it is local:
   misrun    one run's start mark missed: its positions take the previous
             run's source;
   noreset   (global) the post-resample weights are not reset to 1/NP;
-  lost / stale5 again per 128-, 256-, 1024-, 2048-, 4096- and 8192-element unit.
+  lost / stale5 again per 128-, 256-, 1024-, 2048-, 4096- and 8192-element unit;
+  (round 6)
+  torn65    one block's record torn: its max from step 6 with its scaled sums
+            from step 5 (the finalize rescales step 5's sums by M6_b / M);
+  torn56    the reverse: step 5's max with step 6's scaled sums;
+  tornf     one block, one field (S0, one of S1's 3, one of S2's 6) from step 5,
+            the rest of the record from step 6;
+  refp4     one block (or a group of 16 / 128 / 512 blocks, or an XCD) formed
+            its moments about the wrong reference point, the estimate two steps
+            back (the other refp slot) instead of the previous one.
 
 Prints the best fit of each (max relative error over the six distinct entries
 of ACTUAL, which the log printed to 7 digits: a true cause fits to ~1e-6).
@@ -248,6 +257,45 @@ def main():
         zero_s = (np.zeros(m), np.zeros((m, 3)), np.zeros((m, 3, 3)))
         best_local(f"lost@{size}", tot_s, zero_s, base_s)
         best_local(f"stale5@{size}", tot_s, moments(w_prev5 * L5, Pb5, m), base_s)
+    # round 6: torn records and the wrong reference point
+    M6 = w_un.reshape(nb, B).max(1)
+    M5 = (w_prev5 * L5).reshape(nb, B).max(1)
+    r65 = (M6 / M5)
+    b5 = st5                                             # step-5 raw moments (centred on ref5)
+    results["torn65"] = best_local("torn65", tot, (b5[0] * r65, b5[1] * r65[:, None],
+                                                   b5[2] * r65[:, None, None]), base)
+    results["torn56"] = best_local("torn56", tot, (base[0] / r65, base[1] / r65[:, None],
+                                                   base[2] / r65[:, None, None]), base)
+    # one field of one block from step 5 (rescaled by M6_b / M5_b)
+    best = (np.inf, None)
+    fields = [("S0", None)] + [(f"S1[{i}]", i) for i in range(3)] + \
+             [(f"S2[{i}{j}]", (i, j)) for i in range(3) for j in range(i, 3)]
+    for name, f in fields:
+        for k in range(nb):
+            S0, S1, S2 = tot[0], tot[1].copy(), tot[2].copy()
+            if f is None:
+                S0 = S0 - base[0][k] + b5[0][k] * r65[k]
+            elif isinstance(f, int):
+                S1[f] += b5[1][k][f] * r65[k] - base[1][k][f]
+            else:
+                i, j = f
+                d = b5[2][k][i, j] * r65[k] - base[2][k][i, j]
+                S2[i, j] += d
+                if i != j:
+                    S2[j, i] += d
+            e = err(cov_of(S0, S1, S2))
+            if e < best[0]:
+                best = (e, f"{name} of block {k}")
+    print(f"{'tornf':9s} best single-field fit {best[0]:.3g} ({best[1]})")
+    # refp4: moments about the estimate two steps back
+    ref4 = np.ravel(steps[4]["out"]["x_est"])
+    Pw = np.vstack([X - ref4[0], Y - ref4[1], T - ref4[2]])
+    alt4 = moments(w_un, Pw, nb)
+    results["refp4"] = best_local("refp4", tot, alt4, base)
+    for g in (16, 128, 512):
+        m = nb // g
+        grp = lambda q: q.reshape((m, g) + q.shape[1:]).sum(1)
+        best_local(f"refp4@{g}blk", tot, tuple(grp(q) for q in alt4), tuple(grp(q) for q in base))
     print("(a true cause fits to ~1e-6, the printing precision of ACTUAL)")
     return results
 
