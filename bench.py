@@ -557,7 +557,32 @@ def connect_exchange(ag, connect, use_collectives=None):
 
 
 SETTLE_BATCH = 31      # 16 + 8 + 4 + 2 + 1: every captured graph shape once per batch
+PARITY_STEPS = 8       # sharded runs: steps replayed against one handle before timing
 NS_ROUND_STEPS = 64    # NumPy-stream timing window: two of its ring-refill periods
+
+
+def compare_to_single(recs, state, ref_recs, ref_state):
+    """A sharded run's records and gathered final state against one handle's
+    run of the same filter (same seed, observations and controls): the fields
+    the sharded step reproduces bit for bit (argmax, estimate, max, np.sum,
+    resample decisions; particles and weights) and the covariance, which the
+    shards reduce in another fixed order (1e-7, as tests/test_gpu_configs.py's
+    C3).  Returns (bit_identical, worst cov relative difference, first
+    mismatch or None)."""
+    first, worst = None, 0.0
+    for k, (a, b) in enumerate(zip(ref_recs, recs)):
+        for f in ("resampled", "resample_next", "max_idx", "max_val", "weight_sum", "x_est"):
+            if first is None and not np.array_equal(a[f], b[f]):
+                first = f"step {k}: {f} {b[f]!r} != single {a[f]!r}"
+        den = np.maximum(np.abs(a["cov"]), 1e-13)
+        worst = max(worst, float(np.max(np.abs(a["cov"] - b["cov"]) / den)))
+    for name, u, v in zip(("x", "y", "th", "w"), ref_state, state):
+        if first is None and not np.array_equal(u, v):
+            i = int(np.flatnonzero(u != v)[0])
+            first = f"final {name}[{i}] {v[i]!r} != single {u[i]!r}"
+    if first is None and worst > 1e-7:
+        first = f"cov relative difference {worst:.3g} > 1e-7"
+    return first is None, worst, first
 
 
 def settle(run, ctl, n):
@@ -719,12 +744,57 @@ def main():
                 ag.checkpoint("connect done")
             ag.attempt(filt.load_observations, zs)
             ag.checkpoint("load")
+            if multi and os.environ.get("SLAM_BENCH_NO_PARITY") != "1":
+                sharded_parity(filt, ag, n_global, likelihood, kw)
             return timed_runs(filt, ctl, args.warmup, args.steps, barrier_sync, ag, settle_steps)
         finally:
             if filt is not None:
                 filt.close()
             if comm is not None:
                 comm.close()
+
+    parity = {}
+
+    def sharded_parity(filt, ag, n_global, likelihood, kw):
+        # the run's own evidence that the cross-device step is the filter
+        # (VERDICT r5): PARITY_STEPS sharded steps from the initial state, the
+        # final state gathered to rank 0 and compared bit for bit with one
+        # handle of all n_global particles replaying the same steps there;
+        # a mismatch fails the sharded mode on every rank (replicas, reason)
+        import torch
+        recs = ag.attempt(filt.run, 0, ctl[:PARITY_STEPS])
+        st = ag.attempt(filt.get_state)
+        ag.checkpoint("parity run")
+        local = torch.from_numpy(np.ascontiguousarray(np.stack(st))).to(tdev)
+        sizes = [torch.zeros(1, dtype=torch.int64, device=tdev) for _ in range(world)]
+        dist.all_gather(sizes, torch.tensor([local.shape[1]], dtype=torch.int64, device=tdev))
+        nmax = int(max(int(t.item()) for t in sizes))
+        pad = torch.zeros((4, nmax), dtype=torch.float64, device=tdev)
+        pad[:, :local.shape[1]] = local
+        parts = [torch.empty_like(pad) for _ in range(world)]
+        dist.all_gather(parts, pad)
+        if rank == 0:
+            def check():
+                full = np.concatenate([p[:, :int(n.item())].cpu().numpy() for p, n in zip(parts, sizes)], 1)
+                if os.environ.get("SLAM_BENCH_PARITY_INJECT") == "1":          # tests
+                    full[0, 12345] = np.nextafter(full[0, 12345], np.inf)
+                one = DeviceParticleFilter(n_global, lm, **kw)
+                try:
+                    one.load_observations(zs)
+                    ref = one.run(0, ctl[:PARITY_STEPS])
+                    ref_state = one.get_state()
+                finally:
+                    one.close()
+                ok, worst, first = compare_to_single(list(recs), tuple(full), list(ref), ref_state)
+                parity.update(steps=PARITY_STEPS, bit_identical=ok, cov_max_rel=worst,
+                              first_mismatch=first,
+                              reference=f"one handle of {n_global:,} particles on rank 0's GPU, "
+                                        "same seed, observations and controls",
+                              resample_steps=int(sum(r["resampled"] for r in ref)))
+                if not ok:
+                    raise RuntimeError(f"sharded run differs from one handle: {first}")
+            ag.attempt(check)
+        ag.checkpoint("parity")
 
     def measure(likelihood, n_part=None):
         if args.mode == "sharded":
@@ -867,6 +937,8 @@ def main():
         except Exception as e:            # reported, never silently replaced
             vb = {"error": f"{type(e).__name__}: {e}"}
         line["cpu_baseline_vectorised"] = vb
+    if parity:
+        line["parity_check"] = parity
     if sharded_error is not None:
         line["sharded_error"] = sharded_error
     if args.mode == "sharded" and multi:

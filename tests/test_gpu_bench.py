@@ -66,23 +66,55 @@ def test_bench_sharded_mode(launcher):
     assert d["resample_steps"] >= 0 and d["roofline"]["avg_launch_ms"] > 0
 
 
-def test_bench_sharded_two_ranks_share_one_gpu():
-    """bench.py's N > 1 path (the default --mode sharded) with two ranks on the
+@pytest.mark.parametrize("world,total", [(2, None), (3, 3 * 65536), (4, 4 * 65536)])
+def test_bench_sharded_ranks_share_one_gpu(world, total):
+    """bench.py's N > 1 path (the default --mode sharded) with 2-4 ranks on the
     one GPU of the test box: IPC-opened exchange regions across processes, the
-    timed hipGraph replays, max-over-ranks timing, one JSON line from rank 0."""
-    args = [os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "8", "--warmup", "2",
-            "--no-secondary", "--no-cpu-baseline"]
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
-           "--master-addr", "127.0.0.1", "--master-port", "29541"] + args
+    run's own parity check (PARITY_STEPS sharded steps, the state gathered to
+    rank 0 and compared bit for bit with one handle of all the particles), the
+    timed hipGraph replays, max-over-ranks timing, one JSON line from rank 0.
+    Two ranks at the weak-scaling size (2^20 each); three and four at 65,536
+    per rank (--total-particles): each rank's resample exchange is one launch
+    whose grid must be co-resident and waits on its peers', and on one shared
+    GPU three such 512-block grids of 2^20-particle shards oversubscribe it (the
+    waits expire; on the 8-GPU node every rank has its own GPU -- DESIGN 9)."""
+    args = [os.path.join(ROOT, "bench.py"), "--gpus", str(world), "--steps", "8", "--warmup", "2",
+            "--no-secondary", "--no-cpu-baseline", "--settle-steps", "62"]
+    if total:
+        args += ["--total-particles", str(total)]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node",
+           str(world), "--master-addr", "127.0.0.1", "--master-port", str(29560 + world)] + args
     env = dict(os.environ, SLAM_BENCH_SHARE_GPU="1")
     r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=110)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1, r.stdout
     d = json.loads(lines[0])
-    assert d["n_gpus"] == 2 and d["config"]["parallelism"] == "sharded2"
-    assert d["value"] > 1e10 and d["resample_steps"] >= 1
-    assert abs(d["value"] - 2 * 2 ** 20 * 100 / (d["ms_per_step"] / 1e3)) <= 1e-6 * d["value"]
+    n_total = total or world * 2 ** 20
+    assert d["n_gpus"] == world and d["config"]["parallelism"] == f"sharded{world}"
+    assert d["value"] > 1e9 and d["resample_steps"] >= 1
+    assert abs(d["value"] - n_total * 100 / (d["ms_per_step"] / 1e3)) <= 1e-6 * d["value"]
+    pc = d["parity_check"]
+    assert pc["bit_identical"] and pc["first_mismatch"] is None and pc["steps"] == 8, pc
+    assert pc["resample_steps"] >= 1 and pc["cov_max_rel"] <= 1e-7, pc
+
+
+def test_bench_sharded_parity_mismatch_falls_back_to_replicas():
+    """A sharded run whose gathered state differs from the single handle's (one
+    ulp injected into the gathered x on rank 0): every rank leaves the sharded
+    mode, the line measures replicas and carries the failed check."""
+    args = [os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "6", "--warmup", "2",
+            "--no-secondary", "--no-cpu-baseline", "--settle-steps", "31"]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", "29539"] + args
+    env = dict(os.environ, SLAM_BENCH_SHARE_GPU="1", SLAM_BENCH_PARITY_INJECT="1")
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])
+    assert d["config"]["parallelism"] == "replicas2"
+    pc = d["parity_check"]
+    assert not pc["bit_identical"] and pc["first_mismatch"].startswith("final x[12345]"), pc
+    assert d["sharded_error"].startswith("parity"), d["sharded_error"]
 
 
 def test_bench_sharded_failure_falls_back_to_replicas():
