@@ -906,6 +906,12 @@ extern "C" int slam_probe_slow_count(unsigned long long* out) {
 }
 #endif
 
+#ifdef SLAM_FIN_PROBE
+extern "C" int slam_fin_probe_read(long long* out) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_fin_probe), sizeof(long long) * 16) == hipSuccess ? 0 : -1;
+}
+#endif
+
 #ifdef SLAM_PROBE_FUSED
 extern "C" int slam_fprobe_read(unsigned long long* out, int count) {
     return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_fprobe), sizeof(unsigned long long) * count) == hipSuccess

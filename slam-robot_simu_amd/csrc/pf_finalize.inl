@@ -567,7 +567,52 @@ __global__ __launch_bounds__(kFinThreads) void finalize_deferred_kernel(
         // buffer; this step's record went there from write_result_xe
         for (int32_t k = b_first + tid - 1; k < st_now; k += 63) io.res_host[k] = io.res[k];
     }
-    if (s_flag) {
+    if (s_flag && ok && nb <= (int64_t)kFinThreads * kFinRegBlocks) {
+        // fused-block totals of w for the next step's exact cumsum (S1) from the
+        // registers (round 6): lane t holds blocks 2t, 2t + 1 of each half of
+        // 2 kFinThreads blocks; both halves' pair sums scanned over the lanes at
+        // once (wave scans, one barrier).  An approximate prefix: the exact
+        // cumsum classifies against it with a margin, any fixed
+        // order serves.
+        static_assert(kFinRegBlocks == 4, "two halves of lane pairs");
+        double t0[2], t1[2], p[2], tot[2];
+#pragma unroll
+        for (int hf = 0; hf < 2; ++hf) {
+            t0[hf] = has[2 * hf] ? (pm[2 * hf] / s) * q[2 * hf][0] : 0.0;
+            t1[hf] = has[2 * hf + 1] ? (pm[2 * hf + 1] / s) * q[2 * hf + 1][0] : 0.0;
+            p[hf] = t0[hf] + t1[hf];
+        }
+        double inc[2], ex[2];
+#pragma unroll
+        for (int hf = 0; hf < 2; ++hf) {
+            inc[hf] = wave_incl_scan(p[hf]);
+            ex[hf] = inc[hf] - p[hf];
+            if (lane == 63) s_q[hf][wave] = inc[hf];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int hf = 0; hf < 2; ++hf) {
+            double base = 0.0, all = 0.0;
+#pragma unroll
+            for (int w = 0; w < kFinWaves; ++w) {
+                if (w < wave) base = base + s_q[hf][w];
+                all = all + s_q[hf][w];
+            }
+            ex[hf] = base + ex[hf];
+            tot[hf] = all;
+        }
+        ex[1] = tot[0] + ex[1];
+#pragma unroll
+        for (int hf = 0; hf < 2; ++hf) {
+            const int64_t b = fin_blk(tid, 2 * hf);
+            if (b + 1 < nb) {
+                *reinterpret_cast<double2*>(boff + b) = double2{ex[hf], ex[hf] + t0[hf]};
+            } else if (b < nb) {
+                boff[b] = ex[hf];
+            }
+        }
+        if (tid == 0) boff[nb] = tot[0] + tot[1];
+    } else if (s_flag) {
         // fused-block totals of w for the next step's exact cumsum (S1), moved
         // through LDS so that lane t owns the contiguous blocks [t per, (t+1) per)
         auto btot_slow = [&](int64_t b) {
