@@ -448,6 +448,15 @@ int launch_reduce(slam_pf* h, int32_t resampled_known) {
     const int c = h->cur;
     tic(h, 1);
     if (h->deferred) {
+        if (h->nb_part <= kFinThreads * kFinRegBlocks) {
+            finalize_small_kernel<<<1, kFinThreads, 0, s>>>(
+                n, h->dp, h->w_un, h->s_cur, h->tail_leaves, h->tail_ops, h->n_tail_leaves,
+                h->n_tail_ops, h->x[c], h->y[c], h->th[c], h->refp, h->flags, h->cfg.ess_threshold,
+                step_io(h), resampled_known, h->pc.np_recip, h->boff);
+            toc(h, 1);
+            SLAM_HIP_TRY(hipGetLastError());
+            return SLAM_OK;
+        }
         if (h->fsl.nsl > 1)
             finalize_slices_kernel<<<h->fsl.nsl - 1, kFinThreads, 0, s>>>(n, h->dp, h->fsl);
         finalize_deferred_kernel<<<1, kFinThreads, 0, s>>>(
@@ -908,7 +917,7 @@ extern "C" int slam_probe_slow_count(unsigned long long* out) {
 
 #ifdef SLAM_FIN_PROBE
 extern "C" int slam_fin_probe_read(long long* out) {
-    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_fin_probe), sizeof(long long) * 16) == hipSuccess ? 0 : -1;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_fin_probe), sizeof(long long) * 32) == hipSuccess ? 0 : -1;
 }
 #endif
 

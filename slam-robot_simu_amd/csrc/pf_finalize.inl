@@ -22,10 +22,12 @@
 // takes a slow whole-array pass.
 
 #ifdef SLAM_FIN_PROBE
-__device__ long long g_fin_probe[16];
+__device__ long long g_fin_probe[32];
 #define FIN_STAMP(k) do { if (threadIdx.x == 0) g_fin_probe[k] = wall_clock64(); } while (0)
+#define FIN_STAMP_IF(c, k) do { if (c) g_fin_probe[k] = wall_clock64(); } while (0)
 #else
 #define FIN_STAMP(k) do { } while (0)
+#define FIN_STAMP_IF(c, k) do { } while (0)
 #endif
 
 #ifndef SLAM_FIN_THREADS
@@ -204,6 +206,117 @@ __global__ __launch_bounds__(kFinThreads) void finalize_slices_kernel(const int6
         if (lane == 0) sl.q[(int64_t)g * 11 + j] = r;
     }
     if (tid == 0) sl.m[g] = M;
+}
+
+// The next step's fused-block totals of w = w_un / s for its exact cumsum
+// (S1): boff[b] = the exclusive prefix, boff[nb] = the total.  Called by the
+// whole workgroup when the step just finalised resamples next.  pm / q0 /
+// has: the lane's register blocks fin_blk(tid, k) (block max, sum of w_un /
+// M_b); sh: 2048 doubles of LDS; scr: kFinThreads doubles of LDS.
+__device__ void fin_next_prefix(const int64_t n, const int64_t nb, const bool ok, const double s,
+                                const double np_recip, const double (&pm)[kFinRegBlocks],
+                                const double (&q0)[kFinRegBlocks], const bool (&has)[kFinRegBlocks],
+                                const double* __restrict__ w_un, const DeferParts& dp,
+                                double* __restrict__ boff, double* sh, double* scr) {
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    if (ok && nb <= (int64_t)kFinThreads * kFinRegBlocks) {
+        // fused-block totals of w for the next step's exact cumsum (S1) from the
+        // registers (round 6): lane t holds blocks 2t, 2t + 1 of each half of
+        // 2 kFinThreads blocks; both halves' pair sums scanned over the lanes at
+        // once (wave scans, one barrier).  An approximate prefix: the exact
+        // cumsum classifies against it with a margin (DESIGN 6), any fixed
+        // order serves.
+        static_assert(kFinRegBlocks == 4, "two halves of lane pairs");
+        double t0[2], t1[2], p[2], tot[2];
+#pragma unroll
+        for (int hf = 0; hf < 2; ++hf) {
+            t0[hf] = has[2 * hf] ? (pm[2 * hf] / s) * q0[2 * hf] : 0.0;
+            t1[hf] = has[2 * hf + 1] ? (pm[2 * hf + 1] / s) * q0[2 * hf + 1] : 0.0;
+            p[hf] = t0[hf] + t1[hf];
+        }
+        double inc[2], ex[2];
+#pragma unroll
+        for (int hf = 0; hf < 2; ++hf) {
+            inc[hf] = wave_incl_scan(p[hf]);
+            ex[hf] = inc[hf] - p[hf];
+            if (lane == 63) scr[hf * kFinWaves + wave] = inc[hf];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int hf = 0; hf < 2; ++hf) {
+            double base = 0.0, all = 0.0;
+#pragma unroll
+            for (int w = 0; w < kFinWaves; ++w) {
+                if (w < wave) base = base + scr[hf * kFinWaves + w];
+                all = all + scr[hf * kFinWaves + w];
+            }
+            ex[hf] = base + ex[hf];
+            tot[hf] = all;
+        }
+        ex[1] = tot[0] + ex[1];
+#pragma unroll
+        for (int hf = 0; hf < 2; ++hf) {
+            const int64_t b = fin_blk(tid, 2 * hf);
+            if (b + 1 < nb) {
+                *reinterpret_cast<double2*>(boff + b) = double2{ex[hf], ex[hf] + t0[hf]};
+            } else if (b < nb) {
+                boff[b] = ex[hf];
+            }
+        }
+        if (tid == 0) boff[nb] = tot[0] + tot[1];
+    } else {
+        // fused-block totals of w for the next step's exact cumsum (S1), moved
+        // through LDS so that lane t owns the contiguous blocks [t per, (t+1) per)
+        auto btot_slow = [&](int64_t b) {
+            double v = 0.0;
+            const int64_t e = (b + 1) * kPartPer < n ? (b + 1) * kPartPer : n;
+            for (int64_t i = b * kPartPer; i < e; ++i) v += norm_w(w_un[i], s, np_recip);
+            return v;
+        };
+        const bool in_lds = ok && nb <= 2048;
+        if (in_lds) {
+#pragma unroll
+            for (int k = 0; k < kFinRegBlocks; ++k)
+                if (has[k]) sh[fin_blk(tid, k)] = (pm[k] / s) * q0[k];
+        }
+        __syncthreads();
+        auto btot = [&](int64_t b) {
+            if (in_lds) return sh[b];
+            if (ok) return (dp.pmax[b] / s) * dp.ps[0][b];
+            return btot_slow(b);
+        };
+        const int per = (int)((nb + kFinThreads - 1) / kFinThreads);
+        const int64_t b0 = (int64_t)tid * per;
+        // batches of kFinBatch totals (their loads together), then the adds in order
+        auto btot_batch = [&](const int k0, double (&t)[kFinBatch]) {
+#pragma unroll
+            for (int u = 0; u < kFinBatch; ++u) {
+                const int64_t b = b0 + k0 + u;
+                t[u] = (k0 + u < per && b < nb) ? btot(b) : 0.0;
+            }
+        };
+        double loc = 0.0;
+        for (int k0 = 0; k0 < per; k0 += kFinBatch) {
+            double t[kFinBatch];
+            btot_batch(k0, t);
+#pragma unroll
+            for (int u = 0; u < kFinBatch; ++u)
+                if (k0 + u < per && b0 + k0 + u < nb) loc += t[u];
+        }
+        double total;
+        double ex = block_excl_scan<double, kFinThreads>(loc, scr, total);
+        for (int k0 = 0; k0 < per; k0 += kFinBatch) {
+            double t[kFinBatch];
+            btot_batch(k0, t);
+#pragma unroll
+            for (int u = 0; u < kFinBatch; ++u)
+                if (k0 + u < per && b0 + k0 + u < nb) {
+                    boff[b0 + k0 + u] = ex;
+                    ex = ex + t[u];
+                }
+        }
+        if (tid == 0) boff[nb] = total;
+    }
 }
 
 __global__ __launch_bounds__(kFinThreads) void finalize_deferred_kernel(
@@ -553,9 +666,8 @@ __global__ __launch_bounds__(kFinThreads) void finalize_deferred_kernel(
     FIN_STAMP(3);
     if (tid == 0) {
         const int32_t st = io.ctr[0];
-        write_result_xe(tot, s_xe, refp, s, flags, ess_th, io.ess_band, io.res + st, resampled_known,
-                        exp ? io.res_host + st : nullptr);
-        s_flag = flags[kFlagResample];
+        s_flag = write_result_xe(tot, s_xe, refp, s, flags, ess_th, io.ess_band, io.res + st,
+                                 resampled_known, exp ? io.res_host + st : nullptr);
         io.ctr[0] = st + 1;
         io.ctr[1] = io.ctr[1] + 1;
         *s_cur = s;
@@ -567,103 +679,319 @@ __global__ __launch_bounds__(kFinThreads) void finalize_deferred_kernel(
         // buffer; this step's record went there from write_result_xe
         for (int32_t k = b_first + tid - 1; k < st_now; k += 63) io.res_host[k] = io.res[k];
     }
-    if (s_flag && ok && nb <= (int64_t)kFinThreads * kFinRegBlocks) {
-        // fused-block totals of w for the next step's exact cumsum (S1) from the
-        // registers (round 6): lane t holds blocks 2t, 2t + 1 of each half of
-        // 2 kFinThreads blocks; both halves' pair sums scanned over the lanes at
-        // once (wave scans, one barrier).  An approximate prefix: the exact
-        // cumsum classifies against it with a margin (DESIGN 6), any fixed
-        // order serves.
-        static_assert(kFinRegBlocks == 4, "two halves of lane pairs");
-        double t0[2], t1[2], p[2], tot[2];
+    if (s_flag) {
+        double q0[kFinRegBlocks];
 #pragma unroll
-        for (int hf = 0; hf < 2; ++hf) {
-            t0[hf] = has[2 * hf] ? (pm[2 * hf] / s) * q[2 * hf][0] : 0.0;
-            t1[hf] = has[2 * hf + 1] ? (pm[2 * hf + 1] / s) * q[2 * hf + 1][0] : 0.0;
-            p[hf] = t0[hf] + t1[hf];
+        for (int k = 0; k < kFinRegBlocks; ++k) q0[k] = q[k][0];
+        fin_next_prefix(n, nb, ok, s, np_recip, pm, q0, has, w_un, dp, boff, sh, &s_q[0][0]);
+    }
+    FIN_STAMP(5);
+}
+
+// ---------------------------------------------------------------------------
+// NP <= 2^20 (round 6): the same work as
+// finalize_deferred_kernel in an order built around its latencies (phase
+// probe).  The leaves are requested first, so np.sum's buffer chain
+// starts on lane 0 after one round trip and runs while the block partials are
+// still arriving; each wave requests the argmax records of its own candidate
+// blocks (within 2^-48 of the wave's max -- a superset of the global
+// candidates) as soon as the block maxima arrive; the step context and the
+// flag words the record reads are fetched with the partials.
+__global__ __launch_bounds__(kFinThreads) void finalize_small_kernel(
+    const int64_t n, const DeferParts dp, const double* __restrict__ w_un,
+    double* __restrict__ s_cur, const int32_t* __restrict__ tail_leaves,
+    const int32_t* __restrict__ tail_ops, const int32_t n_tail_leaves, const int32_t n_tail_ops,
+    const double* __restrict__ xs, const double* __restrict__ ys, const double* __restrict__ ts,
+    double* __restrict__ refp, int32_t* __restrict__ flags, const double ess_th, StepIO io,
+    const int32_t resampled_known, const double np_recip, double* __restrict__ boff) {
+    static_assert(kFinThreads == 512 && kFinRegBlocks == 4, "the register layout of fin_blk");
+    __shared__ double sh[2048];                      // buffer values / tail leaves / block totals
+    __shared__ double s_q[11][kFinThreads];
+    __shared__ BlockPartial shp[kFinWaves];
+    __shared__ double s_wmax[kFinWaves];
+    __shared__ double s_tot[11];
+    __shared__ double s_s;
+    __shared__ unsigned long long s_min;
+    __shared__ int32_t s_flag;
+    __shared__ int64_t s_mi;
+    __shared__ double s_xe[3];
+    __shared__ int s_ncand;
+    __shared__ int64_t s_cblk[kFinCand];
+    __shared__ FinRecord s_crec[kFinCand];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int64_t nb = (n + kPartPer - 1) / kPartPer;
+    const int64_t nfull = n / kSumChunk;
+    const int64_t nch = (n + kSumChunk - 1) / kSumChunk;
+    FIN_STAMP(0);
+    // the step, the batch's bounds and the flag words the record reads: lane 0,
+    // first in its load queue (used at the end; the wait counts only them)
+    int32_t st_now = 0, b_first = 0, b_last = -1, rstep = 0;
+    FlagWords fw{};
+    double rp[3] = {0.0, 0.0, 0.0};
+    if (tid == 0) {
+        st_now = io.ctr[0];
+        rstep = io.ctr[1];
+        b_first = io.ctr[2];
+        b_last = io.ctr[3];
+        fw = load_flag_words(flags);
+        rp[0] = refp[0];
+        rp[1] = refp[1];
+        rp[2] = refp[2];
+        s_ncand = 0;
+        s_min = ~0ull;
+        s_flag = 0;
+    }
+    // ---- loads: the leaves, then the partials of the lane's blocks
+    // fin_blk(tid, k) (pairs of neighbours, one 16-byte load per array: the
+    // partial arrays hold nb + 1 entries), the step context, the flag words
+    const int part = tid & (kFinLeafLanes - 1);
+    double L[4];
+    {
+        const int64_t c = tid / kFinLeafLanes;
+        const double* Lp = dp.leaf + 16 * (c < nfull ? c : 0) + 4 * part;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) L[j] = Lp[j];
+        __asm__ volatile("" ::: "memory");              // the leaves' loads issue first
+    }
+    double pm[kFinRegBlocks], q[kFinRegBlocks][11];
+    bool has[kFinRegBlocks];
+#pragma unroll
+    for (int kp = 0; kp < kFinRegBlocks / 2; ++kp) {
+        const int64_t b = fin_blk(tid, 2 * kp);
+        has[2 * kp] = b < nb;
+        has[2 * kp + 1] = b + 1 < nb;
+        const int64_t bb = has[2 * kp] ? b : 0;
+        const double2 t = *reinterpret_cast<const double2*>(dp.pmax + bb);
+        pm[2 * kp] = t.x;
+        pm[2 * kp + 1] = t.y;
+    }
+    __asm__ volatile("" ::: "memory");                  // then the partial sums
+#pragma unroll
+    for (int kp = 0; kp < kFinRegBlocks / 2; ++kp) {
+        const int64_t b = fin_blk(tid, 2 * kp);
+        const int64_t bb = b < nb ? b : 0;
+#pragma unroll
+        for (int j = 0; j < 11; ++j) {
+            const double2 u = *reinterpret_cast<const double2*>(dp.ps[j] + bb);
+            q[2 * kp][j] = u.x;
+            q[2 * kp + 1][j] = u.y;
         }
-        double inc[2], ex[2];
+    }
+    // every load above is issued before the first use of a leaf (the scheduler
+    // would otherwise wait for the leaves between them)
+    __asm__ volatile("" ::: "memory");
 #pragma unroll
-        for (int hf = 0; hf < 2; ++hf) {
-            inc[hf] = wave_incl_scan(p[hf]);
-            ex[hf] = inc[hf] - p[hf];
-            if (lane == 63) s_q[hf][wave] = inc[hf];
+    for (int j = 0; j < 4; ++j) __asm__ volatile("" : "+v"(L[j]));
+    // ---- np.sum's buffer values (one round of <= 128 buffers, pairwise inside)
+    {
+        const int64_t c = tid / kFinLeafLanes;
+        double v = (c < nfull) ? (L[0] + L[1]) + (L[2] + L[3]) : 0.0;
+        {
+            const double o = dpp_f64<kDppXor1>(v);
+            v = (part & 1) ? (o + v) : (v + o);          // left operand = lower lane
+        }
+        {
+            const double o = dpp_f64<kDppXor2>(v);
+            v = (part & 2) ? (o + v) : (v + o);
+        }
+        if (part == 0 && c < nfull) sh[c] = v;
+    }
+    __syncthreads();                                     // sh
+    FIN_STAMP(1);
+    double s = 0.0;
+    if (tid == 0 && nfull > 0) {
+        // the buffers left to right while the other waves take their partials
+        __builtin_amdgcn_s_setprio(3);
+        s = lds_chain_sum(s, sh, (int)nfull);
+        __builtin_amdgcn_s_setprio(0);
+    }
+    // ---- block maxima; each wave's argmax candidates (into registers: the
+    // lane's first block within 2^-48 of the wave's max)
+    double mlane = -1.0;
+#pragma unroll
+    for (int k = 0; k < kFinRegBlocks; ++k)
+        if (has[k]) mlane = fmax(mlane, pm[k]);
+    const double wm = wave_max_f64(mlane);
+    if (lane == 0) s_wmax[wave] = wm;
+    double cpm = -1.0;
+    int64_t cblk = -1;
+#pragma unroll
+    for (int k = kFinRegBlocks - 1; k >= 0; --k) {
+        if (has[k] && pm[k] >= wm * (1.0 - 0x1p-48)) {
+            cpm = pm[k];
+            cblk = fin_blk(tid, k);
+        }
+    }
+    FinRecord cr{};
+    if (cblk >= 0) fin_load_record(dp, cblk, cr);
+    __asm__ volatile("" ::: "memory");                  // requested before the sums wait
+    // ---- lane partial sums scaled to the lane's max
+    double acc[11];
+#pragma unroll
+    for (int j = 0; j < 11; ++j) acc[j] = 0.0;
+    if (mlane > 0.0) {
+        const double rm = 1.0 / mlane;
+#pragma unroll
+        for (int k = 0; k < kFinRegBlocks; ++k) {
+            if (has[k]) {
+                const double r = pm[k] * rm;
+                acc[0] += r * q[k][0];
+                acc[1] += (r * r) * q[k][1];
+#pragma unroll
+                for (int j = 2; j < 11; ++j) acc[j] += r * q[k][j];
+            }
+        }
+    }
+    __syncthreads();                                     // s_wmax
+    double M = s_wmax[0];
+#pragma unroll
+    for (int w = 1; w < kFinWaves; ++w) M = fmax(M, s_wmax[w]);
+    {
+        const double rl = (mlane > 0.0 && M > 0.0) ? mlane / M : 0.0;
+        acc[0] *= rl;
+        acc[1] *= rl * rl;
+#pragma unroll
+        for (int j = 2; j < 11; ++j) acc[j] *= rl;
+#pragma unroll
+        for (int j = 0; j < 11; ++j) s_q[j][tid] = acc[j];
+    }
+    if (cblk >= 0 && cpm >= M * (1.0 - 0x1p-48)) {
+        const int slot = atomicAdd(&s_ncand, 1);
+        if (slot < kFinCand) {
+            s_cblk[slot] = cblk;
+            s_crec[slot] = cr;
+        }
+    }
+    if (nch > nfull) {
+        __syncthreads();                                 // sh reused by the tail
+        const double tsum = tail_chunk_sum(w_un + nfull * kSumChunk, tail_leaves, tail_ops,
+                                           n_tail_leaves, n_tail_ops, sh);
+        if (tid == 0) s = s + tsum;
+    }
+    if (tid == 0) s_s = s;
+    __syncthreads();
+    s = s_s;
+    FIN_STAMP(2);
+    const bool ok = (s > 0.0) && !isinf(s) && (M > 0.0);
+    BlockPartial tot;
+    bp_zero(tot);
+    if (ok) {
+        // ---- the 11 sums: wave w reduces quantities w and w + 8
+        for (int j = wave; j < 11; j += kFinWaves) {
+            double r = s_q[j][lane];
+#pragma unroll
+            for (int m = 1; m < kFinThreads / 64; ++m) r = r + s_q[j][lane + 64 * m];
+#pragma unroll
+            for (int d = 1; d < 64; d <<= 1) {
+                const double o = xor_f64(r, d);
+                r = (lane & d) ? (o + r) : (r + o);
+            }
+            if (lane == 0) s_tot[j] = r;
+        }
+        // ---- argmax: the first block whose max rounds to fl(M / s)
+        const double mval = M / s;
+        unsigned long long cb = ~0ull;
+#pragma unroll
+        for (int k = kFinRegBlocks - 1; k >= 0; --k)
+            if (has[k] && pm[k] >= M * (1.0 - 0x1p-48) && pm[k] / s == mval)
+                cb = (unsigned long long)fin_blk(tid, k);
+        if (cb != ~0ull) atomicMin(&s_min, cb);
+        __syncthreads();
+        const int64_t bc = (int64_t)s_min;
+        if (tid == 0) {
+            // block bc's record: staged, or loaded if it was not a staged candidate
+            int slot = -1;
+            const int nc = min(s_ncand, kFinCand);
+            for (int j = 0; j < nc; ++j)
+                if (s_cblk[j] == bc) slot = j;
+            FinRecord f;
+            if (slot >= 0) f = s_crec[slot];
+            else fin_load_record(dp, bc, f);
+            s_mi = f.pi;
+            s_xe[0] = f.xe[0];
+            s_xe[1] = f.xe[1];
+            s_xe[2] = f.xe[2];
+            s_flag = (f.pre / s == mval) ? 1 : 0;
+            if (s_flag) s_min = ~0ull;
         }
         __syncthreads();
-#pragma unroll
-        for (int hf = 0; hf < 2; ++hf) {
-            double base = 0.0, all = 0.0;
-#pragma unroll
-            for (int w = 0; w < kFinWaves; ++w) {
-                if (w < wave) base = base + s_q[hf][w];
-                all = all + s_q[hf][w];
+        if (s_flag) {
+            // a smaller weight ahead of the block max rounds to the same maximum:
+            // the first index of the block whose w equals mval
+            for (int e = tid; e < kPartPer; e += kFinThreads) {
+                const int64_t i = bc * kPartPer + e;
+                if (i < n && norm_w(w_un[i], s, np_recip) == mval)
+                    atomicMin(&s_min, (unsigned long long)i);
             }
-            ex[hf] = base + ex[hf];
-            tot[hf] = all;
-        }
-        ex[1] = tot[0] + ex[1];
-#pragma unroll
-        for (int hf = 0; hf < 2; ++hf) {
-            const int64_t b = fin_blk(tid, 2 * hf);
-            if (b + 1 < nb) {
-                *reinterpret_cast<double2*>(boff + b) = double2{ex[hf], ex[hf] + t0[hf]};
-            } else if (b < nb) {
-                boff[b] = ex[hf];
+            __syncthreads();
+            if (tid == 0) {
+                const int64_t i = (int64_t)s_min;
+                s_mi = i;
+                s_xe[0] = xs[i];
+                s_xe[1] = ys[i];
+                s_xe[2] = ts[i];
             }
         }
-        if (tid == 0) boff[nb] = tot[0] + tot[1];
-    } else if (s_flag) {
-        // fused-block totals of w for the next step's exact cumsum (S1), moved
-        // through LDS so that lane t owns the contiguous blocks [t per, (t+1) per)
-        auto btot_slow = [&](int64_t b) {
-            double v = 0.0;
-            const int64_t e = (b + 1) * kPartPer < n ? (b + 1) * kPartPer : n;
-            for (int64_t i = b * kPartPer; i < e; ++i) v += norm_w(w_un[i], s, np_recip);
-            return v;
-        };
-        const bool in_lds = ok && nb <= 2048;
-        if (in_lds) {
-#pragma unroll
-            for (int k = 0; k < kFinRegBlocks; ++k)
-                if (has[k]) sh[fin_blk(tid, k)] = (pm[k] / s) * q[k][0];
+        if (tid == 0) {
+            const double f = M / s;                      // back from max-relative to w_un / s
+            tot.maxv = mval;
+            tot.maxi = s_mi;
+            tot.sw = s_tot[0] * f;
+            tot.sw2 = s_tot[1] * (f * f);
+            for (int j = 0; j < 3; ++j) tot.m1[j] = s_tot[2 + j] * f;
+            for (int j = 0; j < 6; ++j) tot.m2[j] = s_tot[5 + j] * f;
         }
-        __syncthreads();
-        auto btot = [&](int64_t b) {
-            if (in_lds) return sh[b];
-            if (ok) return (dp.pmax[b] / s) * dp.ps[0][b];
-            return btot_slow(b);
-        };
-        const int per = (int)((nb + kFinThreads - 1) / kFinThreads);
-        const int64_t b0 = (int64_t)tid * per;
-        // batches of kFinBatch totals (their loads together), then the adds in order
-        auto btot_batch = [&](const int k0, double (&t)[kFinBatch]) {
-#pragma unroll
-            for (int u = 0; u < kFinBatch; ++u) {
-                const int64_t b = b0 + k0 + u;
-                t[u] = (k0 + u < per && b < nb) ? btot(b) : 0.0;
-            }
-        };
-        double loc = 0.0;
-        for (int k0 = 0; k0 < per; k0 += kFinBatch) {
-            double t[kFinBatch];
-            btot_batch(k0, t);
-#pragma unroll
-            for (int u = 0; u < kFinBatch; ++u)
-                if (k0 + u < per && b0 + k0 + u < nb) loc += t[u];
+    } else {
+        // ---- every weight through the reference's division (slow, degenerate case)
+        BlockPartial a;
+        bp_zero(a);
+        const double r0 = refp[0], r1 = refp[1], r2 = refp[2];
+        for (int64_t i = tid; i < n; i += kFinThreads) {
+            const double v = norm_w(w_un[i], s, np_recip);
+            BlockPartial o;
+            o.maxv = v;
+            o.maxi = i;
+            o.sw = v;
+            o.sw2 = v * v;
+            const double d0 = xs[i] - r0, d1 = ys[i] - r1, d2 = ts[i] - r2;
+            const double v0 = v * d0, v1 = v * d1, v2 = v * d2;
+            o.m1[0] = v0; o.m1[1] = v1; o.m1[2] = v2;
+            o.m2[0] = v0 * d0; o.m2[1] = v0 * d1; o.m2[2] = v0 * d2;
+            o.m2[3] = v1 * d1; o.m2[4] = v1 * d2; o.m2[5] = v2 * d2;
+            bp_merge(a, o);
         }
-        double total;
-        double ex = block_excl_scan<double, kFinThreads>(loc, s_q[0], total);
-        for (int k0 = 0; k0 < per; k0 += kFinBatch) {
-            double t[kFinBatch];
-            btot_batch(k0, t);
-#pragma unroll
-            for (int u = 0; u < kFinBatch; ++u)
-                if (k0 + u < per && b0 + k0 + u < nb) {
-                    boff[b0 + k0 + u] = ex;
-                    ex = ex + t[u];
-                }
+        tot = bp_block_reduce(a, shp);
+        if (tid == 0) {
+            s_xe[0] = xs[tot.maxi];
+            s_xe[1] = ys[tot.maxi];
+            s_xe[2] = ts[tot.maxi];
         }
-        if (tid == 0) boff[nb] = total;
+    }
+    FIN_STAMP(3);
+    __shared__ int32_t s_exp[3];
+    if (tid == 0) {
+        const bool exp = io.res_host != nullptr && st_now == b_last && b_first <= b_last;
+        s_exp[0] = exp ? 1 : 0;
+        s_exp[1] = b_first;
+        s_exp[2] = st_now;
+        s_flag = write_result_fw(tot, s_xe, refp, rp, s, flags, fw, ess_th, io.ess_band,
+                                 io.res + st_now, resampled_known, exp ? io.res_host + st_now : nullptr);
+        io.ctr[0] = st_now + 1;
+        io.ctr[1] = rstep + 1;
+        *s_cur = s;
+    }
+    __syncthreads();
+    FIN_STAMP(4);
+    if (s_exp[0] && tid >= 1 && tid < 64) {
+        // the batch's earlier records (stored by earlier launches) to the host
+        // buffer; this step's record went there from write_result_fw
+        for (int32_t k = s_exp[1] + tid - 1; k < s_exp[2]; k += 63) io.res_host[k] = io.res[k];
+    }
+    if (s_flag) {
+        double q0[kFinRegBlocks];
+#pragma unroll
+        for (int k = 0; k < kFinRegBlocks; ++k) q0[k] = q[k][0];
+        fin_next_prefix(n, nb, ok, s, np_recip, pm, q0, has, w_un, dp, boff, sh, &s_q[0][0]);
     }
     FIN_STAMP(5);
 }

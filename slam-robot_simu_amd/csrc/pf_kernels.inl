@@ -1763,8 +1763,19 @@ __device__ void write_result(const BlockPartial& r, const double* xs, const doub
 }
 
 // result record with x_est given (deferred path: taken from the block partials)
-__device__ void write_result_xe(const BlockPartial& r, const double* xe, double* refp,
-                                const double s, int32_t* flags, const double ess_th,
+// The flag words the step's record reads (fetched early by the finalize, whose
+// record is on the step's critical path)
+struct FlagWords {
+    int32_t resample, status, n_special, dd_waves, mark_gen;
+};
+__device__ __forceinline__ FlagWords load_flag_words(const int32_t* flags) {
+    return FlagWords{flags[kFlagResample], flags[kFlagStatus], flags[kFlagNSpecial],
+                     flags[kFlagDDWaves], flags[kFlagMarkGen]};
+}
+
+__device__ int32_t write_result_fw(const BlockPartial& r, const double* xe, double* refp,
+                                const double (&rp)[3], const double s, int32_t* flags,
+                                const FlagWords fw, const double ess_th,
                                 const double ess_band, slam_pf_result* res,
                                 const int32_t resampled_known, slam_pf_result* res_host = nullptr) {
     slam_pf_result o;
@@ -1780,26 +1791,37 @@ __device__ void write_result_xe(const BlockPartial& r, const double* xe, double*
         for (int b = 0; b < 3; ++b) o.cov[3 * a + b] = m2[3 * a + b] * inv - mu[a] * mu[b];
     o.ess = 1.0 / r.sw2;
     o.weight_sum = s;
-    o.resampled = resampled_known >= 0 ? resampled_known : (flags[kFlagResample] != 0);
+    o.resampled = resampled_known >= 0 ? resampled_known : (fw.resample != 0);
     o.resample_next = (o.ess < ess_th) ? 1 : 0;
     o.ess_near = (fabs(o.ess - ess_th) <= ess_band * ess_th) ? 1 : 0;
-    o.status = flags[kFlagStatus];
-    o.n_special = flags[kFlagNSpecial];
-    o.dd_waves = flags[kFlagDDWaves];
+    o.status = fw.status;
+    o.n_special = fw.n_special;
+    o.dd_waves = fw.dd_waves;
     flags[kFlagDDWaves] = 0;
     flags[kFlagResample] = o.resample_next;
-    flags[kFlagMarkGen] = flags[kFlagMarkGen] + 1;
+    flags[kFlagMarkGen] = fw.mark_gen + 1;
     flags[kFlagStatus] = 0;
     // the estimate, kept two steps deep as the expansion's reference
     // (closed_prep_reference: the argmax particle is the same bits however
     // the filter is sharded, which a summed mean would not be)
     for (int k = 0; k < 3; ++k) {
-        refp[4 + k] = refp[k];
+        refp[4 + k] = rp[k];
         refp[k] = o.x_est[k];
     }
     refp[7] = 2.0;
     *res = o;
     if (res_host) *res_host = o;
+    return o.resample_next;
+}
+
+// returns resample_next (the flag it stored)
+__device__ int32_t write_result_xe(const BlockPartial& r, const double* xe, double* refp,
+                                const double s, int32_t* flags, const double ess_th,
+                                const double ess_band, slam_pf_result* res,
+                                const int32_t resampled_known, slam_pf_result* res_host = nullptr) {
+    const double rp[3] = {refp[0], refp[1], refp[2]};
+    return write_result_fw(r, xe, refp, rp, s, flags, load_flag_words(flags), ess_th, ess_band, res,
+                           resampled_known, res_host);
 }
 
 // One normalise block = kNormPer particles (kNormThreads lanes x kNormEPT,

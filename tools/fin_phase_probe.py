@@ -17,7 +17,7 @@ import bench  # noqa: E402
 from slamhip.pf import DeviceParticleFilter  # noqa: E402
 
 lib = C.CDLL(os.environ["SLAM_HIP_LIB"])
-buf = (C.c_longlong * 16)()
+buf = (C.c_longlong * 32)()
 n = int(os.environ.get("FP_N", str(1 << 20)))
 lm, zs, (vel, omega, dt) = bench.simulate_world(700)
 ctl = np.tile([vel, omega], (700, 1))
