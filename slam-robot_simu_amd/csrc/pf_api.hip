@@ -448,11 +448,15 @@ int launch_reduce(slam_pf* h, int32_t resampled_known) {
     const int c = h->cur;
     tic(h, 1);
     if (h->deferred) {
-        if (h->nb_part <= kFinThreads * kFinRegBlocks) {
-            finalize_small_kernel<<<1, kFinThreads, 0, s>>>(
+        const bool sliced = h->fsl.nsl > 1;
+        if (!sliced || (h->fsl.nsl <= kFinFastSlices && n / kSumChunk <= 2048)) {
+            if (sliced)
+                finalize_slices_kernel<<<h->fsl.nsl - 1, kFinThreads, 0, s>>>(n, h->dp, h->fsl);
+            auto kern = sliced ? finalize_fast_kernel<true> : finalize_fast_kernel<false>;
+            kern<<<1, kFinThreads, 0, s>>>(
                 n, h->dp, h->w_un, h->s_cur, h->tail_leaves, h->tail_ops, h->n_tail_leaves,
                 h->n_tail_ops, h->x[c], h->y[c], h->th[c], h->refp, h->flags, h->cfg.ess_threshold,
-                step_io(h), resampled_known, h->pc.np_recip, h->boff);
+                step_io(h), resampled_known, h->pc.np_recip, h->boff, h->fsl);
             toc(h, 1);
             SLAM_HIP_TRY(hipGetLastError());
             return SLAM_OK;
@@ -801,6 +805,11 @@ int create_impl(const slam_pf_config* cfg, int64_t n_local, int64_t n_global, in
         A(h->fsl.m, h->fsl.nsl);
         A(h->fsl.q, 11 * (size_t)h->fsl.nsl);
         A(h->fsl.buf, std::max<int64_t>(n / kSumChunk, 1));
+        A(h->fsl.cblk, kSliceCand * (size_t)h->fsl.nsl);
+        A(h->fsl.cpm, kSliceCand * (size_t)h->fsl.nsl);
+        A(h->fsl.ncand, h->fsl.nsl);
+        A(h->fsl.pre, h->nb_part + 1);
+        A(h->fsl.u, h->fsl.nsl);
     }
     SLAM_HIP_TRY(hipMemsetAsync(h->dp.mark, 0xff, sizeof(int64_t) * npad, h->stream));
     SLAM_HIP_TRY(hipMemsetAsync(h->dp.carry, 0, sizeof(int32_t) * (h->nb_part + 1), h->stream));

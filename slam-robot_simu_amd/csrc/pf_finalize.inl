@@ -41,6 +41,7 @@ constexpr int kFinBufPerRound = kFinThreads / kFinLeafLanes;   // 128 buffers pe
 constexpr int kFinCand = 8;                 // argmax candidate records staged in LDS
 constexpr int kFinBatch = 8;                // loads in flight per lane beyond the registers (NP > 2^20)
 constexpr int kFinSumBatch = 2;             // blocks (12 loads each) in flight in the sums pass
+constexpr int kFinPrefixRounds = 32;        // the next step's block prefix in registers (NP <= 2^23)
 
 struct FinRecord {
     double pre, xe[3];
@@ -65,22 +66,28 @@ static_assert(kSumChunk == 16 * kPartPer, "a buffer is 16 fused blocks, 4 per np
 __device__ __forceinline__ double lds_chain_sum(double s, const double* a, const int cnt) {
     constexpr int B = 16;
     int k = 0;
-    if (cnt >= B) {
-        double cur[B];
+    if (cnt >= 2 * B) {
+        // two register batches alternating (no copy between them): batch A
+        // holds [k, k + B), B the next B; each is refilled while the other
+        // is added
+        double ra[B], rb[B];
 #pragma unroll
-        for (int j = 0; j < B; ++j) cur[j] = a[j];
-        for (; k + 2 * B <= cnt; k += B) {
-            double nxt[B];
+        for (int j = 0; j < B; ++j) ra[j] = a[j];
+        for (; k + 2 * B <= cnt; k += 2 * B) {
 #pragma unroll
-            for (int j = 0; j < B; ++j) nxt[j] = a[k + B + j];
+            for (int j = 0; j < B; ++j) rb[j] = a[k + B + j];
+            __asm__ volatile("" ::: "memory");          // (the reads before the adds)
+            __asm__ volatile("" : "+v"(s));
 #pragma unroll
-            for (int j = 0; j < B; ++j) s = s + cur[j];
+            for (int j = 0; j < B; ++j) s = s + ra[j];
+            const int nk = (k + 3 * B <= cnt) ? k + 2 * B : k;   // past the end: a harmless re-read
 #pragma unroll
-            for (int j = 0; j < B; ++j) cur[j] = nxt[j];
+            for (int j = 0; j < B; ++j) ra[j] = a[nk + j];
+            __asm__ volatile("" ::: "memory");
+            __asm__ volatile("" : "+v"(s));
+#pragma unroll
+            for (int j = 0; j < B; ++j) s = s + rb[j];
         }
-#pragma unroll
-        for (int j = 0; j < B; ++j) s = s + cur[j];
-        k += B;
     }
     for (; k < cnt; ++k) s = s + a[k];
     return s;
@@ -104,10 +111,16 @@ __device__ __forceinline__ int64_t fin_blk(const int t, const int k) {
 // must be exactly one round of buffers (16 blocks each), i.e. 512 lanes
 static_assert(kFinThreads * kFinRegBlocks == 16 * kFinBufPerRound,
               "a finalize slice (2048 fused blocks) must span kFinBufPerRound buffers");
+constexpr int kSliceCand = 4;               // argmax candidate blocks a slice lists
 struct FinSlices {
     double* m;          // [nsl] slice max (slice 0: the finalize's own)
     double* q;          // [nsl][11] slice sums scaled to the slice max
     double* buf;        // [nfull] np.sum value of each full 8192-element buffer
+    int64_t* cblk;      // [nsl][kSliceCand] blocks with M_b within 2^-48 of the slice max
+    double* cpm;        // [nsl][kSliceCand] their maxima
+    int32_t* ncand;     // [nsl] how many there were (> kSliceCand: the slice is scanned)
+    double* pre;        // [nb] the next step's block prefix inside each slice, w_un units
+    double* u;          // [nsl] the slice's total of w_un (pre's units)
     int32_t nsl;        // slices of 2048 fused blocks; <= 1: no pre-pass
 };
 
@@ -116,8 +129,13 @@ __global__ __launch_bounds__(kFinThreads) void finalize_slices_kernel(const int6
                                                                       const FinSlices sl) {
     __shared__ double s_q[11][kFinThreads];
     __shared__ double s_wmax[kFinWaves];
+    __shared__ int s_nc;
+    __shared__ int64_t s_cb[kSliceCand];
+    __shared__ double s_cp[kSliceCand];
+    __shared__ double s_pw[2][kFinWaves];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int g = 1 + (int)blockIdx.x;
+    if (tid == 0) s_nc = 0;
     const int64_t nb = (n + kPartPer - 1) / kPartPer;
     const int64_t nfull = n / kSumChunk;
     const int64_t b_base = (int64_t)g * kFinThreads * kFinRegBlocks;
@@ -193,7 +211,54 @@ __global__ __launch_bounds__(kFinThreads) void finalize_slices_kernel(const int6
 #pragma unroll
         for (int j = 0; j < 11; ++j) s_q[j][tid] = acc[j];
     }
+    // the slice's argmax candidates (a global candidate in this slice is one:
+    // the global max is >= M); the finalize checks them instead of the slice
+#pragma unroll
+    for (int k = 0; k < kFinRegBlocks; ++k) {
+        if (has[k] && pm[k] >= M * (1.0 - 0x1p-48)) {
+            const int slot = atomicAdd(&s_nc, 1);
+            if (slot < kSliceCand) {
+                s_cb[slot] = b_base + fin_blk(tid, k);
+                s_cp[slot] = pm[k];
+            }
+        }
+    }
+    // the next step's block prefix (S1) inside the slice in w_un units (M_b
+    // times the block's sum of w_un / M_b): the finalize scales it by 1 / s
+    // and offsets it by the slices before, when the next step resamples
+    double u0[2], u1[2], pex[2];
+#pragma unroll
+    for (int hf = 0; hf < 2; ++hf) {
+        u0[hf] = has[2 * hf] ? pm[2 * hf] * q[2 * hf][0] : 0.0;
+        u1[hf] = has[2 * hf + 1] ? pm[2 * hf + 1] * q[2 * hf + 1][0] : 0.0;
+        const double pr = u0[hf] + u1[hf];
+        const double inc = wave_incl_scan_rows(pr);
+        pex[hf] = inc - pr;
+        if (lane == 63) s_pw[hf][wave] = inc;
+    }
     __syncthreads();
+    {
+        double tot[2];
+#pragma unroll
+        for (int hf = 0; hf < 2; ++hf) {
+            double base = 0.0, all = 0.0;
+#pragma unroll
+            for (int w = 0; w < kFinWaves; ++w) {
+                if (w < wave) base = base + s_pw[hf][w];
+                all = all + s_pw[hf][w];
+            }
+            pex[hf] = base + pex[hf];
+            tot[hf] = all;
+        }
+        pex[1] = tot[0] + pex[1];
+#pragma unroll
+        for (int hf = 0; hf < 2; ++hf) {
+            const int64_t b = b_base + fin_blk(tid, 2 * hf);
+            if (b + 1 < nb) *reinterpret_cast<double2*>(sl.pre + b) = double2{pex[hf], pex[hf] + u0[hf]};
+            else if (b < nb) sl.pre[b] = pex[hf];
+        }
+        if (tid == 0) sl.u[g] = tot[0] + tot[1];
+    }
     for (int j = wave; j < 11; j += kFinWaves) {
         double r = s_q[j][lane];
 #pragma unroll
@@ -205,7 +270,15 @@ __global__ __launch_bounds__(kFinThreads) void finalize_slices_kernel(const int6
         }
         if (lane == 0) sl.q[(int64_t)g * 11 + j] = r;
     }
-    if (tid == 0) sl.m[g] = M;
+    if (tid < kSliceCand) {
+        const bool in = tid < s_nc;
+        sl.cblk[g * kSliceCand + tid] = in ? s_cb[tid] : -1;
+        sl.cpm[g * kSliceCand + tid] = in ? s_cp[tid] : -1.0;
+    }
+    if (tid == 0) {
+        sl.m[g] = M;
+        sl.ncand[g] = s_nc;
+    }
 }
 
 // The next step's fused-block totals of w = w_un / s for its exact cumsum
@@ -237,7 +310,7 @@ __device__ void fin_next_prefix(const int64_t n, const int64_t nb, const bool ok
         double inc[2], ex[2];
 #pragma unroll
         for (int hf = 0; hf < 2; ++hf) {
-            inc[hf] = wave_incl_scan(p[hf]);
+            inc[hf] = wave_incl_scan_rows(p[hf]);
             ex[hf] = inc[hf] - p[hf];
             if (lane == 63) scr[hf * kFinWaves + wave] = inc[hf];
         }
@@ -264,6 +337,62 @@ __device__ void fin_next_prefix(const int64_t n, const int64_t nb, const bool ok
             }
         }
         if (tid == 0) boff[nb] = tot[0] + tot[1];
+    } else if (ok && (nb + kFinWaves * 64 - 1) / (kFinWaves * 64) <= kFinPrefixRounds) {
+        // NP <= 2^23 (round 6: the batched form below took 39 us at 2^23): wave
+        // w takes the contiguous blocks [w R 64, (w+1) R 64) in R rounds of 64
+        // (lane l: block w R 64 + 64 r + l, coalesced), every load issued
+        // first; inclusive wave scans carry the running total over the rounds,
+        // then the waves' totals in order
+        const int R = (int)((nb + kFinWaves * 64 - 1) / (kFinWaves * 64));
+        const int64_t wb0 = (int64_t)wave * R * 64;
+        double pv[kFinPrefixRounds], qv[kFinPrefixRounds];
+#pragma unroll
+        for (int r = 0; r < kFinPrefixRounds; ++r) {
+            if (r < R) {
+                const int64_t b = wb0 + 64 * r + lane;
+                const int64_t bb = b < nb ? b : 0;
+                pv[r] = dp.pmax[bb];
+                qv[r] = dp.ps[0][bb];
+            }
+        }
+        // the rounds' scans are independent (interleaved by the scheduler); the
+        // running total over the rounds is added after
+        double ex[kFinPrefixRounds], rt[kFinPrefixRounds];
+#pragma unroll
+        for (int r = 0; r < kFinPrefixRounds; ++r) {
+            if (r < R) {
+                const int64_t b = wb0 + 64 * r + lane;
+                const double t = b < nb ? (pv[r] / s) * qv[r] : 0.0;
+                const double inc = wave_incl_scan_rows(t);
+                ex[r] = inc - t;
+                rt[r] = __longlong_as_double(
+                    (long long)readlane_int((uint64_t)__double_as_longlong(inc), 63));
+            }
+        }
+        double run = 0.0;
+#pragma unroll
+        for (int r = 0; r < kFinPrefixRounds; ++r) {
+            if (r < R) {
+                ex[r] = run + ex[r];
+                run = run + rt[r];
+            }
+        }
+        if (lane == 0) scr[wave] = run;
+        __syncthreads();
+        double base = 0.0, all = 0.0;
+#pragma unroll
+        for (int w = 0; w < kFinWaves; ++w) {
+            if (w < wave) base = base + scr[w];
+            all = all + scr[w];
+        }
+#pragma unroll
+        for (int r = 0; r < kFinPrefixRounds; ++r) {
+            if (r < R) {
+                const int64_t b = wb0 + 64 * r + lane;
+                if (b < nb) boff[b] = base + ex[r];
+            }
+        }
+        if (tid == 0) boff[nb] = all;
     } else {
         // fused-block totals of w for the next step's exact cumsum (S1), moved
         // through LDS so that lane t owns the contiguous blocks [t per, (t+1) per)
@@ -689,22 +818,36 @@ __global__ __launch_bounds__(kFinThreads) void finalize_deferred_kernel(
 }
 
 // ---------------------------------------------------------------------------
-// NP <= 2^20 (round 6): the same work as
+// NP <= 2^24 (round 6): the same work as
 // finalize_deferred_kernel in an order built around its latencies (phase
 // probe).  The leaves are requested first, so np.sum's buffer chain
 // starts on lane 0 after one round trip and runs while the block partials are
 // still arriving; each wave requests the argmax records of its own candidate
 // blocks (within 2^-48 of the wave's max -- a superset of the global
 // candidates) as soon as the block maxima arrive; the step context and the
-// flag words the record reads are fetched with the partials.
-__global__ __launch_bounds__(kFinThreads) void finalize_small_kernel(
+// flag words the record reads are fetched with the partials.  SLICED (NP >
+// 2^20, finalize_slices_kernel ran first): the slices' buffer values, maxima,
+// sums and argmax candidate lists are fetched in the same first round trip,
+// so the chain runs over every buffer from LDS and the argmax checks the
+// listed candidates instead of walking the blocks beyond the registers.
+constexpr int kFinFastSlices = 16;          // SLICED: NP <= 2^24
+constexpr int kFinSlBuf = 4;                // SLICED: slice buffer values per lane (nfull <= 2048)
+template <bool SLICED>
+__global__ __launch_bounds__(kFinThreads) void finalize_fast_kernel(
     const int64_t n, const DeferParts dp, const double* __restrict__ w_un,
     double* __restrict__ s_cur, const int32_t* __restrict__ tail_leaves,
     const int32_t* __restrict__ tail_ops, const int32_t n_tail_leaves, const int32_t n_tail_ops,
     const double* __restrict__ xs, const double* __restrict__ ys, const double* __restrict__ ts,
     double* __restrict__ refp, int32_t* __restrict__ flags, const double ess_th, StepIO io,
-    const int32_t resampled_known, const double np_recip, double* __restrict__ boff) {
+    const int32_t resampled_known, const double np_recip, double* __restrict__ boff,
+    const FinSlices sl) {
     static_assert(kFinThreads == 512 && kFinRegBlocks == 4, "the register layout of fin_blk");
+    static_assert(kFinSlBuf * kFinThreads + kFinBufPerRound >= 2048, "every buffer of sh");
+    static_assert((kFinFastSlices - 1) * 11 <= kFinThreads, "one slice sum per lane");
+    __shared__ double s_slm[kFinFastSlices];
+    __shared__ double s_slq[kFinFastSlices][11];
+    __shared__ int32_t s_slnc[kFinFastSlices];
+    __shared__ double s_slu[kFinFastSlices];
     __shared__ double sh[2048];                      // buffer values / tail leaves / block totals
     __shared__ double s_q[11][kFinThreads];
     __shared__ BlockPartial shp[kFinWaves];
@@ -744,6 +887,18 @@ __global__ __launch_bounds__(kFinThreads) void finalize_small_kernel(
     // ---- loads: the leaves, then the partials of the lane's blocks
     // fin_blk(tid, k) (pairs of neighbours, one 16-byte load per array: the
     // partial arrays hold nb + 1 entries), the step context, the flag words
+    // SLICED: the slices' buffer values first (the chain reads them right after
+    // the first round's), then the leaves
+    const int nsl = SLICED ? sl.nsl : 1;
+    double bufv[kFinSlBuf] = {};
+    if constexpr (SLICED) {
+#pragma unroll
+        for (int k = 0; k < kFinSlBuf; ++k) {
+            const int64_t c = kFinBufPerRound + tid + (int64_t)kFinThreads * k;
+            if (c < nfull) bufv[k] = sl.buf[c];
+        }
+        __asm__ volatile("" ::: "memory");
+    }
     const int part = tid & (kFinLeafLanes - 1);
     double L[4];
     {
@@ -777,11 +932,30 @@ __global__ __launch_bounds__(kFinThreads) void finalize_small_kernel(
             q[2 * kp + 1][j] = u.y;
         }
     }
+    // SLICED: the slices' maxima, candidate lists and sums
+    double slm = -1.0, slq = 0.0, ccp = -1.0, slu = 0.0;
+    int64_t ccb = -1;
+    int32_t sncv = 0;
+    if constexpr (SLICED) {
+        if (tid >= 1 && tid < nsl) {
+            slm = sl.m[tid];
+            sncv = sl.ncand[tid];
+            slu = sl.u[tid];
+        }
+        if (tid < (nsl - 1) * kSliceCand) {
+            const int g = 1 + tid / kSliceCand;
+            ccb = sl.cblk[g * kSliceCand + tid % kSliceCand];
+            ccp = sl.cpm[g * kSliceCand + tid % kSliceCand];     // unlisted: -1
+        }
+        if (tid < (nsl - 1) * 11) slq = sl.q[11 + tid];
+    }
     // every load above is issued before the first use of a leaf (the scheduler
     // would otherwise wait for the leaves between them)
     __asm__ volatile("" ::: "memory");
 #pragma unroll
     for (int j = 0; j < 4; ++j) __asm__ volatile("" : "+v"(L[j]));
+#pragma unroll
+    for (int k = 0; k < kFinSlBuf; ++k) __asm__ volatile("" : "+v"(bufv[k]));
     // ---- np.sum's buffer values (one round of <= 128 buffers, pairwise inside)
     {
         const int64_t c = tid / kFinLeafLanes;
@@ -796,11 +970,20 @@ __global__ __launch_bounds__(kFinThreads) void finalize_small_kernel(
         }
         if (part == 0 && c < nfull) sh[c] = v;
     }
+    if constexpr (SLICED) {
+#pragma unroll
+        for (int k = 0; k < kFinSlBuf; ++k) {
+            const int64_t c = kFinBufPerRound + tid + (int64_t)kFinThreads * k;
+            if (c < nfull) sh[c] = bufv[k];
+        }
+    }
     __syncthreads();                                     // sh
     FIN_STAMP(1);
     double s = 0.0;
     if (tid == 0 && nfull > 0) {
         // the buffers left to right while the other waves take their partials
+        // (a whole wave walking the lanes by readlane measured slower: 14.9
+        // against 8.8 us for the 1,024 buffers of 2^23)
         __builtin_amdgcn_s_setprio(3);
         s = lds_chain_sum(s, sh, (int)nfull);
         __builtin_amdgcn_s_setprio(0);
@@ -811,8 +994,16 @@ __global__ __launch_bounds__(kFinThreads) void finalize_small_kernel(
 #pragma unroll
     for (int k = 0; k < kFinRegBlocks; ++k)
         if (has[k]) mlane = fmax(mlane, pm[k]);
-    const double wm = wave_max_f64(mlane);
+    const double wm = wave_max_f64(SLICED ? fmax(mlane, slm) : mlane);   // + the slices' maxima
     if (lane == 0) s_wmax[wave] = wm;
+    if constexpr (SLICED) {
+        if (tid < nsl) {
+            s_slm[tid] = slm;
+            s_slnc[tid] = sncv;
+            s_slu[tid] = slu;
+        }
+        if (tid < (nsl - 1) * 11) s_slq[1 + tid / 11][tid % 11] = slq;
+    }
     double cpm = -1.0;
     int64_t cblk = -1;
 #pragma unroll
@@ -862,6 +1053,17 @@ __global__ __launch_bounds__(kFinThreads) void finalize_small_kernel(
             s_crec[slot] = cr;
         }
     }
+    // SLICED: the listed candidates of the slices, records staged the same way
+    const bool slc = SLICED && ccb >= 0 && ccp >= M * (1.0 - 0x1p-48);
+    if (slc) {
+        FinRecord f;
+        fin_load_record(dp, ccb, f);
+        const int slot = atomicAdd(&s_ncand, 1);
+        if (slot < kFinCand) {
+            s_cblk[slot] = ccb;
+            s_crec[slot] = f;
+        }
+    }
     if (nch > nfull) {
         __syncthreads();                                 // sh reused by the tail
         const double tsum = tail_chunk_sum(w_un + nfull * kSumChunk, tail_leaves, tail_ops,
@@ -888,6 +1090,20 @@ __global__ __launch_bounds__(kFinThreads) void finalize_small_kernel(
             }
             if (lane == 0) s_tot[j] = r;
         }
+        if constexpr (SLICED) {                         // + the slices, rescaled to M, in order
+            __syncthreads();
+            if (tid < 11) {
+                double r = s_tot[tid];
+                for (int g = 1; g < nsl; ++g) {
+                    const double mg = s_slm[g];
+                    if (mg > 0.0) {
+                        const double f = mg / M;
+                        r = r + s_slq[g][tid] * (tid == 1 ? f * f : f);
+                    }
+                }
+                s_tot[tid] = r;
+            }
+        }
         // ---- argmax: the first block whose max rounds to fl(M / s)
         const double mval = M / s;
         unsigned long long cb = ~0ull;
@@ -895,6 +1111,25 @@ __global__ __launch_bounds__(kFinThreads) void finalize_small_kernel(
         for (int k = kFinRegBlocks - 1; k >= 0; --k)
             if (has[k] && pm[k] >= M * (1.0 - 0x1p-48) && pm[k] / s == mval)
                 cb = (unsigned long long)fin_blk(tid, k);
+        if constexpr (SLICED) {
+            if (slc && ccp / s == mval) cb = min(cb, (unsigned long long)ccb);
+            // a slice with more candidates than it listed: all of its blocks
+            for (int g = 1; g < nsl; ++g) {
+                if (s_slnc[g] > kSliceCand && s_slm[g] >= M * (1.0 - 0x1p-48)) {
+                    double v[kFinRegBlocks];
+#pragma unroll
+                    for (int k = 0; k < kFinRegBlocks; ++k) {
+                        const int64_t b = (int64_t)g * kFinThreads * kFinRegBlocks + fin_blk(tid, k);
+                        v[k] = b < nb ? dp.pmax[b] : -1.0;
+                    }
+#pragma unroll
+                    for (int k = kFinRegBlocks - 1; k >= 0; --k) {
+                        const int64_t b = (int64_t)g * kFinThreads * kFinRegBlocks + fin_blk(tid, k);
+                        if (b < nb && v[k] / s == mval) cb = min(cb, (unsigned long long)b);
+                    }
+                }
+            }
+        }
         if (cb != ~0ull) atomicMin(&s_min, cb);
         __syncthreads();
         const int64_t bc = (int64_t)s_min;
@@ -991,7 +1226,80 @@ __global__ __launch_bounds__(kFinThreads) void finalize_small_kernel(
         double q0[kFinRegBlocks];
 #pragma unroll
         for (int k = 0; k < kFinRegBlocks; ++k) q0[k] = q[k][0];
-        fin_next_prefix(n, nb, ok, s, np_recip, pm, q0, has, w_un, dp, boff, sh, &s_q[0][0]);
+        if (SLICED && ok) {
+            // the slices' own prefixes (finalize_slices_kernel), w_un units:
+            // slice 0 from the registers the same way, then every block's
+            // (U_0 + ... + U_{g-1} + pre_b) / s
+            double u0[2], u1[2], pex[2], tot[2];
+#pragma unroll
+            for (int hf = 0; hf < 2; ++hf) {
+                u0[hf] = has[2 * hf] ? pm[2 * hf] * q0[2 * hf] : 0.0;
+                u1[hf] = has[2 * hf + 1] ? pm[2 * hf + 1] * q0[2 * hf + 1] : 0.0;
+                const double pr = u0[hf] + u1[hf];
+                const double inc = wave_incl_scan_rows(pr);
+                pex[hf] = inc - pr;
+                if (lane == 63) s_q[hf][wave] = inc;
+            }
+            // slices g >= 1: block 2048 + tid + 512 i (slice 1 + i / 4, coalesced),
+            // the first batch of 32 requested before the barrier
+            const int nrest = (nsl - 1) * kFinRegBlocks;
+            constexpr int kB = 32;
+            auto pre_batch = [&](const int i0, double (&pv)[kB]) {
+#pragma unroll
+                for (int i = 0; i < kB; ++i) {
+                    const int64_t b = (int64_t)kFinThreads * kFinRegBlocks + tid + (int64_t)kFinThreads * (i0 + i);
+                    pv[i] = (i0 + i < nrest && b < nb) ? sl.pre[b] : 0.0;
+                }
+            };
+            double pv[kB];
+            pre_batch(0, pv);
+            __syncthreads();
+#pragma unroll
+            for (int hf = 0; hf < 2; ++hf) {
+                double base = 0.0, all = 0.0;
+#pragma unroll
+                for (int w = 0; w < kFinWaves; ++w) {
+                    if (w < wave) base = base + s_q[hf][w];
+                    all = all + s_q[hf][w];
+                }
+                pex[hf] = base + pex[hf];
+                tot[hf] = all;
+            }
+            pex[1] = tot[0] + pex[1];
+            const double rs = 1.0 / s;
+#pragma unroll
+            for (int hf = 0; hf < 2; ++hf) {
+                const int64_t b = fin_blk(tid, 2 * hf);
+                if (b + 1 < nb)
+                    *reinterpret_cast<double2*>(boff + b) = double2{pex[hf] * rs, (pex[hf] + u0[hf]) * rs};
+                else if (b < nb)
+                    boff[b] = pex[hf] * rs;
+            }
+            // U_0 + ... + U_{g-1} for every slice (every lane, in slice order)
+            double ubs[kFinFastSlices];
+            ubs[0] = 0.0;
+            ubs[1] = tot[0] + tot[1];
+#pragma unroll
+            for (int g = 2; g < kFinFastSlices; ++g) ubs[g] = (g - 1 < nsl) ? ubs[g - 1] + s_slu[g - 1] : ubs[g - 1];
+            double utot = ubs[1];
+#pragma unroll
+            for (int g = 1; g < kFinFastSlices; ++g)
+                if (g < nsl) utot = utot + s_slu[g];
+#pragma unroll
+            for (int i0 = 0; i0 < (kFinFastSlices - 1) * kFinRegBlocks; i0 += kB) {
+                if (i0 < nrest) {
+                    if (i0 > 0) pre_batch(i0, pv);
+#pragma unroll
+                    for (int i = 0; i < kB; ++i) {
+                        const int64_t b = (int64_t)kFinThreads * kFinRegBlocks + tid + (int64_t)kFinThreads * (i0 + i);
+                        if (i0 + i < nrest && b < nb) boff[b] = (ubs[1 + (i0 + i) / kFinRegBlocks] + pv[i]) * rs;
+                    }
+                }
+            }
+            if (tid == 0) boff[nb] = utot * rs;
+        } else {
+            fin_next_prefix(n, nb, ok, s, np_recip, pm, q0, has, w_un, dp, boff, sh, &s_q[0][0]);
+        }
     }
     FIN_STAMP(5);
 }

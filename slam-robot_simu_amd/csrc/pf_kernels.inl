@@ -93,6 +93,30 @@ __device__ __forceinline__ T wave_incl_scan(T v) {
     }
 }
 
+// Inclusive wave scan of doubles in the integer scan's order (DPP row shifts,
+// then the lower rows' totals): a fixed order ~6x shorter in latency than the
+// shuffle form; for sums any fixed order serves (the approximate block prefix
+// of the exact cumsum).
+__device__ __forceinline__ double wave_incl_scan_rows(double v) {
+    auto sh = [](double x, auto d) {
+        return __longlong_as_double((long long)dpp_row_shr0<decltype(d)::value>(
+            (uint64_t)__double_as_longlong(x)));
+    };
+    v = v + sh(v, std::integral_constant<int, 1>{});
+    v = v + sh(v, std::integral_constant<int, 2>{});
+    v = v + sh(v, std::integral_constant<int, 4>{});
+    v = v + sh(v, std::integral_constant<int, 8>{});
+    const uint64_t b = (uint64_t)__double_as_longlong(v);
+    const double r0 = __longlong_as_double((long long)readlane_int(b, 15));
+    const double r1 = __longlong_as_double((long long)readlane_int(b, 31));
+    const double r2 = __longlong_as_double((long long)readlane_int(b, 47));
+    const int row = (int)((threadIdx.x & 63) >> 4);
+    if (row >= 1) v = v + r0;
+    if (row >= 2) v = v + r1;
+    if (row >= 3) v = v + r2;
+    return v;
+}
+
 // Exclusive block scan over NT threads; sh needs NT/64+1 entries.  Returns the
 // exclusive prefix of v, writes the block total to `total`.
 template <typename T, int NT>
