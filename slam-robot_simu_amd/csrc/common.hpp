@@ -59,8 +59,10 @@ struct u32x4 {
 __device__ __forceinline__ u32x4 philox4x32(u32x4 c, uint32_t k0, uint32_t k1) {
 #pragma unroll
     for (int r = 0; r < 10; ++r) {
-        const uint32_t lo0 = 0xD2511F53u * c.x, hi0 = __umulhi(0xD2511F53u, c.x);
-        const uint32_t lo1 = 0xCD9E8D57u * c.z, hi1 = __umulhi(0xCD9E8D57u, c.z);
+        // one 32 x 32 -> 64 product per word (v_mad_u64_u32) for both halves
+        const uint64_t p0 = (uint64_t)0xD2511F53u * c.x, p1 = (uint64_t)0xCD9E8D57u * c.z;
+        const uint32_t lo0 = (uint32_t)p0, hi0 = (uint32_t)(p0 >> 32);
+        const uint32_t lo1 = (uint32_t)p1, hi1 = (uint32_t)(p1 >> 32);
         c = u32x4{hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0};
         k0 += 0x9E3779B9u;
         k1 += 0xBB67AE85u;
@@ -78,7 +80,8 @@ __device__ __forceinline__ double u01_open0(uint32_t a, uint32_t b) {
 __device__ __forceinline__ void philox2x32(uint32_t& c0, uint32_t& c1, uint32_t k) {
 #pragma unroll
     for (int r = 0; r < 10; ++r) {
-        const uint32_t lo = 0xD256D193u * c0, hi = __umulhi(0xD256D193u, c0);
+        const uint64_t p = (uint64_t)0xD256D193u * c0;
+        const uint32_t lo = (uint32_t)p, hi = (uint32_t)(p >> 32);
         c0 = hi ^ k ^ c1;
         c1 = lo;
         k += 0x9E3779B9u;
