@@ -2347,8 +2347,10 @@ __device__ __forceinline__ void wave_tile_classify(const double* __restrict__ w_
     double loc = 0.0;
 #pragma unroll
     for (int k = 0; k < kScanPer; ++k) loc += ts.v[k];
-    double dtot;
-    double run = wave_excl_scan(loc, dtot) + off;
+    // the approximate prefix (any fixed order: the classification's margins
+    // cover its error, and pass C recomputes it with this same code)
+    const double inc = wave_incl_scan_rows(loc);
+    double run = (inc - loc) + off;
     uint64_t ksum = 0;
     int32_t fsum = 0;
 #pragma unroll
