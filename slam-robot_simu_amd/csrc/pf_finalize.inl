@@ -231,10 +231,9 @@ __global__ __launch_bounds__(kFinThreads) void finalize_slices_kernel(const int6
     for (int hf = 0; hf < 2; ++hf) {
         u0[hf] = has[2 * hf] ? pm[2 * hf] * q[2 * hf][0] : 0.0;
         u1[hf] = has[2 * hf + 1] ? pm[2 * hf + 1] * q[2 * hf + 1][0] : 0.0;
-        const double pr = u0[hf] + u1[hf];
-        const double inc = wave_incl_scan_rows(pr);
-        pex[hf] = inc - pr;
-        if (lane == 63) s_pw[hf][wave] = inc;
+        double wt;
+        pex[hf] = wave_excl_scan_rows(u0[hf] + u1[hf], wt);
+        if (lane == 63) s_pw[hf][wave] = wt;
     }
     __syncthreads();
     {
@@ -307,12 +306,11 @@ __device__ void fin_next_prefix(const int64_t n, const int64_t nb, const bool ok
             t1[hf] = has[2 * hf + 1] ? (pm[2 * hf + 1] / s) * q0[2 * hf + 1] : 0.0;
             p[hf] = t0[hf] + t1[hf];
         }
-        double inc[2], ex[2];
+        double wt[2], ex[2];
 #pragma unroll
         for (int hf = 0; hf < 2; ++hf) {
-            inc[hf] = wave_incl_scan_rows(p[hf]);
-            ex[hf] = inc[hf] - p[hf];
-            if (lane == 63) scr[hf * kFinWaves + wave] = inc[hf];
+            ex[hf] = wave_excl_scan_rows(p[hf], wt[hf]);
+            if (lane == 63) scr[hf * kFinWaves + wave] = wt[hf];
         }
         __syncthreads();
 #pragma unroll
@@ -363,10 +361,7 @@ __device__ void fin_next_prefix(const int64_t n, const int64_t nb, const bool ok
             if (r < R) {
                 const int64_t b = wb0 + 64 * r + lane;
                 const double t = b < nb ? (pv[r] / s) * qv[r] : 0.0;
-                const double inc = wave_incl_scan_rows(t);
-                ex[r] = inc - t;
-                rt[r] = __longlong_as_double(
-                    (long long)readlane_int((uint64_t)__double_as_longlong(inc), 63));
+                ex[r] = wave_excl_scan_rows(t, rt[r]);
             }
         }
         double run = 0.0;
@@ -1235,10 +1230,9 @@ __global__ __launch_bounds__(kFinThreads) void finalize_fast_kernel(
             for (int hf = 0; hf < 2; ++hf) {
                 u0[hf] = has[2 * hf] ? pm[2 * hf] * q0[2 * hf] : 0.0;
                 u1[hf] = has[2 * hf + 1] ? pm[2 * hf + 1] * q0[2 * hf + 1] : 0.0;
-                const double pr = u0[hf] + u1[hf];
-                const double inc = wave_incl_scan_rows(pr);
-                pex[hf] = inc - pr;
-                if (lane == 63) s_q[hf][wave] = inc;
+                double wt;
+                pex[hf] = wave_excl_scan_rows(u0[hf] + u1[hf], wt);
+                if (lane == 63) s_q[hf][wave] = wt;
             }
             // slices g >= 1: block 2048 + tid + 512 i (slice 1 + i / 4, coalesced),
             // the first batch of 32 requested before the barrier

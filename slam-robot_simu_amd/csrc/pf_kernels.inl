@@ -93,11 +93,13 @@ __device__ __forceinline__ T wave_incl_scan(T v) {
     }
 }
 
-// Inclusive wave scan of doubles in the integer scan's order (DPP row shifts,
-// then the lower rows' totals): a fixed order ~6x shorter in latency than the
-// shuffle form; for sums any fixed order serves (the approximate block prefix
-// of the exact cumsum).
-__device__ __forceinline__ double wave_incl_scan_rows(double v) {
+// Exclusive wave scan of non-negative doubles in the integer scan's order (DPP
+// row shifts, then the lower rows' totals: ~6x shorter in latency than the
+// shuffle form; any fixed order serves an approximate prefix), formed
+// without a subtraction (inc - v loses a small prefix ahead of a large
+// element: its relative error is unbounded, which the exact cumsum's margins
+// do not cover); `total` = the wave's sum (every lane).
+__device__ __forceinline__ double wave_excl_scan_rows(double v, double& total) {
     auto sh = [](double x, auto d) {
         return __longlong_as_double((long long)dpp_row_shr0<decltype(d)::value>(
             (uint64_t)__double_as_longlong(x)));
@@ -110,11 +112,15 @@ __device__ __forceinline__ double wave_incl_scan_rows(double v) {
     const double r0 = __longlong_as_double((long long)readlane_int(b, 15));
     const double r1 = __longlong_as_double((long long)readlane_int(b, 31));
     const double r2 = __longlong_as_double((long long)readlane_int(b, 47));
+    const double r3 = __longlong_as_double((long long)readlane_int(b, 63));
     const int row = (int)((threadIdx.x & 63) >> 4);
-    if (row >= 1) v = v + r0;
-    if (row >= 2) v = v + r1;
-    if (row >= 3) v = v + r2;
-    return v;
+    double below = 0.0;
+    if (row >= 1) below = r0;
+    if (row >= 2) below = below + r1;
+    if (row >= 3) below = below + r2;
+    total = ((r0 + r1) + r2) + r3;
+    const double prev = sh(v, std::integral_constant<int, 1>{});   // the row's inclusive, one lane down
+    return (threadIdx.x & 15) ? below + prev : below;
 }
 
 // Exclusive block scan over NT threads; sh needs NT/64+1 entries.  Returns the
@@ -2349,8 +2355,8 @@ __device__ __forceinline__ void wave_tile_classify(const double* __restrict__ w_
     for (int k = 0; k < kScanPer; ++k) loc += ts.v[k];
     // the approximate prefix (any fixed order: the classification's margins
     // cover its error, and pass C recomputes it with this same code)
-    const double inc = wave_incl_scan_rows(loc);
-    double run = (inc - loc) + off;
+    double wtot;
+    double run = wave_excl_scan_rows(loc, wtot) + off;
     uint64_t ksum = 0;
     int32_t fsum = 0;
 #pragma unroll
