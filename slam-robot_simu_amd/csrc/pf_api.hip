@@ -6,6 +6,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cmath>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <limits>
@@ -690,13 +691,20 @@ int sync_results(slam_pf* h, int32_t first, int32_t count, slam_pf_result* out, 
     int rc = SLAM_OK;
     for (int i = 0; i < count; ++i) {
         if (out) out[i] = r[i];
-        if (r[i].status & 8)
-            rc = fail(SLAM_ERR_HIP, "exact-cumsum launch: release token timed out");
-        if (r[i].status & 256)
-            rc = fail(SLAM_ERR_HIP, "mt19937 draw: candidate bound exhausted");
-        if (r[i].status & 1)
-            rc = fail(SLAM_ERR_INDEX, "resample position beyond the last cumulative weight "
-                                      "(IndexError in particle_filter.py:219); clamped to NP-1");
+        // every condition named in one message (status word and step), the
+        // IndexError taking precedence as the reference's own error
+        const int32_t st = r[i].status;
+        if (st & (1 | 8 | 256)) {
+            std::string msg;
+            if (st & 1) msg += "resample position beyond the last cumulative weight "
+                               "(IndexError in particle_filter.py:219); clamped to NP-1; ";
+            if (st & 8) msg += "exact-cumsum launch: release token timed out; ";
+            if (st & 256) msg += "mt19937 draw: candidate bound exhausted; ";
+            char tail[96];
+            std::snprintf(tail, sizeof tail, "record %d of the batch, status 0x%x, n_special %d", (int)(first + i),
+                          (unsigned)st, (int)r[i].n_special);
+            rc = fail((st & 1) ? SLAM_ERR_INDEX : SLAM_ERR_HIP, msg + tail);
+        }
     }
     h->resample_next = r[count - 1].resample_next;
     return rc;
