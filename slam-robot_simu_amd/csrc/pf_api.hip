@@ -1093,6 +1093,24 @@ int slam_pf_step(slam_pf* h, const double* control, const double* z, const doubl
     return sync_results(h, 0, 1, res);
 }
 
+// Stand-alone exact cumsum (slam_pf_resample, slam_pf_resample_indices): its
+// expand pass writes run marks with the offset of StepIO slot ctr[0], so the
+// caller's offset goes into slot 0 and ctr[0] back to 0 first -- the previous
+// step end had advanced ctr[0] past the staged slot (an out-of-bounds or stale
+// offset: round 6, test_gpu_zz_order) -- and afterwards the mark generation
+// moves on, so that these marks (not meant for a gather) never win the next
+// step's running max.
+static int stage_scan_offset(slam_pf* h, double u) {
+    h->ofs_host = std::isnan(u) ? u : u * h->pc.np_recip;           // particle_filter.py:214
+    SLAM_HIP_TRY(hipMemcpyAsync(h->ofs, &h->ofs_host, sizeof(double), hipMemcpyHostToDevice, h->stream));
+    return set_ctr(h, 0);
+}
+static int retire_scan_marks(slam_pf* h) {
+    mark_gen_bump_kernel<<<1, 1, 0, h->stream>>>(h->flags);
+    SLAM_HIP_TRY(hipGetLastError());
+    return SLAM_OK;
+}
+
 int slam_pf_resample(slam_pf* h, double u_resample, int32_t force, int32_t* resampled) {
     SLAM_ARG_CHECK(h, "slam_pf_resample: NULL handle");
     h->prep_step = -1;
@@ -1101,8 +1119,8 @@ int slam_pf_resample(slam_pf* h, double u_resample, int32_t force, int32_t* resa
     const int32_t go = force ? 1 : h->resample_next;
     if (resampled) *resampled = go;
     if (!go) return SLAM_OK;
-    int rc = launch_scans(h, 1, true);
-    if (rc) return rc;
+    int rc = stage_scan_offset(h, u_resample);
+    if (rc || (rc = launch_scans(h, 1, true)) || (rc = retire_scan_marks(h))) return rc;
     const double ofs = std::isnan(u_resample) ? u_resample : u_resample * h->pc.np_recip;
     resample_search_kernel<<<grid_for(h->n, 256), 256, 0, h->stream>>>(
         h->n, h->c, h->idx, h->pc.rstep, ofs, h->pc.np_recip, h->cfg.seed, h->stepno, h->flags);
@@ -1130,8 +1148,8 @@ int slam_pf_resample_indices(slam_pf* h, double u_resample, int64_t* idx_out, in
     h->prep_step = -1;
     SLAM_ARG_CHECK(h->n == h->n_global, "slam_pf_resample_indices: sharded handle");
     SLAM_HIP_TRY(hipSetDevice(h->device));
-    int rc = launch_scans(h, 1, true);
-    if (rc) return rc;
+    int rc = stage_scan_offset(h, u_resample);
+    if (rc || (rc = launch_scans(h, 1, true)) || (rc = retire_scan_marks(h))) return rc;
     const double ofs = std::isnan(u_resample) ? u_resample : u_resample * h->pc.np_recip;
     resample_search_kernel<<<grid_for(h->n, 256), 256, 0, h->stream>>>(
         h->n, h->c, h->idx, h->pc.rstep, ofs, h->pc.np_recip, h->cfg.seed, h->stepno, h->flags);

@@ -2691,6 +2691,11 @@ __device__ __forceinline__ void lean_last_block(uint64_t* __restrict__ bk, int32
     PROBE_AT(4);
 }
 
+// A stand-alone exact cumsum's run marks retired (pf_api.hip retire_scan_marks)
+__global__ void mark_gen_bump_kernel(int32_t* __restrict__ flags) {
+    flags[kFlagMarkGen] = flags[kFlagMarkGen] + 1;
+}
+
 // Pass A (two-launch form): classify and stage every tile; the last block
 // scans the tile totals, places and folds.
 __global__ __launch_bounds__(kScanThreads) void scan_lean_classify_kernel(

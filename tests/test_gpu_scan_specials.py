@@ -49,3 +49,49 @@ def test_resample_steps_classify_without_fallback(mode):
     assert not fell_back, f"exact-scan fallback at steps {fell_back[:10]}"
     worst = max(r["n_special"] for r in res)
     assert worst < 4096, worst
+
+
+def test_resample_indices_leaves_the_next_gather_alone():
+    """slam_pf_resample_indices runs the exact cumsum's expand pass too, which
+    writes run marks; they must not reach the next step's gather.  Round 6
+    (test_gpu_zz_order's IndexError, and most likely round 3's C2 miss): the
+    stand-alone scan read its offset from StepIO slot ctr[0], which the
+    previous step end had advanced past the staged slot 0 -- out of bounds on a
+    handle without loaded observations, a NaN (the device offset) here -- and
+    its marks carried the current generation, so an earlier run start from a
+    larger offset won the gather's running max.  Two handles take the same
+    steps (offset 0 on resampling steps); one also asks for the indices first:
+    every record and the final state must be identical."""
+    import bench
+    from slamhip import pf as dpf
+    n = 1 << 16
+    lm, zs, (vel, omega, dt) = bench.simulate_world(40)
+    ctl = np.tile([vel, omega], (40, 1))
+    rs = np.random.RandomState(7)
+    hs = [dpf.DeviceParticleFilter(n, lm, dt=dt, motion="velocity", likelihood="logsum", seed=9)
+          for _ in range(2)]
+    try:
+        for h in hs:
+            h.load_observations(zs)                    # every offset slot NaN
+            h.run(0, ctl[:2])
+        resampled = 0
+        for k in range(2, 16):
+            g = rs.standard_normal((n, 3))
+            recs = []
+            for i, h in enumerate(hs):
+                u = 0.0 if h.resample_next else float("nan")
+                if i == 1 and h.resample_next:
+                    h.resample_indices(u)
+                recs.append(h.step(ctl[k], zs[k], g, u))
+            a, b = recs
+            resampled += int(a["resampled"])
+            for f in ("resampled", "max_idx", "max_val", "weight_sum", "status"):
+                assert a[f] == b[f], (k, f, a[f], b[f])
+            np.testing.assert_array_equal(a["x_est"], b["x_est"], err_msg=f"step {k}")
+        assert resampled >= 3, resampled
+        sa, sb = hs[0].get_state(), hs[1].get_state()
+        for u, v in zip(sa, sb):
+            np.testing.assert_array_equal(u, v)
+    finally:
+        for h in hs:
+            h.close()
