@@ -308,3 +308,30 @@ def test_resample_decision_by_host_dot_near_threshold(slamhip_pf):
                      np.random.multivariate_normal([0.0, 0.0, 0.0], p.q, n),
                      np.random.rand() if dec else np.nan)
         assert out["resampled"] == dec
+
+
+@pytest.mark.parametrize("n", [1 << 20, (1 << 21) + 12345, (1 << 24) + 12345])
+def test_step_end_against_numpy_on_the_devices_weights(slamhip_pf, n):
+    """The device-resident step end (particle_filter.py:115-117, :210, :234) on
+    the device's own w_un: np.sum, max, the first argmax and ESS exact or to
+    1e-12, the covariance to 1e-8 against np.cov of the device's state.  One
+    size per finalize form: 2^20 the one-workgroup fast kernel, 2^21 + 12,345
+    the fast kernel after the slice pre-pass, 2^24 + 12,345 (17 slices, 2,049
+    buffers) the general finalize_deferred_kernel."""
+    import bench
+    lm, zs, (vel, omega, dt) = bench.simulate_world(8)
+    ctl = np.tile([vel, omega], (8, 1))
+    with slamhip_pf.DeviceParticleFilter(n, lm, dt=dt, motion="velocity", likelihood="logsum",
+                                         seed=3) as d:
+        d.load_observations(zs)
+        recs = d.run(0, ctl[:3])
+        w_un, s = d.get_weights_raw()
+        x, y, th, w = d.get_state()
+    r = recs[len(recs) - 1]
+    assert s == np.sum(w_un) and r["weight_sum"] == s
+    np.testing.assert_array_equal(w, w_un / s)
+    assert r["max_val"] == w.max() and r["max_idx"] == int(np.argmax(w))
+    np.testing.assert_array_equal(r["x_est"], [x[r["max_idx"]], y[r["max_idx"]], th[r["max_idx"]]])
+    np.testing.assert_allclose(r["ess"], 1.0 / np.dot(w, w), rtol=1e-12)
+    np.testing.assert_allclose(r["cov"], po.weighted_cov(x, y, th, w), rtol=1e-8, atol=1e-14)
+    assert r["status"] == 0
