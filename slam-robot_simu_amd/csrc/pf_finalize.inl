@@ -1073,16 +1073,13 @@ __global__ __launch_bounds__(kFinThreads) void finalize_fast_kernel(
     BlockPartial tot;
     bp_zero(tot);
     if (ok) {
-        // ---- the 11 sums: wave w reduces quantities w and w + 8
+        // ---- the 11 sums: wave w reduces quantities w and w + 8 (lane-strided
+        // reads, then the wave's rows by DPP: a fixed order, no LDS permutes)
         for (int j = wave; j < 11; j += kFinWaves) {
             double r = s_q[j][lane];
 #pragma unroll
             for (int m = 1; m < kFinThreads / 64; ++m) r = r + s_q[j][lane + 64 * m];
-#pragma unroll
-            for (int d = 1; d < 64; d <<= 1) {
-                const double o = xor_f64(r, d);
-                r = (lane & d) ? (o + r) : (r + o);
-            }
+            r = wave_sum_rows(r);
             if (lane == 0) s_tot[j] = r;
         }
         if constexpr (SLICED) {                         // + the slices, rescaled to M, in order

@@ -123,6 +123,14 @@ __device__ __forceinline__ double wave_excl_scan_rows(double v, double& total) {
     return (threadIdx.x & 15) ? below + prev : below;
 }
 
+// Sum over the wave in the same row order (every lane gets it): the rows'
+// inclusive DPP scans, then ((row0 + row1) + row2) + row3.
+__device__ __forceinline__ double wave_sum_rows(double v) {
+    double total;
+    (void)wave_excl_scan_rows(v, total);
+    return total;
+}
+
 // Exclusive block scan over NT threads; sh needs NT/64+1 entries.  Returns the
 // exclusive prefix of v, writes the block total to `total`.
 template <typename T, int NT>
