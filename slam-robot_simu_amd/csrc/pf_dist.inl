@@ -917,7 +917,7 @@ __global__ __launch_bounds__(kScanThreads) void dist_resample_merged_kernel(
         wave_tile_classify(w_un, *s_in, np_recip, n, tile, boff[tile] + scr->base_off, delta, tsc,
                            ktile, ftile);
     block_tile_offsets(ktile, ftile, kofs, fofs, kblk, fblk);
-    if (active) wave_tile_stage(tile, tsc, kofs, fofs, kblk, fblk, stage, bk, bf);
+    if (active) wave_tile_stage(blockIdx.x, tile, tsc, kofs, fofs, kblk, fblk, stage, bk, bf);
     else if (threadIdx.x == 0) {
         st_wt(&bk[blockIdx.x], kblk);
         st_wt_i(&bf[blockIdx.x], fblk);

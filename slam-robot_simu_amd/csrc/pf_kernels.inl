@@ -11,11 +11,13 @@
 #include "pf_kernels.hpp"
 
 // Phase stamps of the resample passes (probe builds only: -DSLAM_PROBE,
-// read back with slam_probe_read; never in the product library).
+// read back with slam_probe_read; never in the product library).  PROBE_MAX
+// samples every 32nd block: one atomic word taking every block's stamp
+// serialises them (~12 ns each) and would time itself.
 #ifdef SLAM_PROBE
 __device__ unsigned long long g_probe[32];
 #define PROBE_AT(k) do { if (threadIdx.x == 0) g_probe[k] = wall_clock64(); } while (0)
-#define PROBE_MAX(k) do { if (threadIdx.x == 0) atomicMax(&g_probe[k], (unsigned long long)wall_clock64()); } while (0)
+#define PROBE_MAX(k) do { if (threadIdx.x == 0 && (blockIdx.x & 31) == 0) atomicMax(&g_probe[k], (unsigned long long)wall_clock64()); } while (0)
 #else
 #define PROBE_AT(k) do { } while (0)
 #define PROBE_MAX(k) do { } while (0)
@@ -1642,52 +1644,101 @@ __device__ void block_scan_array(const T* in, T* out, const int nb, T* total, T*
 // The two tile-total scans of the exact cumsum (increments k: u64, special
 // counts f: i32) with both arrays' loads issued together (one memory round
 // trip for both); the same sums as two block_scan_array calls.
-template <int NT>
-__device__ void block_scan_pair(const uint64_t* kin, uint64_t* kout, uint64_t* ktotal,
+template <int NT, int kC = 8>
+__device__ __forceinline__ void block_scan_pair(const uint64_t* kin, uint64_t* kout, uint64_t* ktotal,
                                 const int32_t* fin, int32_t* fout, int32_t* ftotal, const int nb,
                                 uint64_t* shk, int32_t* shf, int32_t* f_lds = nullptr) {
-    constexpr int kMaxPer = 8;
-    const int per = (nb + NT - 1) / NT;
-    if (per > kMaxPer) {
-        block_scan_array<uint64_t, NT>(kin, kout, nb, ktotal, shk, true);
-        __syncthreads();
-        block_scan_array<int32_t, NT>(fin, fout, nb, ftotal, shf, true);
-        if (f_lds) {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __syncthreads();
-            for (int k = threadIdx.x; k < nb; k += NT) f_lds[k] = ld_wt_i(&fout[k]);
+    // Up to two entries per thread: thread-contiguous, in registers, one
+    // block scan per array.  Beyond, coalesced: wave w owns the contiguous
+    // span [w*span, (w+1)*span) and walks it in rounds of 64 consecutive
+    // entries (one per lane), kC rounds' loads in flight; each round is a DPP
+    // wave scan.  (The thread-contiguous layout touches one cache line per
+    // lane per access: 17-27 us for the 4,096 tile totals of NP = 2^23 in one
+    // CU, against 7 us here.)
+    constexpr int W = NT / 64;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    if (nb <= 2 * NT) {
+        const int b0 = 2 * threadIdx.x;
+        uint64_t k2[2];
+        int32_t f2[2];
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const bool ok = b0 + k < nb;
+            k2[k] = ok ? ld_wt(kin + b0 + k) : 0;
+            f2[k] = ok ? ld_wt_i(fin + b0 + k) : 0;
+        }
+        uint64_t ktot;
+        int32_t ftot;
+        uint64_t kex = block_excl_scan<uint64_t, NT>(k2[0] + k2[1], shk, ktot);
+        int32_t fex = block_excl_scan<int32_t, NT>(f2[0] + f2[1], shf, ftot);
+#pragma unroll
+        for (int k = 0; k < 2; ++k)
+            if (b0 + k < nb) {
+                st_wt(kout + b0 + k, kex);
+                st_wt_i(fout + b0 + k, fex);
+                if (f_lds) f_lds[b0 + k] = fex;
+                kex = kex + k2[k];
+                fex = fex + f2[k];
+            }
+        if (threadIdx.x == 0) {
+            st_wt(ktotal, ktot);
+            st_wt_i(ftotal, ftot);
         }
         return;
     }
-    const int b0 = threadIdx.x * per;
-    uint64_t kv[kMaxPer];
-    int32_t fv[kMaxPer];
-#pragma unroll
-    for (int k = 0; k < kMaxPer; ++k) {
-        const bool ok = k < per && b0 + k < nb;
-        kv[k] = ok ? ld_wt(kin + b0 + k) : 0;
-        fv[k] = ok ? ld_wt_i(fin + b0 + k) : 0;
-    }
+    const int span = ((nb + W * 64 - 1) / (W * 64)) * 64;
+    const int R = span / 64;
+    const int e0 = wid * span + lane;
+    uint64_t kv[kC];
+    int32_t fv[kC];
     uint64_t kloc = 0;
     int32_t floc = 0;
+    for (int r0 = 0; r0 < R; r0 += kC) {
 #pragma unroll
-    for (int k = 0; k < kMaxPer; ++k) {
-        kloc = kloc + kv[k];
-        floc = floc + fv[k];
+        for (int r = 0; r < kC; ++r) {
+            const int e = e0 + (r0 + r) * 64;
+            const bool ok = r0 + r < R && e < nb;
+            kv[r] = ok ? ld_wt(kin + e) : 0;
+            fv[r] = ok ? ld_wt_i(fin + e) : 0;
+        }
+#pragma unroll
+        for (int r = 0; r < kC; ++r) {
+            kloc = kloc + kv[r];
+            floc = floc + fv[r];
+        }
     }
     uint64_t ktot;
     int32_t ftot;
-    uint64_t kex = block_excl_scan<uint64_t, NT>(kloc, shk, ktot);
-    int32_t fex = block_excl_scan<int32_t, NT>(floc, shf, ftot);
+    // lane 0's exclusive prefix over the block = the sum of the lower waves
+    uint64_t krun = readlane_int(block_excl_scan<uint64_t, NT>(kloc, shk, ktot), 0);
+    int32_t frun = readlane_int(block_excl_scan<int32_t, NT>(floc, shf, ftot), 0);
+    for (int r0 = 0; r0 < R; r0 += kC) {
+        if (R > kC) {                              // (one chunk: still in registers)
 #pragma unroll
-    for (int k = 0; k < kMaxPer; ++k)
-        if (k < per && b0 + k < nb) {
-            st_wt(kout + b0 + k, kex);
-            st_wt_i(fout + b0 + k, fex);
-            if (f_lds) f_lds[b0 + k] = fex;
-            kex = kex + kv[k];
-            fex = fex + fv[k];
+            for (int r = 0; r < kC; ++r) {
+                const int e = e0 + (r0 + r) * 64;
+                const bool ok = r0 + r < R && e < nb;
+                kv[r] = ok ? ld_wt(kin + e) : 0;
+                fv[r] = ok ? ld_wt_i(fin + e) : 0;
+            }
         }
+#pragma unroll
+        for (int r = 0; r < kC; ++r) {
+            if (r0 + r < R) {                      // (wave-uniform)
+                const uint64_t ki = wave_incl_scan(kv[r]);
+                const int32_t fi = wave_incl_scan(fv[r]);
+                const int e = e0 + (r0 + r) * 64;
+                if (e < nb) {
+                    const int32_t fex = frun + (fi - fv[r]);
+                    st_wt(kout + e, krun + (ki - kv[r]));
+                    st_wt_i(fout + e, fex);
+                    if (f_lds) f_lds[e] = fex;
+                }
+                krun += readlane_int(ki, 63);
+                frun += readlane_int(fi, 63);
+            }
+        }
+    }
     if (threadIdx.x == 0) {
         st_wt(ktotal, ktot);
         st_wt_i(ftotal, ftot);
@@ -2427,14 +2478,14 @@ __device__ __forceinline__ void block_tile_offsets(const uint64_t ktile, const i
 
 // Stage a classified tile's specials in its block's area (block-local P,
 // write-through); thread 0 publishes the block totals.
-__device__ __forceinline__ void wave_tile_stage(const int64_t tile, const TileScan& ts,
+__device__ __forceinline__ void wave_tile_stage(const int64_t b, const int64_t tile,
+                                                const TileScan& ts,
                                                 const uint64_t kofs, const int32_t fofs,
                                                 const uint64_t kblk, const int32_t fblk,
                                                 SpecialIn* __restrict__ stage,
                                                 uint64_t* __restrict__ bk,
                                                 int32_t* __restrict__ bf) {
     const int lane = threadIdx.x & 63;
-    const int64_t b = blockIdx.x;
     uint64_t kex = kofs + ts.kex;
     int32_t fex = fofs + ts.fex;
 #pragma unroll
@@ -2468,7 +2519,7 @@ __device__ __forceinline__ void wave_tile_stage(const int64_t tile, const TileSc
 // Bit-identical to serial_fold; a failed run check takes the same fallback
 // (the plain sequential recurrence, flagged).
 constexpr int kFoldTilesLds = 4096;
-__device__ void lean_place_fold(const SpecialIn* __restrict__ stage,
+__device__ __forceinline__ void lean_place_fold(const SpecialIn* __restrict__ stage,
                                 const uint64_t* __restrict__ boffk,
                                 const int32_t* __restrict__ bofff, const int ntiles,
                                 const int32_t M, const uint64_t ktot, const int64_t n,
@@ -2594,7 +2645,8 @@ __device__ __forceinline__ int64_t positions_upto(const double v, const int64_t 
 // weight (the reference's IndexError) are marked with j = n.  The fused block
 // then reads its marks and carry and takes a running max -- no search.
 // wt: the folded data were handed over inside the same launch.
-__device__ void wave_tile_expand(const int64_t tile, const TileScan& ts, const int64_t n,
+__device__ void wave_tile_expand(const int64_t b, const int64_t tile, const TileScan& ts,
+                                 const int64_t n,
                                  const uint64_t* __restrict__ boffk,
                                  const int32_t* __restrict__ bofff, const uint64_t kofs,
                                  const int32_t fofs, const SpecialOut* __restrict__ so,
@@ -2603,7 +2655,6 @@ __device__ void wave_tile_expand(const int64_t tile, const TileScan& ts, const i
                                  const PredictConst& pc, const bool wt, const bool store_c = true) {
     const int lane = threadIdx.x & 63;
     auto ld_so = [wt, so](const int32_t m) { return wt ? ld_wt_struct(&so[m]) : so[m]; };
-    const int64_t b = blockIdx.x;
     const uint64_t bk0 = (wt ? ld_wt(&boffk[b]) : boffk[b]) + kofs;   // the tile's global offsets
     const int32_t bf0 = (wt ? ld_wt_i(&bofff[b]) : bofff[b]) + fofs;
     uint64_t kin = bk0 + ts.kex;
@@ -2675,6 +2726,7 @@ __device__ void wave_tile_expand(const int64_t tile, const TileScan& ts, const i
 }
 
 // the last block of pass A: block-total scans, then place + fold
+template <int kC>
 __device__ __forceinline__ void lean_last_block(uint64_t* __restrict__ bk, int32_t* __restrict__ bf,
                                                 uint64_t* __restrict__ boffk,
                                                 int32_t* __restrict__ bofff,
@@ -2690,7 +2742,7 @@ __device__ __forceinline__ void lean_last_block(uint64_t* __restrict__ bk, int32
     __shared__ int32_t shf[kScanThreads / 64 + 1];
     __shared__ int32_t s_off[kFoldTilesLds];
     PROBE_AT(1);
-    block_scan_pair<kScanThreads>(bk, boffk, ktot, bf, bofff, nspec, nblocks, shk, shf,
+    block_scan_pair<kScanThreads, kC>(bk, boffk, ktot, bf, bofff, nspec, nblocks, shk, shf,
                                   nblocks <= kFoldTilesLds ? s_off : nullptr);
     __syncthreads();
     PROBE_AT(2);
@@ -2705,7 +2757,9 @@ __global__ void mark_gen_bump_kernel(int32_t* __restrict__ flags) {
 }
 
 // Pass A (two-launch form): classify and stage every tile; the last block
-// scans the tile totals, places and folds.
+// scans the tile totals, places and folds.  (A grid-stride form over the
+// co-resident blocks measured slower: 50 + 57 against 45 + 45 us at 2^23 --
+// the passes are VALU-bound and the loop raised their VGPRs, 5 waves/SIMD.)
 __global__ __launch_bounds__(kScanThreads) void scan_lean_classify_kernel(
     const double* __restrict__ w_un, const double* __restrict__ s_in, const double np_recip,
     const int64_t n, const double* __restrict__ boff, const double delta,
@@ -2723,14 +2777,15 @@ __global__ __launch_bounds__(kScanThreads) void scan_lean_classify_kernel(
     if (tile < ntiles)
         wave_tile_classify(w_un, *s_in, np_recip, n, tile, boff[tile], delta, ts, ktile, ftile);
     block_tile_offsets(ktile, ftile, kofs, fofs, kblk, fblk);
-    if (tile < ntiles) wave_tile_stage(tile, ts, kofs, fofs, kblk, fblk, stage, bk, bf);
+    if (tile < ntiles) wave_tile_stage(blockIdx.x, tile, ts, kofs, fofs, kblk, fblk, stage, bk, bf);
     else if (threadIdx.x == 0) {
         st_wt(&bk[blockIdx.x], kblk);
         st_wt_i(&bf[blockIdx.x], fblk);
     }
+    PROBE_MAX(12);
     if (!arrive_last(counter)) return;
-    lean_last_block(bk, bf, boffk, bofff, ktot, nspec, (int)gridDim.x, stage, n, spec_out, flags,
-                    w_un, s_in, np_recip, c);
+    lean_last_block<8>(bk, bf, boffk, bofff, ktot, nspec, (int)gridDim.x, stage, n, spec_out,
+                       flags, w_un, s_in, np_recip, c);
 }
 
 // Pass C (two-launch form): the identical classification, then the expansion.
@@ -2743,6 +2798,7 @@ __global__ __launch_bounds__(kScanThreads) void scan_lean_expand_kernel(
     int64_t* __restrict__ mark, int32_t* __restrict__ carry, const int ntiles) {
     if (!force && flags[kFlagResample] != 1) return;
     if (flags[kFlagFallback]) return;
+    if (blockIdx.x == 0) PROBE_AT(5);
     const int64_t tile = (int64_t)blockIdx.x * kTilesPerBlock + (threadIdx.x >> 6);
     const double ofs = mark ? resample_offset(io.ofs[io.ctr[0]], pc.np_recip, seed, (uint32_t)io.ctr[1]) : 0.0;
     const int64_t gen = (int64_t)(uint32_t)flags[kFlagMarkGen] << 32;
@@ -2752,9 +2808,10 @@ __global__ __launch_bounds__(kScanThreads) void scan_lean_expand_kernel(
     if (tile < ntiles)
         wave_tile_classify(w_un, *s_in, np_recip, n, tile, boff[tile], delta, ts, ktile, ftile);
     block_tile_offsets(ktile, ftile, kofs, fofs, kblk, fblk);
+    PROBE_MAX(9);
     if (tile < ntiles)
-        wave_tile_expand(tile, ts, n, boffk, bofff, kofs, fofs, so, c, mark, carry, ofs, gen, pc,
-                         false);
+        wave_tile_expand(blockIdx.x, tile, ts, n, boffk, bofff, kofs, fofs, so, c, mark, carry,
+                         ofs, gen, pc, false, force != 0 || !mark);   // (device-decided: marks only)
 }
 
 // Passes A and C in ONE launch (NP up to the co-resident grid, checked on the
@@ -2786,14 +2843,14 @@ __global__ __launch_bounds__(kScanThreads) void scan_lean_merged_kernel(
     if (active)
         wave_tile_classify(w_un, *s_in, np_recip, n, tile, boff[tile], delta, ts, ktile, ftile);
     block_tile_offsets(ktile, ftile, kofs, fofs, kblk, fblk);
-    if (active) wave_tile_stage(tile, ts, kofs, fofs, kblk, fblk, stage, bk, bf);
+    if (active) wave_tile_stage(blockIdx.x, tile, ts, kofs, fofs, kblk, fblk, stage, bk, bf);
     else if (threadIdx.x == 0) {
         st_wt(&bk[blockIdx.x], kblk);
         st_wt_i(&bf[blockIdx.x], fblk);
     }
     PROBE_MAX(12);
     if (arrive_last(counter)) {
-        lean_last_block(bk, bf, boffk, bofff, ktot, nspec, (int)gridDim.x, stage, n, spec_out,
+        lean_last_block<4>(bk, bf, boffk, bofff, ktot, nspec, (int)gridDim.x, stage, n, spec_out,
                         flags, w_un, s_in, np_recip, c);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
@@ -2820,7 +2877,8 @@ __global__ __launch_bounds__(kScanThreads) void scan_lean_merged_kernel(
     __syncthreads();
     if (blockIdx.x == 0) PROBE_AT(5);
     if (!active || !s_go || ld_wt_i(&flags[kFlagFallback])) return;
-    wave_tile_expand(tile, ts, n, boffk, bofff, kofs, fofs, spec_out, c, mark, carry, ofs, gen, pc,
+    wave_tile_expand(blockIdx.x, tile, ts, n, boffk, bofff, kofs, fofs, spec_out, c, mark, carry,
+                     ofs, gen, pc,
                      true, force != 0);
 }
 

@@ -21,7 +21,8 @@ buf = (C.c_ulonglong * 32)()
 steps = 8
 lm, zs, (vel, omega, dt) = bench.simulate_world(10 * steps)
 ctl = np.tile([vel, omega], (10 * steps, 1))
-pf = DeviceParticleFilter(bench.NP_PER_GPU, lm, dt=dt, motion="velocity", likelihood="logsum", seed=3)
+NP = int(sys.argv[1]) if len(sys.argv) > 1 else bench.NP_PER_GPU
+pf = DeviceParticleFilter(NP, lm, dt=dt, motion="velocity", likelihood="logsum", seed=3)
 pf.load_observations(zs)
 tick_us = 0.01      # wall_clock64: 100 MHz
 for r in range(10):
@@ -34,4 +35,5 @@ for r in range(10):
     d = lambda a, b: (t[b] - t[a]) * tick_us
     print(f"batch {r}: classify {d(0, 12):6.2f}  ticket {d(12, 1):5.2f}  scans {d(1, 2):5.2f}  "
           f"place+fold {d(2, 4):5.2f}  release {d(4, 5):5.2f} | expand: c {d(5, 6):6.2f}  "
-          f"inverse {d(6, 7):5.2f}  | total {d(0, 7):6.2f}  nspecial {out[-1].get('n_special', '?')}")
+          f"inverse {d(6, 7):5.2f}  | total {d(0, 7):6.2f}  nspecial {out[-1].get('n_special', '?')}"
+          + (f" | expand classify {d(5, 9):6.2f} c {d(9, 6):6.2f}" if t[9] else ""))
