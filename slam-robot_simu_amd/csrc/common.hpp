@@ -123,35 +123,9 @@ __device__ __forceinline__ void pair_normals(const uint64_t p, const uint32_t rs
                                (uint32_t)seed, (uint32_t)(seed >> 32));
     uint32_t c0 = (uint32_t)p, c1 = rstep;
     philox2x32(c0, c1, ((uint32_t)seed ^ (uint32_t)(seed >> 32) * 0x85EBCA6Bu) ^ (kStreamPredict2 * 0x27D4EB2Fu));
-#ifdef SLAM_BM_LOOP
-    // one Box-Muller pair at a time (a loop the compiler does not unroll, the
-    // operands and results picked by selects): the three pairs' polynomial
-    // chains do not interleave, which lowers the register peak they set
-    double o0 = 0.0, o1 = 0.0, o2 = 0.0, o3 = 0.0, o4 = 0.0, o5 = 0.0;
-#pragma nounroll
-    for (int j = 0; j < 3; ++j) {
-        const uint32_t a = j == 0 ? r.x : j == 1 ? r.z : c0;
-        const uint32_t b = j == 0 ? r.y : j == 1 ? r.w : c1;
-        double gc, gs;
-        bm_pair(a, b, T, gc, gs);
-        o0 = j == 0 ? gc : o0;
-        o1 = j == 0 ? gs : o1;
-        o2 = j == 1 ? gc : o2;
-        o3 = j == 1 ? gs : o3;
-        o4 = j == 2 ? gc : o4;
-        o5 = j == 2 ? gs : o5;
-    }
-    g[0] = o0;
-    g[1] = o1;
-    g[2] = o2;
-    g[3] = o3;
-    g[4] = o4;
-    g[5] = o5;
-#else
     bm_pair(r.x, r.y, T, g[0], g[1]);
     bm_pair(r.z, r.w, T, g[2], g[3]);
     bm_pair(c0, c1, T, g[4], g[5]);
-#endif
 }
 
 
