@@ -1,25 +1,26 @@
 """Duration distribution of selected kernels in a rocprofv3 kernel trace
 (development tool): per (kernel, grid) the count and quantiles, split into
-the launches below and above `split` x the fastest one (a device-gated
+the launches below and above `--split` x the fastest one (a device-gated
 kernel's no-op launches against its working ones).
 
     python tools/kdist.py prof/bench_kernel_trace.csv scan_lean finalize [--split 3]
 """
+import argparse
 import collections
 import csv
-import sys
 
 import numpy as np
 
-args = [a for a in sys.argv[2:] if not a.startswith("--")]
-split = 3.0
-if "--split" in sys.argv:
-    split = float(sys.argv[sys.argv.index("--split") + 1])
-    args = [a for a in args if a != sys.argv[sys.argv.index("--split") + 1]]
+ap = argparse.ArgumentParser()
+ap.add_argument("trace")
+ap.add_argument("kernels", nargs="*", help="substrings of the kernel names to keep (all if none)")
+ap.add_argument("--split", type=float, default=3.0)
+args = ap.parse_args()
+
 d = collections.defaultdict(list)
-for r in csv.DictReader(open(sys.argv[1])):
+for r in csv.DictReader(open(args.trace)):
     n = r["Kernel_Name"].split("(")[0].replace("void ", "").replace("slam::", "")
-    if args and not any(a in n for a in args):
+    if args.kernels and not any(a in n for a in args.kernels):
         continue
     g = int(r.get("Grid_Size", r.get("Grid_Size_X", 0)) or 0)
     d[(n, g)].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1000)
@@ -35,6 +36,6 @@ def q(v):
 
 for (k, g), v in sorted(d.items()):
     v = np.asarray(v)
-    lo = v[v < split * v.min()]
-    hi = v[v >= split * v.min()]
+    lo = v[v < args.split * v.min()]
+    hi = v[v >= args.split * v.min()]
     print(f"{k} grid={g}\n   low : {q(lo)}\n   high: {q(hi)}")
