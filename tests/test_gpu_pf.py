@@ -41,24 +41,30 @@ def test_resample_indices_bit_exact(slamhip_pf, tag, n):
     assert nspec < n // 4 + 64
 
 
-@pytest.mark.parametrize("n", [(1 << 21) + 12345, 1 << 23, (1 << 24) + 12345])
+@pytest.mark.parametrize("n", [(1 << 20) + 4097, 1500000, (1 << 21) + 12345, 1 << 23,
+                               (1 << 24) + 12345])
 def test_resample_indices_numpy_above_2p20(slamhip_pf, n):
     """particle_filter.py:212-221 above the fixture sizes, bit-exact: the
-    device's exact cumsum in its two-launch form (the last block's coalesced
-    workgroup-total scan in one chunk of rounds, in two, and in five with a
-    partial one and the tile offsets read from global memory rather than LDS)
-    against np.cumsum + searchsorted (the oracle's systematic_indices) on the
-    same weights, offset u x (1/NP) as particle_filter.py:214 forms it."""
+    device's exact cumsum -- its one-launch form past 512 workgroups (the
+    coalesced workgroup-total scan, 515 and 733 totals), then the two-launch
+    form (that scan in one chunk of rounds, in two, and in five with a partial
+    one and the tile offsets read from global memory) -- against np.cumsum +
+    searchsorted (the oracle's systematic_indices) on the same weights, offset
+    u x (1/NP) as particle_filter.py:214 forms it."""
     rs = np.random.RandomState(n % 9973)
     w = heavy_weights(rs, n, zero_frac=0.3)
     w = w / np.sum(w.reshape(1, n))
     u = 0.9 * float(rs.random_sample())
-    with slamhip_pf.DeviceParticleFilter(n, np.zeros((1, 2))) as d:
-        d.set_state(w=w)
-        idx, nspec = d.resample_indices(u)
     ref = po.systematic_indices(w, u * (1.0 / n))
-    np.testing.assert_array_equal(idx, ref)
-    assert 0 < nspec < n // 4
+    # both forms where the one-launch form is available (set_scan_merged
+    # refuses it otherwise), the two-launch form beyond
+    for merged in ((True, False) if n < (1 << 21) else (False,)):
+        with slamhip_pf.DeviceParticleFilter(n, np.zeros((1, 2))) as d:
+            d.set_scan_merged(merged)
+            d.set_state(w=w)
+            idx, nspec = d.resample_indices(u)
+        np.testing.assert_array_equal(idx, ref, err_msg=f"merged={merged}")
+        assert 0 < nspec < n // 4
 
 
 @pytest.mark.parametrize("n", [1, 7, 8, 100, 128, 129, 500, 1000, 8192, 8193, 20000, 100003, 1 << 20])
