@@ -1,8 +1,14 @@
 """Phase timing of the resample passes (development tool): runs the C2
 workload through a probe build (tools/build_variant.sh probe -DSLAM_PROBE) and
-prints, for the last resample step of each batch, the wall-clock phases of
-scan_lean_merged_kernel (classify, ticket, tile-total scans, place + fold,
-release, c stored, inverse map) in microseconds."""
+prints, for the last resample step of each batch, the wall-clock phases of the
+exact cumsum (classify, ticket, tile-total scans, place + fold, release, c
+stored, inverse map) in microseconds: scan_lean_merged_kernel at 2^20, the
+two-launch form (plus its expand pass's own classification) above.
+
+    python tools/scan_probe.py [NP]        (default the bench's 2^20)
+
+The max stamps sample every 32nd workgroup (pf_kernels.inl PROBE_MAX): one
+word taking every workgroup's atomic would serialise them and time itself."""
 import ctypes as C
 import os
 import sys
